@@ -1,0 +1,476 @@
+/*
+ * dts_napi.c -- thin N-API binding of include/dts.h for the Node.js worker.
+ *
+ * The reference server is Node.js (index.js); its worker would spawn the
+ * ffmpeg-static binary (index.js:9).  This addon is the in-process
+ * replacement: the worker builds a graph from the job row
+ * (database.js:73-79) and runs segment frames through libdts.so.  Frame
+ * processing runs in napi_async_work on the libuv pool so the event loop never
+ * blocks; results resolve a Promise.  Written for Node 12 / N-API 8 (plain C,
+ * no node-addon-api), built by gcc against /usr/include/node.
+ */
+#include <node_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dts.h"
+
+#define NAPI_OK(env, call)                                                    \
+    do {                                                                      \
+        if ((call) != napi_ok) {                                              \
+            napi_throw_error((env), NULL, "N-API call failed: " #call);       \
+            return NULL;                                                      \
+        }                                                                     \
+    } while (0)
+
+static napi_value throw_dts(napi_env env, int code, const char *what)
+{
+    char msg[256];
+    snprintf(msg, sizeof msg, "%s: %s (%d)", what, dts_strerror(code), code);
+    char codebuf[32];
+    snprintf(codebuf, sizeof codebuf, "%d", code);
+    napi_throw_error(env, codebuf, msg);
+    return NULL;
+}
+
+static int get_i32(napi_env env, napi_value obj, const char *key, int32_t dflt, int32_t *out)
+{
+    bool has = false;
+    napi_value v;
+    *out = dflt;
+    if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return 0;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok) return -1;
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_undefined || t == napi_null) return 0;
+    return napi_get_value_int32(env, v, out) == napi_ok ? 0 : -1;
+}
+
+static int get_f64(napi_env env, napi_value obj, const char *key, double dflt, double *out)
+{
+    bool has = false;
+    napi_value v;
+    *out = dflt;
+    if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return 0;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok) return -1;
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_undefined || t == napi_null) return 0;
+    return napi_get_value_double(env, v, out) == napi_ok ? 0 : -1;
+}
+
+static void finalize_ctx(napi_env env, void *data, void *hint)
+{
+    (void)env;
+    (void)hint;
+    dts_ctx_destroy((dts_ctx *)data);
+}
+
+static void finalize_graph(napi_env env, void *data, void *hint)
+{
+    (void)env;
+    (void)hint;
+    dts_graph_destroy((dts_graph *)data);
+}
+
+/* ---- version(), deviceCount() ------------------------------------------ */
+static napi_value js_version(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    napi_value s;
+    NAPI_OK(env, napi_create_string_utf8(env, dts_version(), NAPI_AUTO_LENGTH, &s));
+    return s;
+}
+
+static napi_value js_device_count(napi_env env, napi_callback_info info)
+{
+    (void)info;
+    int n = 0;
+    dts_device_count(&n);
+    napi_value v;
+    NAPI_OK(env, napi_create_int32(env, n, &v));
+    return v;
+}
+
+/* ---- createContext(device) -> external ---------------------------------- */
+static napi_value js_create_context(napi_env env, napi_callback_info info)
+{
+    size_t argc = 1;
+    napi_value argv[1];
+    int32_t dev = 0;
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
+    dts_ctx *ctx = NULL;
+    int e = dts_ctx_create(dev, &ctx);
+    if (e) return throw_dts(env, e, "dts_ctx_create");
+    napi_value ext;
+    NAPI_OK(env, napi_create_external(env, ctx, finalize_ctx, NULL, &ext));
+    return ext;
+}
+
+/* ---- createGraph(ctx, spec) -> external --------------------------------- */
+static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
+{
+    memset(s, 0, sizeof *s);
+    napi_value src, outs;
+    if (napi_get_named_property(env, o, "src", &src) != napi_ok) return -1;
+    if (get_i32(env, src, "w", 0, &s->src_w) || get_i32(env, src, "h", 0, &s->src_h) ||
+        get_i32(env, src, "fmt", 0, &s->src_fmt))
+        return -1;
+    if (napi_get_named_property(env, o, "outputs", &outs) != napi_ok) return -1;
+    uint32_t n = 0;
+    if (napi_get_array_length(env, outs, &n) != napi_ok || n < 1 || n > DTS_MAX_OUTPUTS) return -1;
+    s->nout = (int32_t)n;
+    for (uint32_t i = 0; i < n; ++i) {
+        napi_value oi, par;
+        bool has = false;
+        napi_get_element(env, outs, i, &oi);
+        dts_output_spec *os = &s->out[i];
+        if (get_i32(env, oi, "w", 0, &os->w) || get_i32(env, oi, "h", 0, &os->h) ||
+            get_i32(env, oi, "fmt", DTS_FMT_NV12, &os->fmt) || get_i32(env, oi, "method", DTS_SCALE_BICUBIC, &os->method))
+            return -1;
+        os->param[0] = os->param[1] = DTS_PARAM_DEFAULT;
+        napi_has_named_property(env, oi, "param", &has);
+        if (has) {
+            napi_get_named_property(env, oi, "param", &par);
+            uint32_t pn = 0;
+            if (napi_get_array_length(env, par, &pn) == napi_ok)
+                for (uint32_t k = 0; k < pn && k < 2; ++k) {
+                    napi_value pv;
+                    napi_get_element(env, par, k, &pv);
+                    napi_valuetype t;
+                    napi_typeof(env, pv, &t);
+                    if (t == napi_number) napi_get_value_double(env, pv, &os->param[k]);
+                }
+        }
+    }
+    if (get_i32(env, o, "quality", 0, &s->quality) || get_i32(env, o, "qualityOut", 0, &s->quality_out) ||
+        get_i32(env, o, "maxBatch", 0, &s->max_batch))
+        return -1;
+    return 0;
+}
+
+static napi_value js_create_graph(napi_env env, napi_callback_info info)
+{
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 2) return throw_dts(env, DTS_E_INVAL, "createGraph(ctx, spec)");
+    dts_ctx *ctx = NULL;
+    if (napi_get_value_external(env, argv[0], (void **)&ctx) != napi_ok || !ctx)
+        return throw_dts(env, DTS_E_INVAL, "createGraph: ctx");
+    dts_graph_spec s;
+    if (parse_spec(env, argv[1], &s)) return throw_dts(env, DTS_E_INVAL, "createGraph: spec");
+    dts_graph *g = NULL;
+    int e = dts_graph_create(ctx, &s, &g);
+    if (e) return throw_dts(env, e, "dts_graph_create");
+    napi_value ext;
+    NAPI_OK(env, napi_create_external(env, g, finalize_graph, NULL, &ext));
+    return ext;
+}
+
+static napi_value set_num(napi_env env, napi_value obj, const char *k, double v)
+{
+    napi_value n;
+    napi_create_double(env, v, &n);
+    napi_set_named_property(env, obj, k, n);
+    return obj;
+}
+
+static napi_value js_graph_info(napi_env env, napi_callback_info info)
+{
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    dts_graph *g = NULL;
+    if (argc < 1 || napi_get_value_external(env, argv[0], (void **)&g) != napi_ok || !g)
+        return throw_dts(env, DTS_E_INVAL, "graphInfo(graph)");
+    dts_graph_info gi;
+    int e = dts_graph_info_get(g, &gi);
+    if (e) return throw_dts(env, e, "dts_graph_info_get");
+    napi_value o;
+    NAPI_OK(env, napi_create_object(env, &o));
+    set_num(env, o, "srcFrameBytes", (double)gi.src_frame_bytes);
+    set_num(env, o, "algoBytesPerFrame", (double)gi.algo_bytes_per_frame);
+    set_num(env, o, "jobs", gi.njobs);
+    set_num(env, o, "ldsBytes", gi.lds_bytes);
+    napi_value arr;
+    napi_create_array(env, &arr);
+    for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) {
+        napi_value n;
+        napi_create_double(env, (double)gi.out_frame_bytes[k], &n);
+        napi_set_element(env, arr, (uint32_t)k, n);
+    }
+    napi_set_named_property(env, o, "outFrameBytes", arr);
+    return o;
+}
+
+/* ---- frames ------------------------------------------------------------- */
+/* {data: [Buffer, Buffer, Buffer|null], pitch: [n, n, n]} */
+static int parse_frame(napi_env env, napi_value o, dts_frame *f)
+{
+    napi_value data, pitch;
+    memset(f, 0, sizeof *f);
+    if (napi_get_named_property(env, o, "data", &data) != napi_ok ||
+        napi_get_named_property(env, o, "pitch", &pitch) != napi_ok)
+        return -1;
+    for (uint32_t p = 0; p < 3; ++p) {
+        napi_value b, pv;
+        bool isbuf = false;
+        if (napi_get_element(env, data, p, &b) != napi_ok) return -1;
+        napi_is_buffer(env, b, &isbuf);
+        if (isbuf) {
+            size_t len = 0;
+            if (napi_get_buffer_info(env, b, &f->data[p], &len) != napi_ok) return -1;
+        } else {
+            f->data[p] = NULL;
+        }
+        if (napi_get_element(env, pitch, p, &pv) != napi_ok) return -1;
+        int64_t pi = 0;
+        napi_valuetype t;
+        napi_typeof(env, pv, &t);
+        if (t == napi_number) napi_get_value_int64(env, pv, &pi);
+        f->pitch[p] = pi;
+    }
+    return 0;
+}
+
+static int parse_frames(napi_env env, napi_value arr, dts_frame **out, uint32_t *n)
+{
+    if (napi_get_array_length(env, arr, n) != napi_ok) return -1;
+    *out = (dts_frame *)calloc(*n ? *n : 1, sizeof(dts_frame));
+    if (!*out) return -1;
+    for (uint32_t i = 0; i < *n; ++i) {
+        napi_value fo;
+        napi_get_element(env, arr, i, &fo);
+        if (parse_frame(env, fo, &(*out)[i])) return -1;
+    }
+    return 0;
+}
+
+/* ---- run(graph, src[], dst[], qref[]|null) -> Promise<qstat[]|null> ---- */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref keep[4];            /* graph, src, dst, qref arrays kept alive */
+    dts_graph *g;
+    dts_frame *src, *dst, *qref;
+    dts_qstat *q;
+    int n, status;
+} run_job;
+
+static void run_execute(napi_env env, void *data)
+{
+    (void)env;
+    run_job *j = (run_job *)data;
+    j->status = dts_graph_submit(j->g, j->src, j->n, j->dst, j->qref, j->q);
+    int w = dts_graph_wait(j->g);
+    if (!j->status) j->status = w;
+}
+
+static napi_value qstat_obj(napi_env env, const dts_qstat *q)
+{
+    napi_value o, a;
+    napi_create_object(env, &o);
+    const char *comp[3] = {"y", "u", "v"};
+    napi_create_object(env, &a);
+    for (int c = 0; c < 3; ++c) set_num(env, a, comp[c], (double)q->sse[c]);
+    napi_set_named_property(env, o, "sse", a);
+    napi_create_object(env, &a);
+    for (int c = 0; c < 3; ++c) set_num(env, a, comp[c], q->psnr[c]);
+    napi_set_named_property(env, o, "psnr", a);
+    napi_create_object(env, &a);
+    for (int c = 0; c < 3; ++c) set_num(env, a, comp[c], q->ssim[c]);
+    napi_set_named_property(env, o, "ssim", a);
+    set_num(env, o, "mseAvg", q->mse_avg);
+    set_num(env, o, "psnrAvg", q->psnr_avg);
+    set_num(env, o, "ssimAll", q->ssim_all);
+    set_num(env, o, "ssimDb", q->ssim_db);
+    return o;
+}
+
+static void run_complete(napi_env env, napi_status st, void *data)
+{
+    run_job *j = (run_job *)data;
+    if (st != napi_ok || j->status) {
+        napi_value err, msg, code;
+        char buf[160], cb[32];
+        int e = j->status ? j->status : DTS_E_INVAL;
+        snprintf(buf, sizeof buf, "dts run: %s (%d)", dts_strerror(e), e);
+        snprintf(cb, sizeof cb, "%d", e);
+        napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &msg);
+        napi_create_string_utf8(env, cb, NAPI_AUTO_LENGTH, &code);
+        napi_create_error(env, code, msg, &err);
+        napi_reject_deferred(env, j->deferred, err);
+    } else {
+        napi_value res;
+        if (j->q) {
+            napi_create_array_with_length(env, (size_t)j->n, &res);
+            for (int i = 0; i < j->n; ++i) napi_set_element(env, res, (uint32_t)i, qstat_obj(env, &j->q[i]));
+        } else {
+            napi_get_null(env, &res);
+        }
+        napi_resolve_deferred(env, j->deferred, res);
+    }
+    for (int k = 0; k < 4; ++k)
+        if (j->keep[k]) napi_delete_reference(env, j->keep[k]);
+    napi_delete_async_work(env, j->work);
+    free(j->src);
+    free(j->dst);
+    free(j->qref);
+    free(j->q);
+    free(j);
+}
+
+static napi_value js_run(napi_env env, napi_callback_info info)
+{
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 3) return throw_dts(env, DTS_E_INVAL, "run(graph, src, dst[, qref])");
+    run_job *j = (run_job *)calloc(1, sizeof(run_job));
+    if (!j) return throw_dts(env, DTS_E_NOMEM, "run");
+    if (napi_get_value_external(env, argv[0], (void **)&j->g) != napi_ok || !j->g) {
+        free(j);
+        return throw_dts(env, DTS_E_INVAL, "run: graph");
+    }
+    uint32_t ns = 0, nd = 0, nq = 0;
+    if (parse_frames(env, argv[1], &j->src, &ns) || parse_frames(env, argv[2], &j->dst, &nd)) {
+        free(j->src);
+        free(j->dst);
+        free(j);
+        return throw_dts(env, DTS_E_INVAL, "run: frames");
+    }
+    j->n = (int)ns;
+    napi_valuetype qt = napi_undefined;
+    if (argc >= 4) napi_typeof(env, argv[3], &qt);
+    if (qt == napi_object) {
+        if (parse_frames(env, argv[3], &j->qref, &nq) || nq != ns) {
+            free(j->src);
+            free(j->dst);
+            free(j->qref);
+            free(j);
+            return throw_dts(env, DTS_E_INVAL, "run: qref frames");
+        }
+        j->q = (dts_qstat *)calloc(ns ? ns : 1, sizeof(dts_qstat));
+    }
+    for (int k = 0; k < 4 && (size_t)k < argc; ++k) {
+        napi_valuetype t;
+        napi_typeof(env, argv[k], &t);
+        if (t == napi_object || t == napi_external) napi_create_reference(env, argv[k], 1, &j->keep[k]);
+    }
+    napi_value promise, name;
+    NAPI_OK(env, napi_create_promise(env, &j->deferred, &promise));
+    napi_create_string_utf8(env, "dts_run", NAPI_AUTO_LENGTH, &name);
+    NAPI_OK(env, napi_create_async_work(env, NULL, name, run_execute, run_complete, j, &j->work));
+    NAPI_OK(env, napi_queue_async_work(env, j->work));
+    (void)nd;
+    return promise;
+}
+
+/* ---- synthFrame(w, h, fmt, pattern, seed, index, frame) ---------------- */
+static napi_value js_synth_frame(napi_env env, napi_callback_info info)
+{
+    size_t argc = 7;
+    napi_value argv[7];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 7) return throw_dts(env, DTS_E_INVAL, "synthFrame(w, h, fmt, pattern, seed, index, frame)");
+    int32_t w, h, fmt, pat;
+    uint32_t seed;
+    int64_t idx;
+    napi_get_value_int32(env, argv[0], &w);
+    napi_get_value_int32(env, argv[1], &h);
+    napi_get_value_int32(env, argv[2], &fmt);
+    napi_get_value_int32(env, argv[3], &pat);
+    napi_get_value_uint32(env, argv[4], &seed);
+    napi_get_value_int64(env, argv[5], &idx);
+    dts_frame f;
+    if (parse_frame(env, argv[6], &f)) return throw_dts(env, DTS_E_INVAL, "synthFrame: frame");
+    int e = dts_synth_host(w, h, fmt, pat, seed, idx, &f);
+    if (e) return throw_dts(env, e, "dts_synth_host");
+    napi_value u;
+    napi_get_undefined(env, &u);
+    return u;
+}
+
+/* ---- frameLayout(w, h, fmt) -> {pitch, rows, bytes} --------------------- */
+static napi_value js_frame_layout(napi_env env, napi_callback_info info)
+{
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t w = 0, h = 0, fmt = 0;
+    if (argc < 3) return throw_dts(env, DTS_E_INVAL, "frameLayout(w, h, fmt)");
+    napi_get_value_int32(env, argv[0], &w);
+    napi_get_value_int32(env, argv[1], &h);
+    napi_get_value_int32(env, argv[2], &fmt);
+    int64_t pitch[3], rows[3], bytes = 0;
+    int e = dts_frame_layout(w, h, fmt, pitch, rows, &bytes);
+    if (e) return throw_dts(env, e, "dts_frame_layout");
+    napi_value o, pa, ra;
+    napi_create_object(env, &o);
+    napi_create_array(env, &pa);
+    napi_create_array(env, &ra);
+    for (uint32_t p = 0; p < 3; ++p) {
+        napi_value a, b;
+        napi_create_double(env, (double)pitch[p], &a);
+        napi_create_double(env, (double)rows[p], &b);
+        napi_set_element(env, pa, p, a);
+        napi_set_element(env, ra, p, b);
+    }
+    napi_set_named_property(env, o, "pitch", pa);
+    napi_set_named_property(env, o, "rows", ra);
+    set_num(env, o, "bytes", (double)bytes);
+    return o;
+}
+
+/* ---- fpsMap(nbIn, inNum, inDen, outNum, outDen) -> number[] ------------- */
+static napi_value js_fps_map(napi_env env, napi_callback_info info)
+{
+    size_t argc = 5;
+    napi_value argv[5];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 5) return throw_dts(env, DTS_E_INVAL, "fpsMap(nbIn, inNum, inDen, outNum, outDen)");
+    int64_t nb;
+    int32_t a, b, c, d;
+    napi_get_value_int64(env, argv[0], &nb);
+    napi_get_value_int32(env, argv[1], &a);
+    napi_get_value_int32(env, argv[2], &b);
+    napi_get_value_int32(env, argv[3], &c);
+    napi_get_value_int32(env, argv[4], &d);
+    int64_t n = dts_fps_map(nb, a, b, c, d, NULL, 0);
+    if (n < 0) return throw_dts(env, (int)n, "dts_fps_map");
+    int64_t *idx = (int64_t *)calloc((size_t)(n ? n : 1), sizeof(int64_t));
+    if (!idx) return throw_dts(env, DTS_E_NOMEM, "fpsMap");
+    dts_fps_map(nb, a, b, c, d, idx, n);
+    napi_value arr;
+    napi_create_array_with_length(env, (size_t)n, &arr);
+    for (int64_t i = 0; i < n; ++i) {
+        napi_value v;
+        napi_create_double(env, (double)idx[i], &v);
+        napi_set_element(env, arr, (uint32_t)i, v);
+    }
+    free(idx);
+    return arr;
+}
+
+static napi_value init(napi_env env, napi_value exports)
+{
+    napi_property_descriptor props[] = {
+        {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
+        {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_default, NULL},
+        {"createContext", NULL, js_create_context, NULL, NULL, NULL, napi_default, NULL},
+        {"createGraph", NULL, js_create_graph, NULL, NULL, NULL, napi_default, NULL},
+        {"graphInfo", NULL, js_graph_info, NULL, NULL, NULL, napi_default, NULL},
+        {"run", NULL, js_run, NULL, NULL, NULL, napi_default, NULL},
+        {"synthFrame", NULL, js_synth_frame, NULL, NULL, NULL, napi_default, NULL},
+        {"frameLayout", NULL, js_frame_layout, NULL, NULL, NULL, napi_default, NULL},
+        {"fpsMap", NULL, js_fps_map, NULL, NULL, NULL, napi_default, NULL},
+    };
+    napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+    return exports;
+}
+
+NAPI_MODULE(dts_napi, init)

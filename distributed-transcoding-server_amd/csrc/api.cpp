@@ -1,0 +1,916 @@
+// api.cpp -- C-ABI of libdts (include/dts.h).
+//
+// Host side of the MI355X worker: builds libswscale-identical filter tables
+// once per graph (vf_scale config_props -> sws_init_context equivalent), owns
+// the device tables / batch buffers / pinned staging rings, and enqueues the
+// ladder + quality kernels.  Replaces the ffmpeg child process the reference
+// would spawn from the path resolved at /root/reference/index.js:9.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "dts_internal.h"
+#include "filters.h"
+
+using namespace dts;
+
+struct dts_ctx {
+    int device = 0;
+    int last_hip = 0;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    // quality scratch (partials), grown on demand
+    void *qscratch = nullptr;
+    size_t qscratch_bytes = 0;
+};
+
+namespace {
+
+constexpr int kSwsAccurateRnd = 0x40000;
+constexpr int kSwsBitexact = 0x80000;
+
+#define HIPCHK(ctx, expr)                                  \
+    do {                                                   \
+        hipError_t e_ = (expr);                            \
+        if (e_ != hipSuccess) {                            \
+            (ctx)->last_hip = (int)e_;                     \
+            return DTS_E_HIP;                              \
+        }                                                  \
+    } while (0)
+
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+bool fmt_in_ok(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12 || f == DTS_FMT_P010LE; }
+bool fmt_out_ok(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12; }
+bool method_ok(int m)
+{
+    switch (m) {
+    case DTS_SCALE_BILINEAR: case DTS_SCALE_BICUBIC: case DTS_SCALE_X: case DTS_SCALE_POINT:
+    case DTS_SCALE_AREA: case DTS_SCALE_GAUSS: case DTS_SCALE_SINC: case DTS_SCALE_LANCZOS:
+        return true;
+    default:
+        return false;
+    }
+}
+
+// plane geometry of a frame: row bytes and rows per plane (plane 2 unused for semi-planar)
+void plane_geom(int w, int h, int fmt, int64_t rowb[3], int64_t rows[3])
+{
+    const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+    rows[0] = h;
+    rows[1] = ch;
+    switch (fmt) {
+    case DTS_FMT_YUV420P:
+        rowb[0] = w; rowb[1] = cw; rowb[2] = cw; rows[2] = ch;
+        break;
+    case DTS_FMT_NV12:
+        rowb[0] = w; rowb[1] = 2 * cw; rowb[2] = 0; rows[2] = 0;
+        break;
+    default: // P010LE
+        rowb[0] = 2 * w; rowb[1] = 4 * cw; rowb[2] = 0; rows[2] = 0;
+        break;
+    }
+}
+
+// device-side layout we use for our own batch buffers
+struct DevLayout {
+    int64_t pitch[3] = {0, 0, 0}, off[3] = {0, 0, 0}, rows[3] = {0, 0, 0}, rowb[3] = {0, 0, 0};
+    int64_t fstride = 0;
+    void init(int w, int h, int fmt)
+    {
+        plane_geom(w, h, fmt, rowb, rows);
+        int64_t o = 0;
+        for (int p = 0; p < 3; ++p) {
+            pitch[p] = rowb[p] ? align_up(rowb[p] + 16, 256) : 0;
+            off[p] = o;
+            o += align_up(pitch[p] * rows[p], 4096);
+        }
+        fstride = o;
+    }
+    DevPlanes planes(uint8_t *base) const
+    {
+        DevPlanes d{};
+        for (int p = 0; p < 3; ++p) {
+            d.data[p] = (uint64_t)(base + off[p]);
+            d.pitch[p] = pitch[p] ? pitch[p] : pitch[1];
+        }
+        if (!rowb[2]) d.data[2] = d.data[1];
+        d.fstride = fstride;
+        return d;
+    }
+};
+
+int64_t packed_bytes(int w, int h, int fmt)
+{
+    int64_t rowb[3], rows[3];
+    plane_geom(w, h, fmt, rowb, rows);
+    return rowb[0] * rows[0] + rowb[1] * rows[1] + rowb[2] * rows[2];
+}
+
+} // namespace
+
+struct dts_graph {
+    dts_ctx *ctx = nullptr;
+    dts_graph_spec spec{};
+    dts_graph_info info{};
+    int src_kind = 0;
+    int ndmax = 0;
+    int ring_pairs = 16;
+    int stage_bytes = 0;
+    int lds_bytes = 0;
+    std::vector<Job> jobs;
+    std::vector<RungKind> rk;             // host copy with device pointers
+    void *dev_tables = nullptr;           // all per-graph device tables
+    Job *dev_jobs = nullptr;
+    RungKind *dev_rk = nullptr;
+
+    // host-path batch resources (2 slots)
+    int batch = 32;
+    DevLayout lay_src, lay_out[DTS_MAX_OUTPUTS], lay_q;
+    uint8_t *dev_src[2] = {nullptr, nullptr}, *dev_out[2][DTS_MAX_OUTPUTS] = {}, *dev_q[2] = {nullptr, nullptr};
+    dts_qraw *dev_qraw[2] = {nullptr, nullptr};
+    uint8_t *pin_in[2] = {nullptr, nullptr}, *pin_out[2] = {nullptr, nullptr};
+    dts_qraw *pin_qraw[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    int64_t pin_in_bytes = 0, pin_out_bytes = 0;
+    // pending host submit
+    bool pending = false;
+    const dts_frame *p_dst = nullptr;
+    dts_qstat *p_q = nullptr;
+    int p_chunk_first[2] = {-1, -1}, p_chunk_n[2] = {0, 0};
+};
+
+// ---------------------------------------------------------------------------
+// graph construction
+// ---------------------------------------------------------------------------
+namespace {
+
+struct KindTables {
+    HTable h;
+    VTable v;
+    std::vector<int32_t> vlim;
+    int srcW, srcH, dstW, dstH;
+    int sws_h, sws_v;
+};
+
+int build_kind(const dts_graph_spec &s, int k, int kind, KindTables &kt)
+{
+    const dts_output_spec &o = s.out[k];
+    const int flags = o.method | kSwsAccurateRnd | kSwsBitexact;
+    kt.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
+    kt.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
+    kt.dstW = kind ? (o.w + 1) >> 1 : o.w;
+    kt.dstH = kind ? (o.h + 1) >> 1 : o.h;
+    // utils.c get_local_pos: luma (0, 0); 4:2:0 chroma default -513 -> centred
+    const int pos = kind ? sws_local_pos(1, -513) : sws_local_pos(0, 0);
+    SwsFilter fh, fv;
+    int e = sws_build_filter(kt.srcW, kt.dstW, 1 << 14, 4, flags, o.param, pos, pos, fh);
+    if (e) return e;
+    e = sws_build_filter(kt.srcH, kt.dstH, 1 << 12, 2, flags, o.param, pos, pos, fv);
+    if (e) return e;
+    kt.sws_h = fh.size;
+    kt.sws_v = fv.size;
+    e = s.src_fmt == DTS_FMT_P010LE ? pack_h_p010(fh, kt.dstW, kt.h) : pack_h_u8(fh, kt.dstW, kt.h);
+    if (e) return e;
+    return pack_v(fv, kt.dstH, kt.v);
+}
+
+// strips of one (rung, kind): window of source samples each strip stages
+void make_jobs(const KindTables &kt, int rung, int kind, bool p010, std::vector<Job> &jobs, int &max_stage)
+{
+    const int maxcols = kind ? kChromaCols : kLumaCols;
+    const int nplanes = kind ? 2 : 1;
+    const int bps = p010 ? 2 : 1;                    // staged bytes per sample
+    const int tap_bytes = p010 ? 4 : 4;              // bytes per coefficient dword
+    int cols = maxcols;
+    for (;;) {
+        bool fits = true;
+        std::vector<Job> js;
+        for (int x0 = 0; x0 < kt.dstW; x0 += cols) {
+            const int n = std::min(cols, kt.dstW - x0);
+            int lo = kt.h.pos[x0], hi = 0;
+            for (int i = x0; i < x0 + n; ++i) {
+                lo = std::min(lo, kt.h.pos[i]);
+                hi = std::max(hi, kt.h.pos[i] * bps + kt.h.nd * tap_bytes);
+            }
+            const int sx0 = (lo * bps) / 16 * 16 / bps;  // 16-byte aligned start (samples)
+            const int swb = (int)align_up(hi - sx0 * bps, 16);
+            const int nload = kBlkRows * (swb / 16) * nplanes;
+            if (nload > kMaxLoads * kThreads) {
+                fits = false;
+                break;
+            }
+            Job j{};
+            j.rung = (int16_t)rung;
+            j.kind = (int16_t)kind;
+            j.x0 = x0;
+            j.ncols = n;
+            j.sx0 = sx0;
+            j.swb = swb;
+            j.nload = nload;
+            js.push_back(j);
+            max_stage = std::max(max_stage, nplanes * kBlkRows * swb);
+        }
+        if (fits || cols <= 8) {
+            jobs.insert(jobs.end(), js.begin(), js.end());
+            return;
+        }
+        cols /= 2;
+    }
+}
+
+template <class T>
+size_t push_blob(std::vector<uint8_t> &blob, const std::vector<T> &v)
+{
+    const size_t off = align_up((int64_t)blob.size(), 256);
+    blob.resize(off + v.size() * sizeof(T));
+    if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *dts_version(void) { return "dts-mi355x 0.1 (gfx950; abi 1)"; }
+
+const char *dts_strerror(int err)
+{
+    switch (err) {
+    case DTS_OK: return "success";
+    case DTS_E_INVAL: return "invalid argument";
+    case DTS_E_NOMEM: return "out of memory";
+    case DTS_E_RANGE: return "filter does not fit the GPU tables";
+    case DTS_E_UNSUPPORTED: return "unsupported format or method";
+    case DTS_E_BUSY: return "a submit is still pending";
+    case DTS_E_NODEV: return "no HIP device";
+    case DTS_E_HIP: return "HIP runtime error";
+    default: return "unknown error";
+    }
+}
+
+int dts_device_count(int *count)
+{
+    if (!count) return DTS_E_INVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return DTS_OK;
+}
+
+int dts_ctx_create(int device, dts_ctx **out)
+{
+    if (!out) return DTS_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DTS_E_NODEV;
+    if (device < 0 || device >= n) return DTS_E_INVAL;
+    dts_ctx *c = new (std::nothrow) dts_ctx();
+    if (!c) return DTS_E_NOMEM;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream[1], hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DTS_E_HIP;
+    }
+    *out = c;
+    return DTS_OK;
+}
+
+void dts_ctx_destroy(dts_ctx *c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    for (auto &s : c->stream)
+        if (s) hipStreamDestroy(s);
+    if (c->qscratch) hipFree(c->qscratch);
+    delete c;
+}
+
+int dts_ctx_last_hip_error(const dts_ctx *c) { return c ? c->last_hip : 0; }
+
+int dts_frame_layout(int w, int h, int fmt, int64_t pitch[3], int64_t rows[3], int64_t *packed)
+{
+    if (w <= 0 || h <= 0 || !fmt_in_ok(fmt) || !pitch || !rows) return DTS_E_INVAL;
+    plane_geom(w, h, fmt, pitch, rows);
+    if (packed) *packed = pitch[0] * rows[0] + pitch[1] * rows[1] + pitch[2] * rows[2];
+    return DTS_OK;
+}
+
+void dts_graph_destroy(dts_graph *g);
+
+int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
+{
+    if (!ctx || !spec || !out) return DTS_E_INVAL;
+    *out = nullptr;
+    const dts_graph_spec &s = *spec;
+    if (s.src_w < 4 || s.src_h < 4 || s.src_w > 16384 || s.src_h > 16384 || !fmt_in_ok(s.src_fmt)) return DTS_E_INVAL;
+    if (s.nout < 1 || s.nout > DTS_MAX_OUTPUTS) return DTS_E_INVAL;
+    for (int k = 0; k < s.nout; ++k) {
+        const dts_output_spec &o = s.out[k];
+        if (o.w < 2 || o.h < 2 || o.w > 16384 || o.h > 16384) return DTS_E_INVAL;
+        if (!fmt_out_ok(o.fmt)) return DTS_E_UNSUPPORTED;
+        if (!method_ok(o.method)) return DTS_E_UNSUPPORTED;
+    }
+    if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
+    if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
+    try {
+        dts_graph *g = new dts_graph();
+        g->ctx = ctx;
+        g->spec = s;
+        g->batch = s.max_batch > 0 ? s.max_batch : 32;
+        g->src_kind = s.src_fmt == DTS_FMT_P010LE ? kSrcP010 : (s.src_fmt == DTS_FMT_NV12 ? kSrcNV12 : kSrcPlanar8);
+        const bool p010 = s.src_fmt == DTS_FMT_P010LE;
+
+        std::vector<KindTables> kts((size_t)s.nout * 2);
+        int ndmax_need = 1;
+        for (int k = 0; k < s.nout; ++k)
+            for (int kind = 0; kind < 2; ++kind) {
+                KindTables &kt = kts[(size_t)k * 2 + kind];
+                const int e = build_kind(s, k, kind, kt);
+                if (e) {
+                    delete g;
+                    return e;
+                }
+                ndmax_need = std::max(ndmax_need, kt.h.nd);
+                g->info.h_taps[k][kind] = kt.h.span;
+                g->info.v_taps[k][kind] = kt.v.span;
+                g->info.sws_h_size[k][kind] = kt.sws_h;
+                g->info.sws_v_size[k][kind] = kt.sws_v;
+            }
+        g->ndmax = ladder_ndmax_for(ndmax_need);
+        if (!g->ndmax) {
+            delete g;
+            return DTS_E_RANGE;
+        }
+        // ring size: smallest power of two holding every V window
+        int rp = 8;
+        for (; rp <= 256; rp *= 2) {
+            bool ok = true;
+            for (auto &kt : kts) ok = ok && plan_vlimits(kt.v, kt.srcH, kt.dstH, rp, kt.vlim);
+            if (ok) break;
+        }
+        if (rp > 256) {
+            delete g;
+            return DTS_E_RANGE;
+        }
+        g->ring_pairs = rp;
+        int max_stage = 0;
+        for (int k = 0; k < s.nout; ++k)
+            for (int kind = 0; kind < 2; ++kind) make_jobs(kts[(size_t)k * 2 + kind], k, kind, p010, g->jobs, max_stage);
+        // heaviest strips first (H taps x columns x source rows)
+        std::stable_sort(g->jobs.begin(), g->jobs.end(), [&](const Job &a, const Job &b) {
+            const KindTables &ka = kts[(size_t)a.rung * 2 + a.kind], &kb = kts[(size_t)b.rung * 2 + b.kind];
+            const int64_t ca = (int64_t)ka.h.nd * a.ncols * ka.srcH * (a.kind ? 2 : 1);
+            const int64_t cb = (int64_t)kb.h.nd * b.ncols * kb.srcH * (b.kind ? 2 : 1);
+            return ca > cb;
+        });
+        g->stage_bytes = (int)align_up(max_stage, 16);
+        g->lds_bytes = 2 * g->stage_bytes + rp * kLumaCols * 4;
+        if (g->lds_bytes > 160 * 1024) {
+            delete g;
+            return DTS_E_RANGE;
+        }
+
+        // upload tables
+        std::vector<uint8_t> blob;
+        struct Offs { size_t hpos, hbias, hch, hcl, vpos, vcoef, vlim; };
+        std::vector<Offs> offs(kts.size());
+        for (size_t i = 0; i < kts.size(); ++i) {
+            KindTables &kt = kts[i];
+            offs[i].hpos = push_blob(blob, kt.h.pos);
+            offs[i].hbias = push_blob(blob, kt.h.bias);
+            offs[i].hch = push_blob(blob, kt.h.hi);
+            offs[i].hcl = push_blob(blob, kt.h.lo);
+            offs[i].vpos = push_blob(blob, kt.v.pos);
+            offs[i].vcoef = push_blob(blob, kt.v.coef);
+            offs[i].vlim = push_blob(blob, kt.vlim);
+        }
+        const size_t jobs_off = push_blob(blob, g->jobs);
+        const size_t rk_off = align_up((int64_t)blob.size(), 256);
+        blob.resize(rk_off + kts.size() * sizeof(RungKind));
+        hipSetDevice(ctx->device);
+        if (hipMalloc(&g->dev_tables, blob.size()) != hipSuccess) {
+            ctx->last_hip = (int)hipGetLastError();
+            delete g;
+            return DTS_E_HIP;
+        }
+        uint8_t *base = static_cast<uint8_t *>(g->dev_tables);
+        g->rk.resize(kts.size());
+        for (size_t i = 0; i < kts.size(); ++i) {
+            KindTables &kt = kts[i];
+            RungKind &r = g->rk[i];
+            r.dstW = kt.dstW;
+            r.dstH = kt.dstH;
+            r.nd = kt.h.nd;
+            r.nv = kt.v.nv;
+            r.nblocks = (int)kt.vlim.size();
+            r.hpos = reinterpret_cast<const int32_t *>(base + offs[i].hpos);
+            r.hbias = reinterpret_cast<const int32_t *>(base + offs[i].hbias);
+            r.hch = reinterpret_cast<const uint32_t *>(base + offs[i].hch);
+            r.hcl = reinterpret_cast<const uint32_t *>(base + offs[i].hcl);
+            r.vpos = reinterpret_cast<const int32_t *>(base + offs[i].vpos);
+            r.vcoef = reinterpret_cast<const uint32_t *>(base + offs[i].vcoef);
+            r.vlim = reinterpret_cast<const int32_t *>(base + offs[i].vlim);
+        }
+        std::memcpy(blob.data() + rk_off, g->rk.data(), kts.size() * sizeof(RungKind));
+        g->dev_jobs = reinterpret_cast<Job *>(base + jobs_off);
+        g->dev_rk = reinterpret_cast<RungKind *>(base + rk_off);
+        if (hipMemcpy(g->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            ctx->last_hip = (int)hipGetLastError();
+            dts_graph_destroy(g);
+            return DTS_E_HIP;
+        }
+
+        // info
+        g->info.src_frame_bytes = packed_bytes(s.src_w, s.src_h, s.src_fmt);
+        int64_t algo = g->info.src_frame_bytes;
+        for (int k = 0; k < s.nout; ++k) {
+            g->info.out_frame_bytes[k] = packed_bytes(s.out[k].w, s.out[k].h, s.out[k].fmt);
+            algo += g->info.out_frame_bytes[k];
+        }
+        if (s.quality) algo += g->info.out_frame_bytes[s.quality_out];
+        g->info.algo_bytes_per_frame = algo;
+        g->info.njobs = (int)g->jobs.size();
+        g->info.lds_bytes = g->lds_bytes;
+
+        g->lay_src.init(s.src_w, s.src_h, s.src_fmt);
+        for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt);
+        if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt);
+        *out = g;
+        return DTS_OK;
+    } catch (const std::bad_alloc &) {
+        return DTS_E_NOMEM;
+    } catch (...) {
+        return DTS_E_INVAL;
+    }
+}
+
+void dts_graph_destroy(dts_graph *g)
+{
+    if (!g) return;
+    hipSetDevice(g->ctx->device);
+    for (int sl = 0; sl < 2; ++sl) {
+        if (g->done[sl]) hipEventSynchronize(g->done[sl]);
+    }
+    for (int sl = 0; sl < 2; ++sl) {
+        if (g->dev_src[sl]) hipFree(g->dev_src[sl]);
+        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
+            if (g->dev_out[sl][k]) hipFree(g->dev_out[sl][k]);
+        if (g->dev_q[sl]) hipFree(g->dev_q[sl]);
+        if (g->dev_qraw[sl]) hipFree(g->dev_qraw[sl]);
+        if (g->pin_in[sl]) hipHostFree(g->pin_in[sl]);
+        if (g->pin_out[sl]) hipHostFree(g->pin_out[sl]);
+        if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
+        if (g->done[sl]) hipEventDestroy(g->done[sl]);
+    }
+    if (g->dev_tables) hipFree(g->dev_tables);
+    delete g;
+}
+
+int dts_graph_info_get(const dts_graph *g, dts_graph_info *info)
+{
+    if (!g || !info) return DTS_E_INVAL;
+    *info = g->info;
+    return DTS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device-resident path
+// ---------------------------------------------------------------------------
+static bool planes_ok(const dts_dev_frames &f, int w, int h, int fmt, int align)
+{
+    int64_t rowb[3], rows[3];
+    plane_geom(w, h, fmt, rowb, rows);
+    for (int p = 0; p < 3; ++p) {
+        if (!rowb[p]) continue;
+        if (!f.data[p] || f.pitch[p] < rowb[p]) return false;
+        if (((uintptr_t)f.data[p] % align) || (f.pitch[p] % align)) return false;
+    }
+    return (f.frame_stride % align) == 0;
+}
+
+static DevPlanes to_dev(const dts_dev_frames &f, int fmt)
+{
+    DevPlanes d{};
+    for (int p = 0; p < 3; ++p) {
+        d.data[p] = (uint64_t)f.data[p];
+        d.pitch[p] = f.pitch[p];
+    }
+    if (fmt != DTS_FMT_YUV420P) {
+        d.data[2] = d.data[1];
+        d.pitch[2] = d.pitch[1];
+    }
+    d.fstride = f.frame_stride;
+    return d;
+}
+
+static int ensure_qscratch(dts_ctx *ctx, size_t bytes)
+{
+    if (ctx->qscratch_bytes >= bytes) return DTS_OK;
+    if (ctx->qscratch) {
+        hipDeviceSynchronize();
+        hipFree(ctx->qscratch);
+        ctx->qscratch = nullptr;
+        ctx->qscratch_bytes = 0;
+    }
+    HIPCHK(ctx, hipMalloc(&ctx->qscratch, bytes));
+    ctx->qscratch_bytes = bytes;
+    return DTS_OK;
+}
+
+static int quality_enqueue(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_frames &a, const dts_dev_frames &b,
+                           int n, dts_qraw *qraw, hipStream_t st)
+{
+    QualityParams q{};
+    q.a = to_dev(a, fmt);
+    q.b = to_dev(b, fmt);
+    q.pw[0] = w;
+    q.ph[0] = h;
+    q.pw[1] = q.pw[2] = (w + 1) >> 1;
+    q.ph[1] = q.ph[2] = (h + 1) >> 1;
+    int total = 0;
+    for (int p = 0; p < 3; ++p) {
+        q.tiles_x[p] = (q.pw[p] + 4 * kQTileBX - 1) / (4 * kQTileBX);
+        q.tiles_y[p] = (q.ph[p] + 4 * kQTileBY - 1) / (4 * kQTileBY);
+        q.tile_base[p] = total;
+        total += q.tiles_x[p] * q.tiles_y[p];
+    }
+    q.tile_base[3] = total;
+    q.interleaved = fmt == DTS_FMT_NV12;
+    q.nframes = n;
+    const size_t need = (size_t)n * total * (sizeof(double) + sizeof(unsigned long long));
+    int e = ensure_qscratch(ctx, need);
+    if (e) return e;
+    q.partial_ssim = static_cast<double *>(ctx->qscratch);
+    q.partial_sse = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(ctx->qscratch) +
+                                                          (size_t)n * total * sizeof(double));
+    q.out = qraw;
+    HIPCHK(ctx, launch_quality(q, total, st));
+    return DTS_OK;
+}
+
+int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
+                         const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
+{
+    if (!g || !src || !dst || nframes < 0) return DTS_E_INVAL;
+    if (nframes == 0) return DTS_OK;
+    const dts_graph_spec &s = g->spec;
+    if (!planes_ok(*src, s.src_w, s.src_h, s.src_fmt, 16)) return DTS_E_INVAL;
+    for (int k = 0; k < s.nout; ++k)
+        if (!planes_ok(dst[k], s.out[k].w, s.out[k].h, s.out[k].fmt, 4)) return DTS_E_INVAL;
+    if (s.src_fmt == DTS_FMT_YUV420P && src->pitch[1] != src->pitch[2]) return DTS_E_INVAL;
+    const bool want_q = s.quality && qref && qraw_dev;
+    if (want_q && !planes_ok(*qref, s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, 4))
+        return DTS_E_INVAL;
+    dts_ctx *ctx = g->ctx;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+
+    LadderParams p{};
+    p.src = to_dev(*src, s.src_fmt);
+    for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) {
+        const int kk = k < s.nout ? k : 0;
+        p.dst[k] = to_dev(dst[kk], s.out[kk].fmt);
+        p.dst_fmt[k] = s.out[kk].fmt;
+    }
+    p.srcW = s.src_w;
+    p.srcH = s.src_h;
+    p.chrW = (s.src_w + 1) >> 1;
+    p.chrH = (s.src_h + 1) >> 1;
+    p.src_kind = g->src_kind;
+    p.nrungs = s.nout;
+    p.njobs = (int)g->jobs.size();
+    p.ring_pairs = g->ring_pairs;
+    p.stage_bytes = g->stage_bytes;
+    p.jobs = g->dev_jobs;
+    p.rk = g->dev_rk;
+    // bound the grid (blocks = frames x jobs) per launch
+    const int max_frames = std::max(1, (1 << 30) / std::max(1, p.njobs));
+    for (int f0 = 0; f0 < nframes; f0 += max_frames) {
+        const int n = std::min(max_frames, nframes - f0);
+        LadderParams pp = p;
+        pp.nframes = n;
+        pp.src.data[0] += (uint64_t)(f0 * src->frame_stride);
+        pp.src.data[1] += (uint64_t)(f0 * src->frame_stride);
+        pp.src.data[2] += (uint64_t)(f0 * src->frame_stride);
+        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
+            for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
+        HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, st));
+    }
+    if (want_q) {
+        const dts_output_spec &o = s.out[s.quality_out];
+        return quality_enqueue(ctx, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
+    }
+    return DTS_OK;
+}
+
+int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_frames *a, const dts_dev_frames *b,
+                           int nframes, dts_qraw *qraw_dev, void *stream)
+{
+    if (!ctx || !a || !b || !qraw_dev || nframes < 0 || w < 1 || h < 1) return DTS_E_INVAL;
+    if (!fmt_out_ok(fmt)) return DTS_E_UNSUPPORTED;
+    if (!planes_ok(*a, w, h, fmt, 4) || !planes_ok(*b, w, h, fmt, 4)) return DTS_E_INVAL;
+    if (nframes == 0) return DTS_OK;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+    return quality_enqueue(ctx, w, h, fmt, *a, *b, nframes, qraw_dev, st);
+}
+
+int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out)
+{
+    if (!raw || !out || n < 0 || w < 1 || h < 1) return DTS_E_INVAL;
+    int pw[3] = {w, (w + 1) >> 1, (w + 1) >> 1}, ph[3] = {h, (h + 1) >> 1, (h + 1) >> 1};
+    double area = 0;
+    for (int c = 0; c < 3; ++c) area += (double)pw[c] * ph[c];
+    for (int i = 0; i < n; ++i) {
+        dts_qstat &q = out[i];
+        double mse = 0, ssim = 0;
+        for (int c = 0; c < 3; ++c) {
+            const double wgt = (double)pw[c] * ph[c] / area;
+            q.sse[c] = raw[i].sse[c];
+            q.mse[c] = raw[i].sse[c] / (double)((int64_t)pw[c] * ph[c]);
+            q.psnr[c] = 10.0 * std::log10(255.0 * 255.0 / q.mse[c]);   // vf_psnr get_psnr
+            mse += q.mse[c] * wgt;
+            const int nw = ((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1);
+            q.ssim[c] = raw[i].ssim_sum[c] / nw;   // vf_ssim ssim_plane (0/0 = NaN for planes < 8x8, as vf_ssim)
+            ssim += wgt * q.ssim[c];
+        }
+        q.mse_avg = mse;
+        q.psnr_avg = 10.0 * std::log10(255.0 * 255.0 / mse);
+        q.ssim_all = ssim;
+        q.ssim_db = 10.0 * std::log10(1.0 / (1.0 - ssim));                // vf_ssim ssim_db
+    }
+    return DTS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host-memory path: pinned double-buffered staging over two HIP streams
+// ---------------------------------------------------------------------------
+static int ensure_host_path(dts_graph *g)
+{
+    if (g->pin_in[0]) return DTS_OK;
+    dts_ctx *ctx = g->ctx;
+    const dts_graph_spec &s = g->spec;
+    const int B = g->batch;
+    g->pin_in_bytes = (int64_t)B * g->info.src_frame_bytes;
+    if (s.quality) g->pin_in_bytes += (int64_t)B * g->info.out_frame_bytes[s.quality_out];
+    g->pin_out_bytes = 0;
+    for (int k = 0; k < s.nout; ++k) g->pin_out_bytes += (int64_t)B * g->info.out_frame_bytes[k];
+    for (int sl = 0; sl < 2; ++sl) {
+        HIPCHK(ctx, hipMalloc(&g->dev_src[sl], (size_t)B * g->lay_src.fstride));
+        for (int k = 0; k < s.nout; ++k) HIPCHK(ctx, hipMalloc(&g->dev_out[sl][k], (size_t)B * g->lay_out[k].fstride));
+        if (s.quality) {
+            HIPCHK(ctx, hipMalloc(&g->dev_q[sl], (size_t)B * g->lay_q.fstride));
+            HIPCHK(ctx, hipMalloc(&g->dev_qraw[sl], (size_t)B * sizeof(dts_qraw)));
+            HIPCHK(ctx, hipHostMalloc(&g->pin_qraw[sl], (size_t)B * sizeof(dts_qraw), hipHostMallocDefault));
+        }
+        HIPCHK(ctx, hipHostMalloc(&g->pin_in[sl], (size_t)g->pin_in_bytes, hipHostMallocDefault));
+        HIPCHK(ctx, hipHostMalloc(&g->pin_out[sl], (size_t)g->pin_out_bytes, hipHostMallocDefault));
+        HIPCHK(ctx, hipEventCreateWithFlags(&g->done[sl], hipEventDisableTiming));
+    }
+    return DTS_OK;
+}
+
+// copy rows of a caller frame into/out of a packed pinned image
+static void pack_frame(uint8_t *dst, const dts_frame &f, int w, int h, int fmt)
+{
+    int64_t rowb[3], rows[3];
+    plane_geom(w, h, fmt, rowb, rows);
+    for (int p = 0; p < 3; ++p)
+        for (int64_t y = 0; y < rows[p]; ++y) {
+            std::memcpy(dst, static_cast<const uint8_t *>(f.data[p]) + y * f.pitch[p], (size_t)rowb[p]);
+            dst += rowb[p];
+        }
+}
+
+static void unpack_frame(const uint8_t *src, const dts_frame &f, int w, int h, int fmt)
+{
+    int64_t rowb[3], rows[3];
+    plane_geom(w, h, fmt, rowb, rows);
+    for (int p = 0; p < 3; ++p)
+        for (int64_t y = 0; y < rows[p]; ++y) {
+            std::memcpy(static_cast<uint8_t *>(f.data[p]) + y * f.pitch[p], src, (size_t)rowb[p]);
+            src += rowb[p];
+        }
+}
+
+// packed pinned image <-> device batch with our pitch: one 2D copy per plane per frame
+static hipError_t copy_frames(uint8_t *dev, const DevLayout &lay, uint8_t *host, int n, bool h2d, hipStream_t st)
+{
+    for (int f = 0; f < n; ++f)
+        for (int p = 0; p < 3; ++p) {
+            if (!lay.rowb[p]) continue;
+            uint8_t *d = dev + (int64_t)f * lay.fstride + lay.off[p];
+            hipError_t e = h2d ? hipMemcpy2DAsync(d, lay.pitch[p], host, lay.rowb[p], lay.rowb[p], lay.rows[p],
+                                                  hipMemcpyHostToDevice, st)
+                               : hipMemcpy2DAsync(host, lay.rowb[p], d, lay.pitch[p], lay.rowb[p], lay.rows[p],
+                                                  hipMemcpyDeviceToHost, st);
+            if (e != hipSuccess) return e;
+            host += lay.rowb[p] * lay.rows[p];
+        }
+    return hipSuccess;
+}
+
+static dts_dev_frames dev_frames(uint8_t *base, const DevLayout &lay)
+{
+    dts_dev_frames d{};
+    for (int p = 0; p < 3; ++p) {
+        d.data[p] = lay.rowb[p] ? base + lay.off[p] : nullptr;
+        d.pitch[p] = lay.pitch[p];
+    }
+    d.frame_stride = lay.fstride;
+    return d;
+}
+
+static int finish_slot(dts_graph *g, int sl)
+{
+    if (g->p_chunk_first[sl] < 0) return DTS_OK;
+    dts_ctx *ctx = g->ctx;
+    const dts_graph_spec &s = g->spec;
+    HIPCHK(ctx, hipEventSynchronize(g->done[sl]));
+    const int f0 = g->p_chunk_first[sl], n = g->p_chunk_n[sl];
+    const uint8_t *hp = g->pin_out[sl];
+    for (int k = 0; k < s.nout; ++k)
+        for (int f = 0; f < n; ++f) {
+            unpack_frame(hp, g->p_dst[(int64_t)(f0 + f) * s.nout + k], s.out[k].w, s.out[k].h, s.out[k].fmt);
+            hp += g->info.out_frame_bytes[k];
+        }
+    if (s.quality && g->p_q) {
+        const dts_output_spec &o = s.out[s.quality_out];
+        dts_qstat_finalize(o.w, o.h, g->pin_qraw[sl], n, g->p_q + f0);
+    }
+    g->p_chunk_first[sl] = -1;
+    return DTS_OK;
+}
+
+int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_frame *dst, const dts_frame *qref,
+                     dts_qstat *q)
+{
+    if (!g || !src || !dst || nframes < 0) return DTS_E_INVAL;
+    if (g->pending) return DTS_E_BUSY;
+    const dts_graph_spec &s = g->spec;
+    if (s.quality && !qref) return DTS_E_INVAL;
+    dts_ctx *ctx = g->ctx;
+    hipSetDevice(ctx->device);
+    try {
+        int e = ensure_host_path(g);
+        if (e) return e;
+        g->pending = true;
+        g->p_dst = dst;
+        g->p_q = q;
+        const int B = g->batch;
+        int chunk = 0;
+        for (int f0 = 0; f0 < nframes; f0 += B, ++chunk) {
+            const int sl = chunk & 1;
+            const int n = std::min(B, nframes - f0);
+            e = finish_slot(g, sl);              // slot reuse: drain chunk-2 first
+            if (e) return e;
+            hipStream_t st = ctx->stream[sl];
+            uint8_t *hp = g->pin_in[sl];
+            for (int f = 0; f < n; ++f) {
+                pack_frame(hp + (int64_t)f * g->info.src_frame_bytes, src[f0 + f], s.src_w, s.src_h, s.src_fmt);
+            }
+            HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n, true, st));
+            uint8_t *qhp = hp + (int64_t)B * g->info.src_frame_bytes;
+            if (s.quality) {
+                const dts_output_spec &o = s.out[s.quality_out];
+                for (int f = 0; f < n; ++f)
+                    pack_frame(qhp + (int64_t)f * g->info.out_frame_bytes[s.quality_out], qref[f0 + f], o.w, o.h, o.fmt);
+                HIPCHK(ctx, copy_frames(g->dev_q[sl], g->lay_q, qhp, n, true, st));
+            }
+            dts_dev_frames dsrc = dev_frames(g->dev_src[sl], g->lay_src);
+            dts_dev_frames ddst[DTS_MAX_OUTPUTS];
+            for (int k = 0; k < s.nout; ++k) ddst[k] = dev_frames(g->dev_out[sl][k], g->lay_out[k]);
+            dts_dev_frames dq = s.quality ? dev_frames(g->dev_q[sl], g->lay_q) : dts_dev_frames{};
+            e = dts_graph_run_device(g, &dsrc, n, ddst, s.quality ? &dq : nullptr, s.quality ? g->dev_qraw[sl] : nullptr,
+                                     st);
+            if (e) return e;
+            uint8_t *op = g->pin_out[sl];
+            for (int k = 0; k < s.nout; ++k) {
+                HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
+                op += (int64_t)B * g->info.out_frame_bytes[k];
+            }
+            if (s.quality)
+                HIPCHK(ctx, hipMemcpyAsync(g->pin_qraw[sl], g->dev_qraw[sl], (size_t)n * sizeof(dts_qraw),
+                                           hipMemcpyDeviceToHost, st));
+            HIPCHK(ctx, hipEventRecord(g->done[sl], st));
+            g->p_chunk_first[sl] = f0;
+            g->p_chunk_n[sl] = n;
+        }
+        return DTS_OK;
+    } catch (const std::bad_alloc &) {
+        return DTS_E_NOMEM;
+    }
+}
+
+int dts_graph_wait(dts_graph *g)
+{
+    if (!g) return DTS_E_INVAL;
+    if (!g->pending) return DTS_OK;
+    hipSetDevice(g->ctx->device);
+    // finish the older slot first (chunk order does not matter for correctness)
+    int e0 = finish_slot(g, 0), e1 = finish_slot(g, 1);
+    g->pending = false;
+    return e0 ? e0 : e1;
+}
+
+int dts_sws_filter(int src_n, int dst_n, int one, int align, int method, const double param[2], int pos,
+                   int16_t *coeff, int32_t *filter_pos, int cap)
+{
+    if (src_n < 1 || dst_n < 1 || !coeff || !filter_pos || cap < 1 || !method_ok(method)) return DTS_E_INVAL;
+    const double dflt[2] = {DTS_PARAM_DEFAULT, DTS_PARAM_DEFAULT};
+    try {
+        SwsFilter f;
+        const int e = sws_build_filter(src_n, dst_n, one, align, method | kSwsAccurateRnd | kSwsBitexact,
+                                       param ? param : dflt, pos, pos, f);
+        if (e) return e;
+        if (f.size > cap) return DTS_E_RANGE;
+        for (int i = 0; i < dst_n; ++i) {
+            filter_pos[i] = f.pos[i];
+            for (int j = 0; j < f.size; ++j) coeff[(size_t)i * f.size + j] = f.coeff[(size_t)i * f.size + j];
+        }
+        return f.size;
+    } catch (...) {
+        return DTS_E_NOMEM;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic source
+// ---------------------------------------------------------------------------
+int dts_synth_host(int w, int h, int fmt, int pattern, uint32_t seed, int64_t frame, const dts_frame *dst)
+{
+    if (w < 1 || h < 1 || !fmt_in_ok(fmt) || !dst || pattern < 0 || pattern > 1) return DTS_E_INVAL;
+    const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+    const bool ten = fmt == DTS_FMT_P010LE;
+    for (int y = 0; y < h; ++y) {
+        uint8_t *row = static_cast<uint8_t *>(dst->data[0]) + (int64_t)y * dst->pitch[0];
+        for (int x = 0; x < w; ++x) {
+            const int v = synth_sample(pattern, seed, x, y, frame, 0, w, h, ten);
+            if (ten) {
+                row[2 * x] = (uint8_t)(v << 6);
+                row[2 * x + 1] = (uint8_t)((v << 6) >> 8);
+            } else {
+                row[x] = (uint8_t)v;
+            }
+        }
+    }
+    for (int y = 0; y < ch; ++y)
+        for (int x = 0; x < cw; ++x) {
+            const int u = synth_sample(pattern, seed, x, y, frame, 1, cw, ch, ten);
+            const int v = synth_sample(pattern, seed, x, y, frame, 2, cw, ch, ten);
+            if (fmt == DTS_FMT_YUV420P) {
+                static_cast<uint8_t *>(dst->data[1])[(int64_t)y * dst->pitch[1] + x] = (uint8_t)u;
+                static_cast<uint8_t *>(dst->data[2])[(int64_t)y * dst->pitch[2] + x] = (uint8_t)v;
+            } else if (fmt == DTS_FMT_NV12) {
+                uint8_t *row = static_cast<uint8_t *>(dst->data[1]) + (int64_t)y * dst->pitch[1];
+                row[2 * x] = (uint8_t)u;
+                row[2 * x + 1] = (uint8_t)v;
+            } else {
+                uint8_t *row = static_cast<uint8_t *>(dst->data[1]) + (int64_t)y * dst->pitch[1];
+                row[4 * x] = (uint8_t)(u << 6);
+                row[4 * x + 1] = (uint8_t)((u << 6) >> 8);
+                row[4 * x + 2] = (uint8_t)(v << 6);
+                row[4 * x + 3] = (uint8_t)((v << 6) >> 8);
+            }
+        }
+    return DTS_OK;
+}
+
+int dts_synth_device(dts_ctx *ctx, int w, int h, int fmt, int pattern, uint32_t seed, int64_t first,
+                     const dts_dev_frames *dst, int nframes, void *stream)
+{
+    if (!ctx || !dst || w < 1 || h < 1 || !fmt_in_ok(fmt) || nframes < 0 || pattern < 0 || pattern > 1)
+        return DTS_E_INVAL;
+    if (!planes_ok(*dst, w, h, fmt, 1)) return DTS_E_INVAL;
+    if (!nframes) return DTS_OK;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+    HIPCHK(ctx, launch_synth(w, h, fmt, pattern, seed, first, to_dev(*dst, fmt), nframes, st));
+    return DTS_OK;
+}
+
+// vf_fps.c (FFmpeg 4.4) frame selection, round=near, constant-rate input
+// whose first pts is 0: t_i = round(i * in_den*out_num / (in_num*out_den)),
+// output k repeats the last input with t_i <= k; EOF pts bounds the count.
+int64_t dts_fps_map(int64_t nb_in, int in_num, int in_den, int out_num, int out_den, int64_t *out_idx, int64_t cap)
+{
+    if (nb_in < 0 || in_num <= 0 || in_den <= 0 || out_num <= 0 || out_den <= 0 || cap < 0) return DTS_E_INVAL;
+    if (cap > 0 && !out_idx) return DTS_E_INVAL;
+    const __int128 b = (__int128)in_den * out_num, c = (__int128)in_num * out_den;
+    auto near = [&](int64_t a) { return (int64_t)(((__int128)a * b + c / 2) / c); };
+    const int64_t nout = nb_in ? near(nb_in) : 0;
+    int64_t i = 0;
+    for (int64_t k = 0; k < nout && k < cap; ++k) {
+        while (i + 1 < nb_in && near(i + 1) <= k) ++i;
+        out_idx[k] = i;
+    }
+    return nout;
+}
+
+} // extern "C"

@@ -1,0 +1,161 @@
+// dts_internal.h -- shared between the host side of libdts (api.cpp,
+// filters.cpp) and the HIP kernels (kernels.hip).  All code here is compiled
+// by hipcc for gfx950 (device) and x86-64 (host).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dts.h"
+
+namespace dts {
+
+// ---------------------------------------------------------------------------
+// Ladder (scale + format convert) launch geometry
+// ---------------------------------------------------------------------------
+constexpr int kThreads = 256;      // workgroup size (4 waves)
+constexpr int kBlkRows = 8;        // source rows per pipeline step (4 row pairs)
+constexpr int kLumaCols = 256;     // output columns per luma strip (1 per thread)
+constexpr int kChromaCols = 128;   // output columns per chroma strip (U: t<128, V: t>=128)
+constexpr int kMaxLoads = 4;       // uint4 staging loads per thread per step
+constexpr int kMaxRungs = DTS_MAX_OUTPUTS;
+
+// source kinds: what the staging loads unpack
+enum SrcKind : int { kSrcPlanar8 = 0, kSrcNV12 = 1, kSrcP010 = 2 };
+
+struct DevPlanes {                  // one batch of frames in HBM
+    uint64_t data[3];
+    int64_t pitch[3];
+    int64_t fstride;
+};
+
+struct RungKind {                   // GPU tables of one rung for luma (0) or chroma (1)
+    int32_t dstW, dstH;
+    int32_t nd;                     // H: coefficient dwords per output (u8: 4 taps, p010: 2 taps)
+    int32_t nv;                     // V: row pairs per output row
+    int32_t nblocks;                // source pipeline steps
+    int32_t pad_;
+    const int32_t *hpos;            // [dstW] first source sample of the GPU window
+    const int32_t *hbias;           // [dstW] 128 * sum(coeff) (u8 path)
+    const uint32_t *hch;            // [nd][dstW] u8: high i8x4 parts; p010: int16x2 pairs
+    const uint32_t *hcl;            // [nd][dstW] u8: low i8x4 parts
+    const int32_t *vpos;            // [dstH] even first source row of the GPU window
+    const uint32_t *vcoef;          // [dstH][nv] int16x2 (even row low, odd row high)
+    const int32_t *vlim;            // [nblocks] output rows finished after step b
+};
+
+struct Job {                        // one workgroup's work inside a frame
+    int16_t rung, kind;             // kind 0 = luma, 1 = chroma (U and V)
+    int32_t x0;                     // first output column of the strip
+    int32_t ncols;                  // columns in this strip
+    int32_t sx0;                    // first source sample staged (16-byte aligned in bytes)
+    int32_t swb;                    // staged bytes per source row per plane (multiple of 16)
+    int32_t nload;                  // uint4 staging loads per step (all planes, all rows)
+};
+
+struct LadderParams {
+    DevPlanes src;
+    DevPlanes dst[kMaxRungs];
+    int32_t dst_fmt[kMaxRungs];
+    int32_t srcW, srcH, chrW, chrH;
+    int32_t src_kind;
+    int32_t nrungs;
+    int32_t njobs;
+    int32_t ring_pairs;             // power of two
+    int32_t stage_bytes;            // one stage buffer (all planes), bytes
+    int32_t nframes;
+    const Job *jobs;                // device [njobs]
+    const RungKind *rk;             // device [nrungs][2]
+};
+
+// ---------------------------------------------------------------------------
+// Quality (vf_psnr + vf_ssim) launch geometry
+// ---------------------------------------------------------------------------
+constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x
+constexpr int kQTileBY = 16;        // 4x4 blocks per tile, y
+
+struct QualityParams {
+    DevPlanes a, b;
+    int32_t pw[3], ph[3];           // plane sizes
+    int32_t tiles_x[3], tiles_y[3];
+    int32_t tile_base[4];           // prefix of tiles per plane
+    int32_t interleaved;            // 1 = nv12 (plane 1 holds U,V interleaved)
+    int32_t nframes;
+    double *partial_ssim;           // [nframes][tiles]
+    unsigned long long *partial_sse;// [nframes][tiles]
+    dts_qraw *out;                  // [nframes]
+};
+
+// ---------------------------------------------------------------------------
+// Synthetic source (testsrc2-like), identical on host and device
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint32_t synth_hash(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__host__ __device__ inline uint32_t synth_noise(uint32_t seed, int x, int y, int64_t f, int comp)
+{
+    return synth_hash(seed ^ ((uint32_t)x * 0x9E3779B1u) ^ ((uint32_t)y * 0x85EBCA77u) ^
+                      ((uint32_t)f * 0xC2B2AE3Du) ^ ((uint32_t)comp * 0x27D4EB2Fu));
+}
+
+__host__ __device__ inline int synth_clampi(int v, int lo, int hi)
+{
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// comp 0 = Y (plane size w x h), 1 = U, 2 = V (plane size cw x ch).
+// Returns an 8-bit sample, or a 10-bit sample when ten_bit.
+__host__ __device__ inline int synth_sample(int pattern, uint32_t seed, int x, int y, int64_t f,
+                                            int comp, int pw, int ph, bool ten_bit)
+{
+    uint32_t n = synth_noise(seed, x, y, f, comp);
+    if (pattern == 1)
+        return ten_bit ? (int)(n & 1023u) : (int)(n & 255u);
+    int fm = (int)(f % 4096);
+    int span = pw + ph;
+    int v;
+    if (comp == 0) {
+        int g = ((x + y + 2 * fm) % span) * 219 / span;
+        int barw = pw / 16 > 0 ? pw / 16 : 1;
+        int bar = (((x + 4 * fm) / barw) & 1) ? 24 : 0;
+        int nz = (int)(n & 31u) - 16;
+        v = 16 + g + bar + nz;
+        v = synth_clampi(v, 16, 235);
+    } else {
+        int g = comp == 1 ? ((x + fm) % (pw > 0 ? pw : 1)) * 224 / (pw > 0 ? pw : 1)
+                          : ((y + fm) % (ph > 0 ? ph : 1)) * 224 / (ph > 0 ? ph : 1);
+        int nz = (int)(n & 7u) - 4;
+        v = synth_clampi(16 + g + nz, 16, 240);
+    }
+    if (ten_bit) {
+        int lo = comp == 0 ? 64 : 64, hi = comp == 0 ? 940 : 960;
+        v = synth_clampi(v * 4 + (int)((n >> 8) & 3u), lo, hi);
+    }
+    return v;
+}
+
+// ordered dither libswscale ff_dither_8x8_128 (FFmpeg 4.4 swscale.c; values
+// restated from memory)
+#define DTS_DITHER_8X8_128                                              \
+    {                                                                   \
+        {36, 68, 60, 92, 34, 66, 58, 90}, {100, 4, 124, 28, 98, 2, 122, 26}, \
+        {52, 84, 44, 76, 50, 82, 42, 74}, {116, 20, 108, 12, 114, 18, 106, 10}, \
+        {32, 64, 56, 88, 38, 70, 62, 94}, {96, 0, 120, 24, 102, 6, 126, 30}, \
+        {48, 80, 40, 72, 54, 86, 46, 78}, {112, 16, 104, 8, 118, 22, 110, 14}, \
+    }
+
+// kernels.hip entry points (host-side launchers)
+hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, hipStream_t s);
+hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s);
+hipError_t launch_synth(int w, int h, int fmt, int pattern, uint32_t seed, int64_t first,
+                        const DevPlanes &dst, int nframes, hipStream_t s);
+int ladder_ndmax_for(int nd);       // template bucket for a required nd (0 = unsupported)
+
+} // namespace dts

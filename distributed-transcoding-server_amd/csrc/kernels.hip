@@ -1,0 +1,585 @@
+// kernels.hip -- gfx950 kernels of the per-segment pixel filtergraph.
+//
+//  k_ladder   : fused separable polyphase scale + pixel-format convert for
+//               every rendition of a graph in ONE launch (libswscale
+//               hScale8To15/hScale16To15 -> yuv2planeX_8 / yuv2nv12cX under
+//               SWS_BITEXACT|SWS_ACCURATE_RND, bit-exact).
+//  k_quality  : vf_psnr SSE + vf_ssim 4x4-block / 8x8-window SSIM partials.
+//  k_qreduce  : fixed-order reduction of the quality partials per frame.
+//  k_synth    : deterministic testsrc2-like source frames.
+//
+// Design (DESIGN.md "Kernels"): one workgroup = one (frame, rendition, plane
+// kind, column strip).  It walks the source rows top to bottom in steps of
+// 8 rows: the strip's source window is staged into LDS with 16-B coalesced
+// loads (prefetched one step ahead in registers), each thread produces the
+// 15-bit horizontal intermediates of its output column for the 8 rows with
+// v_dot4_i32_i8 (u8) / v_dot2_i32_i16 (p010) from per-thread coefficient
+// registers, row pairs are packed int16x2 into an LDS ring, and the vertical
+// FIR (v_dot2_i32_i16 with wave-uniform coefficients) emits every output row
+// whose window is complete.  No intermediate touches HBM; each source byte is
+// fetched from HBM once per rendition strip (re-reads of the same frame by
+// the other renditions hit the XCD L2 / Infinity Cache).
+#include "dts_internal.h"
+
+namespace dts {
+
+__constant__ uint8_t c_dither[8][8] = DTS_DITHER_8X8_128;
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c)
+{
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, a), __builtin_bit_cast(short2v, b), c, false);
+}
+
+__device__ __forceinline__ uint32_t clip8(int v)
+{
+    v >>= 19;
+    return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// ---------------------------------------------------------------------------
+// k_ladder
+// ---------------------------------------------------------------------------
+template <int SRC, int NDMAX>
+__global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int t = threadIdx.x;
+    const int jid = blockIdx.x % P.njobs;
+    const int frame = blockIdx.x / P.njobs;
+    const Job J = P.jobs[jid];
+    const int kind = J.kind;
+    const RungKind K = P.rk[J.rung * 2 + kind];
+    const int RP = P.ring_pairs;
+    const int pcols = kind ? kChromaCols : kLumaCols;
+    const int srcH = kind ? P.chrH : P.srcH;
+    const int swb = J.swb;
+    const int plane_stage = kBlkRows * swb;         // bytes of one plane in a stage buffer
+
+    uint8_t *const stage0 = smem;
+    uint8_t *const stage1 = smem + P.stage_bytes;
+    uint32_t *const ring = reinterpret_cast<uint32_t *>(smem + 2 * P.stage_bytes);
+
+    // ---- staging item decode (fixed per thread for the whole walk) --------
+    const int n16 = swb >> 4;                        // 16-B chunks per row per plane
+    const bool inter_chroma = kind && (SRC != kSrcPlanar8);
+    const int per_row = inter_chroma ? 2 * n16 : n16;
+    const int pln = kind ? (SRC == kSrcPlanar8 ? 1 : 1) : 0;
+    const int64_t pitch = P.src.pitch[kind ? 1 : 0];
+    const int64_t fbase = (int64_t)frame * P.src.fstride;
+    const uint8_t *gptr[kMaxLoads];
+    int srow[kMaxLoads], sofs[kMaxLoads];
+    bool sok[kMaxLoads];
+#pragma unroll
+    for (int k = 0; k < kMaxLoads; ++k) {
+        const int i = t + k * kThreads;
+        int plane = pln, row = 0, c = 0;
+        if (inter_chroma) {
+            row = i / per_row;
+            c = i - row * per_row;
+        } else {
+            const int pr = i / n16;
+            c = i - pr * n16;
+            plane += pr / kBlkRows;
+            row = pr % kBlkRows;
+        }
+        int64_t boff;        // byte offset of the chunk inside the source row
+        if (!inter_chroma)
+            boff = (int64_t)J.sx0 * (SRC == kSrcP010 ? 2 : 1) + 16 * c;
+        else
+            boff = (int64_t)J.sx0 * (SRC == kSrcP010 ? 4 : 2) + 16 * c;
+        gptr[k] = reinterpret_cast<const uint8_t *>(P.src.data[plane]) + fbase + row * P.src.pitch[plane] + boff;
+        srow[k] = row;
+        sok[k] = (i < J.nload) && (boff + 16 <= P.src.pitch[plane]);
+        if (inter_chroma)
+            sofs[k] = row * swb + 8 * c;                 // U at +0, V at +plane_stage
+        else
+            sofs[k] = (plane - pln) * plane_stage + row * swb + 16 * c;
+    }
+    const int64_t rowstep = (int64_t)kBlkRows * pitch;
+
+    uint4 pre[kMaxLoads];
+    auto issue = [&](int b) {
+#pragma unroll
+        for (int k = 0; k < kMaxLoads; ++k) {
+            if (sok[k] && b * kBlkRows + srow[k] < srcH)
+                pre[k] = *reinterpret_cast<const uint4 *>(gptr[k] + b * rowstep);
+            else
+                pre[k] = make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto commit = [&](uint8_t *stage) {
+#pragma unroll
+        for (int k = 0; k < kMaxLoads; ++k) {
+            if (t + k * kThreads >= J.nload) continue;
+            uint4 v = pre[k];
+            if (!inter_chroma) {
+                if (SRC == kSrcP010) {
+                    v.x = (v.x >> 6) & 0x03ff03ffu;
+                    v.y = (v.y >> 6) & 0x03ff03ffu;
+                    v.z = (v.z >> 6) & 0x03ff03ffu;
+                    v.w = (v.w >> 6) & 0x03ff03ffu;
+                } else {
+                    v.x ^= 0x80808080u;
+                    v.y ^= 0x80808080u;
+                    v.z ^= 0x80808080u;
+                    v.w ^= 0x80808080u;
+                }
+                *reinterpret_cast<uint4 *>(stage + sofs[k]) = v;
+            } else if (SRC == kSrcNV12) {
+                uint2 u, w;
+                u.x = perm(v.y, v.x, 0x06040200u) ^ 0x80808080u;
+                u.y = perm(v.w, v.z, 0x06040200u) ^ 0x80808080u;
+                w.x = perm(v.y, v.x, 0x07050301u) ^ 0x80808080u;
+                w.y = perm(v.w, v.z, 0x07050301u) ^ 0x80808080u;
+                *reinterpret_cast<uint2 *>(stage + sofs[k]) = u;
+                *reinterpret_cast<uint2 *>(stage + plane_stage + sofs[k]) = w;
+            } else { // p010 interleaved UV: dword = U16 | V16 << 16
+                uint2 u, w;
+                u.x = (perm(v.y, v.x, 0x05040100u) >> 6) & 0x03ff03ffu;
+                u.y = (perm(v.w, v.z, 0x05040100u) >> 6) & 0x03ff03ffu;
+                w.x = (perm(v.y, v.x, 0x07060302u) >> 6) & 0x03ff03ffu;
+                w.y = (perm(v.w, v.z, 0x07060302u) >> 6) & 0x03ff03ffu;
+                *reinterpret_cast<uint2 *>(stage + sofs[k]) = u;
+                *reinterpret_cast<uint2 *>(stage + plane_stage + sofs[k]) = w;
+            }
+        }
+    };
+
+    // ---- horizontal lane: one output column, coefficients in registers ----
+    const int hplane = kind ? (t >> 7) : 0;
+    const int hcol = kind ? (t & (kChromaCols - 1)) : t;
+    const bool hact = hcol < J.ncols;
+    const int hx = J.x0 + (hact ? hcol : 0);
+    uint32_t chv[NDMAX], clv[NDMAX];
+    int bias = 0, lofs = 0;
+    {
+        const int p = K.hpos[hx];
+        bias = SRC == kSrcP010 ? 0 : K.hbias[hx];
+        lofs = hplane * plane_stage + (p - J.sx0) * (SRC == kSrcP010 ? 2 : 1);
+#pragma unroll
+        for (int k = 0; k < NDMAX; ++k) {
+            chv[k] = k < K.nd ? K.hch[(int64_t)k * K.dstW + hx] : 0u;
+            clv[k] = (SRC != kSrcP010 && k < K.nd) ? K.hcl[(int64_t)k * K.dstW + hx] : 0u;
+        }
+    }
+    const int nd = K.nd;
+
+    auto hpass = [&](int b, const uint8_t *stage) {
+        if (!hact) return;
+#pragma unroll
+        for (int pr = 0; pr < kBlkRows / 2; ++pr) {
+            int hv[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const uint32_t *rp = reinterpret_cast<const uint32_t *>(stage + lofs + (2 * pr + s) * swb);
+                int val;
+                if (SRC == kSrcP010) {
+                    int a = 0;
+#pragma unroll
+                    for (int k = 0; k < NDMAX; ++k)
+                        if (k < nd) a = dot2(rp[k], chv[k], a);
+                    val = a >> 9;                                   // hScale16To15: sh = depth - 1
+                } else {
+                    int a = 0, c = bias;
+#pragma unroll
+                    for (int k = 0; k < NDMAX; ++k)
+                        if (k < nd) {
+                            const uint32_t v = rp[k];
+                            a = dot4(v, chv[k], a);
+                            c = dot4(v, clv[k], c);
+                        }
+                    val = (a * 256 + c) >> 7;                       // hScale8To15
+                }
+                hv[s] = val < 32767 ? val : 32767;
+            }
+            const int slot = (b * (kBlkRows / 2) + pr) & (RP - 1);
+            ring[(hplane * RP + slot) * pcols + hcol] = (uint32_t)(hv[0] & 0xffff) | ((uint32_t)hv[1] << 16);
+        }
+    };
+
+    // ---- vertical: one output row per wave, wave-uniform coefficients ----
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int lane = t & 63;
+    const int rung = J.rung;
+    DevPlanes dst = P.dst[0];
+    int dfmt = P.dst_fmt[0];
+    if (rung == 1) { dst = P.dst[1]; dfmt = P.dst_fmt[1]; }
+    if (rung == 2) { dst = P.dst[2]; dfmt = P.dst_fmt[2]; }
+    if (rung == 3) { dst = P.dst[3]; dfmt = P.dst_fmt[3]; }
+    const int64_t dbase = (int64_t)frame * dst.fstride;
+    const bool hidepth = SRC == kSrcP010;
+
+    auto vpass = [&](int b) {
+        const int vlo = b ? K.vlim[b - 1] : 0;
+        const int vhi = K.vlim[b];
+        for (int y = vlo + wave; y < vhi; y += kThreads / 64) {
+            const int q0 = K.vpos[y] >> 1;
+            const uint32_t *vc = K.vcoef + (int64_t)y * K.nv;
+            if (kind == 0) {
+                const int c0 = 4 * lane;
+                int d[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) d[i] = (hidepth ? c_dither[y & 7][(c0 + i) & 7] : 64) << 12;
+                int a0 = d[0], a1 = d[1], a2 = d[2], a3 = d[3];
+                for (int k = 0; k < K.nv; ++k) {
+                    const int slot = (q0 + k) & (RP - 1);
+                    const uint4 v = *reinterpret_cast<const uint4 *>(ring + slot * kLumaCols + c0);
+                    const uint32_t c = vc[k];
+                    a0 = dot2(v.x, c, a0);
+                    a1 = dot2(v.y, c, a1);
+                    a2 = dot2(v.z, c, a2);
+                    a3 = dot2(v.w, c, a3);
+                }
+                const uint32_t o = clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24);
+                uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[0]) + dbase + (int64_t)y * dst.pitch[0] + J.x0;
+                if (c0 + 3 < J.ncols) {
+                    *reinterpret_cast<uint32_t *>(row + c0) = o;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (c0 + i < J.ncols) row[c0 + i] = (uint8_t)(o >> (8 * i));
+                }
+            } else {
+                const int c0 = 2 * lane;
+                int du0 = 64 << 12, du1 = 64 << 12, dv0 = 64 << 12, dv1 = 64 << 12;
+                if (hidepth) {     // vscale.c: U dither offset 0, V offset 3 (x0 is a multiple of 8)
+                    du0 = c_dither[y & 7][(c0) & 7] << 12;
+                    du1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
+                    dv0 = c_dither[y & 7][(c0 + 3) & 7] << 12;
+                    dv1 = c_dither[y & 7][(c0 + 4) & 7] << 12;
+                }
+                int u0 = du0, u1 = du1, v0 = dv0, v1 = dv1;
+                for (int k = 0; k < K.nv; ++k) {
+                    const int slot = (q0 + k) & (RP - 1);
+                    const uint2 uu = *reinterpret_cast<const uint2 *>(ring + slot * kChromaCols + c0);
+                    const uint2 vv = *reinterpret_cast<const uint2 *>(ring + (RP + slot) * kChromaCols + c0);
+                    const uint32_t c = vc[k];
+                    u0 = dot2(uu.x, c, u0);
+                    u1 = dot2(uu.y, c, u1);
+                    v0 = dot2(vv.x, c, v0);
+                    v1 = dot2(vv.y, c, v1);
+                }
+                const uint32_t U0 = clip8(u0), U1 = clip8(u1), V0 = clip8(v0), V1 = clip8(v1);
+                if (dfmt == DTS_FMT_NV12) {
+                    uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[1]) + dbase + (int64_t)y * dst.pitch[1] + 2 * J.x0;
+                    const uint32_t o = U0 | (V0 << 8) | (U1 << 16) | (V1 << 24);
+                    if (c0 + 1 < J.ncols)
+                        *reinterpret_cast<uint32_t *>(row + 2 * c0) = o;
+                    else if (c0 < J.ncols)
+                        *reinterpret_cast<uint16_t *>(row + 2 * c0) = (uint16_t)o;
+                } else {
+                    uint8_t *ru = reinterpret_cast<uint8_t *>(dst.data[1]) + dbase + (int64_t)y * dst.pitch[1] + J.x0;
+                    uint8_t *rv = reinterpret_cast<uint8_t *>(dst.data[2]) + dbase + (int64_t)y * dst.pitch[2] + J.x0;
+                    if (c0 + 1 < J.ncols) {
+                        *reinterpret_cast<uint16_t *>(ru + c0) = (uint16_t)(U0 | (U1 << 8));
+                        *reinterpret_cast<uint16_t *>(rv + c0) = (uint16_t)(V0 | (V1 << 8));
+                    } else if (c0 < J.ncols) {
+                        ru[c0] = (uint8_t)U0;
+                        rv[c0] = (uint8_t)V0;
+                    }
+                }
+            }
+        }
+    };
+
+    // ---- the walk ---------------------------------------------------------
+    const int nb = K.nblocks;
+    issue(0);
+    commit(stage0);
+    __syncthreads();
+    for (int b = 0; b < nb; ++b) {
+        const uint8_t *cur = (b & 1) ? stage1 : stage0;
+        uint8_t *nxt = (b & 1) ? stage0 : stage1;
+        const bool more = b + 1 < nb;
+        if (more) issue(b + 1);
+        hpass(b, cur);
+        if (more) commit(nxt);
+        __syncthreads();
+        vpass(b);
+        __syncthreads();
+    }
+}
+
+int ladder_ndmax_for(int nd)
+{
+    static const int buckets[] = {2, 3, 4, 6, 8, 12, 16};
+    for (int b : buckets)
+        if (nd <= b) return b;
+    return 0;
+}
+
+template <int SRC>
+static hipError_t launch_ladder_src(const LadderParams &p, int ndmax, int lds, hipStream_t s)
+{
+    const dim3 grid((unsigned)(p.njobs * p.nframes)), block(kThreads);
+    switch (ndmax) {
+#define DTS_CASE(N)                                                                  \
+    case N:                                                                          \
+        hipLaunchKernelGGL((k_ladder<SRC, N>), grid, block, lds, s, p);            \
+        break;
+        DTS_CASE(2) DTS_CASE(3) DTS_CASE(4) DTS_CASE(6) DTS_CASE(8) DTS_CASE(12) DTS_CASE(16)
+#undef DTS_CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, hipStream_t s)
+{
+    switch (p.src_kind) {
+    case kSrcPlanar8: return launch_ladder_src<kSrcPlanar8>(p, ndmax, lds_bytes, s);
+    case kSrcNV12: return launch_ladder_src<kSrcNV12>(p, ndmax, lds_bytes, s);
+    case kSrcP010: return launch_ladder_src<kSrcP010>(p, ndmax, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_quality: vf_psnr + vf_ssim partials.  One workgroup per (frame, plane,
+// tile of 64x16 4x4-blocks).  Block sums (s1, s2, ss, s12) of the tile plus a
+// one-block apron go to LDS; each owned block adds ss - 2*s12 = sum((a-b)^2)
+// to the SSE; each 8x8 window (2x2 blocks at stride 4) evaluates ssim_end1 in
+// f32 exactly as vf_ssim.c and accumulates in f64.  Pixels outside whole
+// blocks (plane width/height not multiples of 4) add to the SSE directly.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float ssim_end1(int s1, int s2, int ss, int s12)
+{
+    const int c1 = (int)(.01 * .01 * 255 * 255 * 64 + .5);
+    const int c2 = (int)(.03 * .03 * 255 * 255 * 64 * 63 + .5);
+    const int vars = ss * 64 - s1 * s1 - s2 * s2;
+    const int covar = s12 * 64 - s1 * s2;
+    return (float)(2 * s1 * s2 + c1) * (float)(2 * covar + c2) /
+           ((float)(s1 * s1 + s2 * s2 + c1) * (float)(vars + c2));
+}
+
+__device__ __forceinline__ uint32_t load4(const uint8_t *row, int x, bool inter, int comp)
+{
+    if (!inter) return *reinterpret_cast<const uint32_t *>(row + x);
+    const uint2 v = *reinterpret_cast<const uint2 *>(row + 2 * x);
+    return perm(v.y, v.x, comp ? 0x07050301u : 0x06040200u);
+}
+
+__device__ __forceinline__ int load1(const uint8_t *row, int x, bool inter, int comp)
+{
+    return inter ? row[2 * x + comp] : row[x];
+}
+
+__global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
+{
+    __shared__ int4 bs[kQTileBY + 1][kQTileBX + 1];
+    __shared__ double red_s[kThreads / 64];
+    __shared__ unsigned long long red_e[kThreads / 64];
+    const int t = threadIdx.x;
+    const int total = P.tile_base[3];
+    const int frame = blockIdx.x / total;
+    const int gt = blockIdx.x % total;
+    const int plane = gt >= P.tile_base[2] ? 2 : (gt >= P.tile_base[1] ? 1 : 0);
+    const int tile = gt - P.tile_base[plane];
+    const int tx = tile % P.tiles_x[plane], ty = tile / P.tiles_x[plane];
+    const int w = P.pw[plane], h = P.ph[plane];
+    const int W4 = w >> 2, H4 = h >> 2;
+    const int bx0 = tx * kQTileBX, by0 = ty * kQTileBY;
+    const bool inter = P.interleaved && plane > 0;
+    const int comp = plane == 2 ? 1 : 0;
+    const int dp = inter ? 1 : plane;
+    const uint8_t *A = reinterpret_cast<const uint8_t *>(P.a.data[dp]) + (int64_t)frame * P.a.fstride;
+    const uint8_t *B = reinterpret_cast<const uint8_t *>(P.b.data[dp]) + (int64_t)frame * P.b.fstride;
+    const int64_t pa = P.a.pitch[dp], pb = P.b.pitch[dp];
+
+    unsigned long long sse = 0;
+    for (int i = t; i < (kQTileBY + 1) * (kQTileBX + 1); i += kThreads) {
+        const int by = i / (kQTileBX + 1), bx = i - by * (kQTileBX + 1);
+        const int gx = bx0 + bx, gy = by0 + by;
+        int4 r = make_int4(0, 0, 0, 0);
+        if (gx < W4 && gy < H4) {
+            int s1 = 0, s2 = 0, ss = 0, s12 = 0;
+#pragma unroll
+            for (int yy = 0; yy < 4; ++yy) {
+                const uint32_t va = load4(A + (int64_t)(4 * gy + yy) * pa, 4 * gx, inter, comp);
+                const uint32_t vb = load4(B + (int64_t)(4 * gy + yy) * pb, 4 * gx, inter, comp);
+#pragma unroll
+                for (int xx = 0; xx < 4; ++xx) {
+                    const int a = (va >> (8 * xx)) & 255, b = (vb >> (8 * xx)) & 255;
+                    s1 += a;
+                    s2 += b;
+                    ss += a * a + b * b;
+                    s12 += a * b;
+                }
+            }
+            r = make_int4(s1, s2, ss, s12);
+            if (bx < kQTileBX && by < kQTileBY) sse += (unsigned long long)(ss - 2 * s12);
+        }
+        bs[by][bx] = r;
+    }
+    // pixels outside whole blocks, inside this tile's pixel rectangle
+    {
+        const int px0 = tx * 4 * kQTileBX, py0 = ty * 4 * kQTileBY;
+        const int px1 = min(w, px0 + 4 * kQTileBX), py1 = min(h, py0 + 4 * kQTileBY);
+        // right strip: x >= 4*W4, y < 4*H4
+        const int ax0 = max(px0, 4 * W4), ay1 = min(py1, 4 * H4);
+        const int aw = max(0, px1 - ax0), ah = max(0, ay1 - py0);
+        for (int i = t; i < aw * ah; i += kThreads) {
+            const int y = py0 + i / aw, x = ax0 + i % aw;
+            const int d = load1(A + (int64_t)y * pa, x, inter, comp) - load1(B + (int64_t)y * pb, x, inter, comp);
+            sse += (unsigned long long)(d * d);
+        }
+        // bottom strip: y >= 4*H4
+        const int by0p = max(py0, 4 * H4);
+        const int bw = max(0, px1 - px0), bh = max(0, py1 - by0p);
+        for (int i = t; i < bw * bh; i += kThreads) {
+            const int y = by0p + i / bw, x = px0 + i % bw;
+            const int d = load1(A + (int64_t)y * pa, x, inter, comp) - load1(B + (int64_t)y * pb, x, inter, comp);
+            sse += (unsigned long long)(d * d);
+        }
+    }
+    __syncthreads();
+    double ssim = 0.0;
+    for (int i = t; i < kQTileBY * kQTileBX; i += kThreads) {
+        const int wy = i / kQTileBX, wx = i - wy * kQTileBX;
+        if (bx0 + wx < W4 - 1 && by0 + wy < H4 - 1) {
+            const int4 p = bs[wy][wx], q = bs[wy][wx + 1], r = bs[wy + 1][wx], s = bs[wy + 1][wx + 1];
+            ssim += (double)ssim_end1(p.x + q.x + r.x + s.x, p.y + q.y + r.y + s.y, p.z + q.z + r.z + s.z,
+                                      p.w + q.w + r.w + s.w);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ssim += __shfl_xor(ssim, o);
+        sse += __shfl_xor(sse, o);
+    }
+    if ((t & 63) == 0) {
+        red_s[t >> 6] = ssim;
+        red_e[t >> 6] = sse;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double s = 0;
+        unsigned long long e = 0;
+        for (int i = 0; i < kThreads / 64; ++i) {
+            s += red_s[i];
+            e += red_e[i];
+        }
+        P.partial_ssim[(int64_t)frame * total + gt] = s;
+        P.partial_sse[(int64_t)frame * total + gt] = e;
+    }
+}
+
+// one workgroup per (frame, plane); fixed-order tree reduction
+__global__ void __launch_bounds__(kThreads) k_qreduce(const QualityParams P)
+{
+    __shared__ double rs[kThreads];
+    __shared__ unsigned long long re[kThreads];
+    const int frame = blockIdx.x / 3, plane = blockIdx.x % 3, t = threadIdx.x;
+    const int total = P.tile_base[3];
+    const int lo = P.tile_base[plane], hi = P.tile_base[plane + 1];
+    double s = 0;
+    unsigned long long e = 0;
+    for (int i = lo + t; i < hi; i += kThreads) {
+        s += P.partial_ssim[(int64_t)frame * total + i];
+        e += P.partial_sse[(int64_t)frame * total + i];
+    }
+    rs[t] = s;
+    re[t] = e;
+    __syncthreads();
+    for (int o = kThreads / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            rs[t] += rs[t + o];
+            re[t] += re[t + o];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        P.out[frame].sse[plane] = re[0];
+        P.out[frame].ssim_sum[plane] = rs[0];
+    }
+}
+
+hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quality, dim3((unsigned)(total_tiles * p.nframes)), dim3(kThreads), 0, s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_qreduce, dim3((unsigned)(3 * p.nframes)), dim3(kThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_synth: one thread per 4 samples of one plane row
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_synth(int w, int h, int fmt, int pattern, uint32_t seed,
+                                                    int64_t first, DevPlanes dst, int quads_y, int quads_c)
+{
+    const int64_t frame = blockIdx.y;
+    const int64_t f = first + frame;
+    const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+    int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const bool ten = fmt == DTS_FMT_P010LE;
+    uint8_t *base0 = reinterpret_cast<uint8_t *>(dst.data[0]) + frame * dst.fstride;
+    if (q < quads_y) {
+        const int qw = (w + 3) >> 2;
+        const int y = (int)(q / qw), x0 = (int)(q % qw) * 4;
+        uint8_t *row = base0 + (int64_t)y * dst.pitch[0];
+        for (int i = 0; i < 4 && x0 + i < w; ++i) {
+            const int v = synth_sample(pattern, seed, x0 + i, y, f, 0, w, h, ten);
+            if (ten) {
+                const int s = v << 6;
+                row[2 * (x0 + i)] = (uint8_t)s;
+                row[2 * (x0 + i) + 1] = (uint8_t)(s >> 8);
+            } else {
+                row[x0 + i] = (uint8_t)v;
+            }
+        }
+        return;
+    }
+    q -= quads_y;
+    if (q >= quads_c) return;
+    const int qw = (cw + 3) >> 2;
+    const int y = (int)(q / qw), x0 = (int)(q % qw) * 4;
+    for (int i = 0; i < 4 && x0 + i < cw; ++i) {
+        const int x = x0 + i;
+        const int u = synth_sample(pattern, seed, x, y, f, 1, cw, ch, ten);
+        const int v = synth_sample(pattern, seed, x, y, f, 2, cw, ch, ten);
+        if (fmt == DTS_FMT_YUV420P) {
+            reinterpret_cast<uint8_t *>(dst.data[1])[frame * dst.fstride + (int64_t)y * dst.pitch[1] + x] = (uint8_t)u;
+            reinterpret_cast<uint8_t *>(dst.data[2])[frame * dst.fstride + (int64_t)y * dst.pitch[2] + x] = (uint8_t)v;
+        } else if (fmt == DTS_FMT_NV12) {
+            uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[1]) + frame * dst.fstride + (int64_t)y * dst.pitch[1];
+            row[2 * x] = (uint8_t)u;
+            row[2 * x + 1] = (uint8_t)v;
+        } else {
+            uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[1]) + frame * dst.fstride + (int64_t)y * dst.pitch[1];
+            const int su = u << 6, sv = v << 6;
+            row[4 * x] = (uint8_t)su;
+            row[4 * x + 1] = (uint8_t)(su >> 8);
+            row[4 * x + 2] = (uint8_t)sv;
+            row[4 * x + 3] = (uint8_t)(sv >> 8);
+        }
+    }
+}
+
+hipError_t launch_synth(int w, int h, int fmt, int pattern, uint32_t seed, int64_t first, const DevPlanes &dst,
+                        int nframes, hipStream_t s)
+{
+    const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
+    const int quads_y = ((w + 3) >> 2) * h;
+    const int quads_c = ((cw + 3) >> 2) * ch;
+    const int blocks = (quads_y + quads_c + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks, (unsigned)nframes), dim3(kThreads), 0, s, w, h, fmt, pattern,
+                       seed, first, dst, quads_y, quads_c);
+    return hipGetLastError();
+}
+
+} // namespace dts

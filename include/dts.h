@@ -1,0 +1,202 @@
+/*
+ * dts.h -- C-ABI of the MI355X-native transcoding worker (libdts.so).
+ *
+ * Drop-in boundary for the reference's per-segment pixel path.  The reference
+ * (BadAimWeeb/distributed-transcoding-server) would get this path by spawning
+ * the ffmpeg binary whose path it resolves at index.js:9
+ * (`require("ffmpeg-static")`, ffmpeg 4.4.0 per package-lock.json:384-397)
+ * with a filtergraph built from the job row fields Jobs.width / height /
+ * framerate (database.js:73-75) for the segment JobChunks.chunkOffset
+ * (database.js:109).  The spawn/dispatch code itself is absent from the
+ * reference (index.js:13 constructs socket.io with no handlers), so each entry
+ * point below names the ffmpeg/libav* interface it replaces:
+ *
+ *   dts_graph_create   <- `-vf scale=W:H:flags=<m>+accurate_rnd+bitexact,
+ *                          format=<fmt>` / `-filter_complex split=N...`
+ *                          (vf_scale.c config_props -> sws_init_context)
+ *   dts_graph_submit   <- the per-frame filter_frame() of that graph
+ *   (+ _wait)             (vf_scale.c scale_frame -> sws_scale), plus the
+ *                          optional `psnr`/`ssim` filters against a reference
+ *   dts_quality_*      <- vf_psnr.c do_psnr / vf_ssim.c do_ssim
+ *   dts_fps_map        <- vf_fps.c frame selection (round=near)
+ *   dts_synth_*        <- `-f lavfi testsrc2` (synthetic source; testsrc2 itself
+ *                          needs ffmpeg, so this is a deterministic stand-in)
+ *
+ * Conventions: every call returns 0 (DTS_OK) or a negative DTS_E_* code and
+ * never throws or aborts across the ABI.  Plain pointers and sizes only.
+ * One dts_ctx per GPU; a ctx and its graphs are single-threaded (the caller
+ * serialises calls); distinct ctxs may be driven from different threads.
+ */
+#ifndef DTS_H
+#define DTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DTS_ABI_VERSION 1
+#define DTS_MAX_OUTPUTS 4
+
+/* error codes (AVERROR-style negative ints) */
+#define DTS_OK             0
+#define DTS_E_INVAL      (-22)   /* bad argument / spec */
+#define DTS_E_NOMEM      (-12)
+#define DTS_E_RANGE      (-34)   /* filter too large for the GPU tables */
+#define DTS_E_UNSUPPORTED (-95)  /* format / method combination not built */
+#define DTS_E_BUSY       (-16)   /* submit while a previous submit is pending */
+#define DTS_E_NODEV      (-19)   /* no HIP device */
+#define DTS_E_HIP      (-1000)   /* HIP runtime error; see dts_ctx_last_hip_error */
+
+/* pixel formats (yuv420p / nv12 / p010le as in libavutil/pixfmt.h) */
+#define DTS_FMT_YUV420P 0
+#define DTS_FMT_NV12    1
+#define DTS_FMT_P010LE  2
+
+/* scaling methods = libswscale SWS_* flag values (swscale.h) */
+#define DTS_SCALE_BILINEAR 0x2
+#define DTS_SCALE_BICUBIC  0x4
+#define DTS_SCALE_X        0x8
+#define DTS_SCALE_POINT    0x10
+#define DTS_SCALE_AREA     0x20
+#define DTS_SCALE_GAUSS    0x80
+#define DTS_SCALE_SINC     0x100
+#define DTS_SCALE_LANCZOS  0x200
+#define DTS_PARAM_DEFAULT  123456.0 /* SWS_PARAM_DEFAULT */
+
+/* quality checks (vf_psnr / vf_ssim) */
+#define DTS_Q_NONE 0
+#define DTS_Q_PSNR 1
+#define DTS_Q_SSIM 2
+#define DTS_Q_BOTH 3
+
+typedef struct dts_ctx dts_ctx;
+typedef struct dts_graph dts_graph;
+
+typedef struct dts_output_spec {
+    int32_t w, h;       /* output size (even for 4:2:0 not required) */
+    int32_t fmt;        /* DTS_FMT_YUV420P or DTS_FMT_NV12 */
+    int32_t method;     /* DTS_SCALE_*; always run as method|ACCURATE_RND|BITEXACT */
+    double param[2];    /* sws param[0..1]; DTS_PARAM_DEFAULT for defaults */
+} dts_output_spec;
+
+typedef struct dts_graph_spec {
+    int32_t src_w, src_h, src_fmt;      /* source segment frames */
+    int32_t nout;                       /* 1..DTS_MAX_OUTPUTS renditions */
+    dts_output_spec out[DTS_MAX_OUTPUTS];
+    int32_t quality;                    /* DTS_Q_* */
+    int32_t quality_out;                /* output index compared with qref */
+    int32_t max_batch;                  /* frames per device launch; 0 = 32 */
+} dts_graph_spec;
+
+/* host frame: plane p at data[p] with row pitch pitch[p] bytes.
+ * yuv420p: Y, U, V.  nv12 / p010le: Y, interleaved UV, (unused). */
+typedef struct dts_frame {
+    void *data[3];
+    int64_t pitch[3];
+} dts_frame;
+
+/* device-resident batch: frame f plane p at data[p] + f * frame_stride.
+ * Source pitches and plane bases must be multiples of 16 bytes, output
+ * pitches multiples of 4. */
+typedef struct dts_dev_frames {
+    void *data[3];
+    int64_t pitch[3];
+    int64_t frame_stride;
+} dts_dev_frames;
+
+/* raw per-frame quality record as produced on the device and gathered
+ * across GPUs (integer SSE exact; SSIM window sums in f64). */
+typedef struct dts_qraw {
+    uint64_t sse[3];
+    double ssim_sum[3];
+} dts_qraw;
+
+/* finished per-frame statistics, same meaning as the lavfi.psnr.* /
+ * lavfi.ssim.* frame metadata of vf_psnr.c / vf_ssim.c */
+typedef struct dts_qstat {
+    uint64_t sse[3];
+    double mse[3], mse_avg;
+    double psnr[3], psnr_avg;   /* +inf when mse == 0 */
+    double ssim[3], ssim_all, ssim_db;
+} dts_qstat;
+
+typedef struct dts_graph_info {
+    int64_t src_frame_bytes;            /* packed algorithmic bytes per source frame */
+    int64_t out_frame_bytes[DTS_MAX_OUTPUTS];
+    int64_t algo_bytes_per_frame;       /* read src once + write outputs (+ read qref) */
+    int32_t njobs;                      /* workgroups per frame in the ladder launch */
+    int32_t lds_bytes;                  /* dynamic LDS per workgroup */
+    int32_t h_taps[DTS_MAX_OUTPUTS][2]; /* GPU H tap span (luma, chroma) per output */
+    int32_t v_taps[DTS_MAX_OUTPUTS][2]; /* GPU V tap span (luma, chroma) per output */
+    int32_t sws_h_size[DTS_MAX_OUTPUTS][2]; /* libswscale filter sizes (luma, chroma) */
+    int32_t sws_v_size[DTS_MAX_OUTPUTS][2];
+} dts_graph_info;
+
+const char *dts_version(void);
+const char *dts_strerror(int err);
+
+int dts_device_count(int *count);
+int dts_ctx_create(int device, dts_ctx **out);
+void dts_ctx_destroy(dts_ctx *ctx);
+int dts_ctx_last_hip_error(const dts_ctx *ctx);
+
+int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out);
+void dts_graph_destroy(dts_graph *g);
+int dts_graph_info_get(const dts_graph *g, dts_graph_info *info);
+
+/* Host-memory path (the Node worker's path).  dst holds nframes*nout frames,
+ * frame-major (dst[f*nout + k]).  qref/q may be NULL when quality is off.
+ * The caller keeps every buffer alive until dts_graph_wait returns. */
+int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes,
+                     const dts_frame *dst, const dts_frame *qref, dts_qstat *q);
+int dts_graph_wait(dts_graph *g);
+
+/* Device-resident path: enqueue one batch on `stream` (a hipStream_t, NULL =
+ * the ctx's stream).  dst[k] is the batch of output k.  When the graph has
+ * quality on, qref is the reference batch for output quality_out and qraw
+ * receives nframes device-side dts_qraw records (device pointer). */
+int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes,
+                         const dts_dev_frames *dst, const dts_dev_frames *qref,
+                         dts_qraw *qraw_dev, void *stream);
+
+/* Standalone quality (vf_psnr + vf_ssim) on device-resident 8-bit 4:2:0
+ * batches (fmt yuv420p or nv12 for both a and b). */
+int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt,
+                           const dts_dev_frames *a, const dts_dev_frames *b,
+                           int nframes, dts_qraw *qraw_dev, void *stream);
+/* vf_psnr get_psnr / vf_ssim ssim_db finishing of raw records (host). */
+int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out);
+
+/* Synthetic deterministic source (testsrc2-like): pattern 0 = gradient +
+ * moving bars + seeded noise (limited range), 1 = uniform random full range. */
+int dts_synth_host(int w, int h, int fmt, int pattern, uint32_t seed,
+                   int64_t frame_index, const dts_frame *dst);
+int dts_synth_device(dts_ctx *ctx, int w, int h, int fmt, int pattern,
+                     uint32_t seed, int64_t first_frame,
+                     const dts_dev_frames *dst, int nframes, void *stream);
+
+/* Layout helper: bytes per plane for a tightly packed frame (pitch = row bytes). */
+int dts_frame_layout(int w, int h, int fmt, int64_t pitch[3], int64_t rows[3],
+                     int64_t *packed_bytes);
+
+/* Diagnostic: the libswscale filter (initFilter, SWS_BITEXACT|ACCURATE_RND,
+ * x86 filterAlign) that a graph builds for one direction of one plane.
+ * one = 1<<14 (horizontal) or 1<<12 (vertical); pos = get_local_pos() siting.
+ * Writes dst_n*cap int16 taps (row stride = returned size) and dst_n
+ * positions; returns the filter size (>0) or <0.  Needs no device. */
+int dts_sws_filter(int src_n, int dst_n, int one, int align, int method,
+                   const double param[2], int pos, int16_t *coeff, int32_t *filter_pos,
+                   int cap);
+
+/* vf_fps (round=near) frame index map for a constant-rate input starting at
+ * pts 0.  Returns the output frame count (<= cap written) or <0. */
+int64_t dts_fps_map(int64_t nb_in, int in_num, int in_den, int out_num,
+                    int out_den, int64_t *out_idx, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DTS_H */

@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "distributed-transcoding-server_amd")
+for p in (os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs via gpurun)")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    import dtsffi
+    if dtsffi.device_count() < 1:
+        pytest.fail("gpu test without a HIP device: the HIP path must run, there is no fallback")
+    c = dtsffi.Context(0)
+    yield c
+    c.close()

@@ -1,0 +1,137 @@
+"""GPU parity: the HIP ladder (scale + format convert) vs the CPU oracle.
+
+Bit-exact for every method (the GPU consumes the same integer tables the
+libswscale C path builds; the oracle restates that path).  Calls go through
+the C-ABI (libdts.so).  Oracle parity vs libswscale itself is unpinned: see
+DESIGN.md "Oracle".
+"""
+import numpy as np
+import pytest
+
+import dtsffi as D
+from _util import first_diff, oracle_frame, planes_equal, random_frame
+
+pytestmark = pytest.mark.gpu
+
+BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
+
+
+def run_and_check(ctx, sw, sh, sfmt, outs, frames):
+    g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, outs))
+    got, _ = g.run_host(frames)
+    for f, src in enumerate(frames):
+        for k, o in enumerate(outs):
+            want = oracle_frame(src, sw, sh, sfmt, o[0], o[1], o[2], o[3], o[4] if len(o) > 4 else
+                                (D.PARAM_DEFAULT, D.PARAM_DEFAULT))
+            assert planes_equal(got[f][k], want), f"frame {f} out {k} {o}: {first_diff(got[f][k], want)}"
+    g.close()
+
+
+@pytest.mark.parametrize("method", [BIC, BIL, LAN])
+def test_ladder_small(ctx, method):
+    """4K-ladder shape at 1/10 scale: 384x216 -> 192x108 / 128x72 / 86x48 nv12."""
+    frames = [D.synth_host(384, 216, D.FMT_YUV420P, 0, 0x5EED, f) for f in range(3)]
+    outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_NV12, method), (86, 48, D.FMT_NV12, method)]
+    run_and_check(ctx, 384, 216, D.FMT_YUV420P, outs, frames)
+
+
+@pytest.mark.parametrize("sw,sh,dw,dh", [(37, 23, 19, 11), (64, 36, 32, 18), (100, 60, 150, 90),
+                                         (333, 211, 97, 55), (640, 360, 1280, 720), (1000, 8, 300, 5),
+                                         (17, 300, 40, 41)])
+@pytest.mark.parametrize("method", [BIC, BIL, LAN, D.SCALE_POINT, D.SCALE_AREA, D.SCALE_GAUSS])
+def test_odd_sizes_random(ctx, sw, sh, dw, dh, method):
+    rng = np.random.default_rng(sw * 1000 + dh + method)
+    frames = [random_frame(sw, sh, D.FMT_YUV420P, rng) for _ in range(2)]
+    run_and_check(ctx, sw, sh, D.FMT_YUV420P, [(dw, dh, D.FMT_YUV420P, method), (dw, dh, D.FMT_NV12, method)],
+                  frames)
+
+
+@pytest.mark.parametrize("sfmt", [D.FMT_NV12, D.FMT_P010LE])
+@pytest.mark.parametrize("method", [BIC, LAN, BIL])
+def test_semiplanar_sources(ctx, sfmt, method):
+    rng = np.random.default_rng(7 + sfmt)
+    frames = [random_frame(258, 146, sfmt, rng), D.synth_host(258, 146, sfmt, 0, 3, 5)]
+    run_and_check(ctx, 258, 146, sfmt, [(130, 74, D.FMT_NV12, method), (97, 51, D.FMT_YUV420P, method),
+                                        (258, 146, D.FMT_YUV420P, method)], frames)
+
+
+def test_same_size_identity(ctx):
+    """1:1 luma is the identity, yuv420p -> nv12 is a lossless interleave."""
+    rng = np.random.default_rng(1)
+    src = random_frame(130, 66, D.FMT_YUV420P, rng)
+    g = D.Graph(ctx, D.make_spec(130, 66, D.FMT_YUV420P, [(130, 66, D.FMT_NV12, BIC)]))
+    (out,), _ = g.run_host([src])
+    out = out[0]
+    assert np.array_equal(out[0], src[0])
+    assert np.array_equal(out[1][:, 0::2], src[1]) and np.array_equal(out[1][:, 1::2], src[2])
+
+
+def test_params_bicubic_b_c(ctx):
+    frames = [D.synth_host(200, 120, D.FMT_YUV420P, 1, 11, 0)]
+    run_and_check(ctx, 200, 120, D.FMT_YUV420P, [(90, 50, D.FMT_NV12, BIC, (1 / 3, 1 / 3)),
+                                                 (90, 50, D.FMT_NV12, LAN, (2.0, D.PARAM_DEFAULT))], frames)
+
+
+def test_ladder_4k_one_frame(ctx):
+    """BASELINE config 2 geometry at full size, one frame, bit-exact."""
+    frames = [D.synth_host(3840, 2160, D.FMT_YUV420P, 0, 0x5EED, 0)]
+    outs = [(1920, 1080, D.FMT_NV12, BIC), (1280, 720, D.FMT_NV12, BIC), (854, 480, D.FMT_NV12, BIC)]
+    run_and_check(ctx, 3840, 2160, D.FMT_YUV420P, outs, frames)
+
+
+def test_p010_4k_to_1080p(ctx):
+    """BASELINE config 3 geometry (scale/convert part): 4K p010 -> 1080p yuv420p with ordered dither."""
+    frames = [D.synth_host(3840, 2160, D.FMT_P010LE, 0, 0x5EED, 0)]
+    run_and_check(ctx, 3840, 2160, D.FMT_P010LE, [(1920, 1080, D.FMT_YUV420P, BIC)], frames)
+
+
+def test_many_frames_batches(ctx):
+    """More frames than one batch; both pinned slots cycle."""
+    frames = [D.synth_host(160, 90, D.FMT_YUV420P, 0, 9, f) for f in range(11)]
+    g = D.Graph(ctx, D.make_spec(160, 90, D.FMT_YUV420P, [(80, 46, D.FMT_NV12, BIC)], max_batch=4))
+    got, _ = g.run_host(frames)
+    for f, src in enumerate(frames):
+        want = oracle_frame(src, 160, 90, D.FMT_YUV420P, 80, 46, D.FMT_NV12, BIC)
+        assert planes_equal(got[f][0], want), first_diff(got[f][0], want)
+
+
+def test_device_path_matches_host_path(ctx):
+    """dts_graph_run_device on torch-allocated HBM == the host path."""
+    import torch
+    w, h = 640, 360
+    outs = [(320, 180, D.FMT_NV12, BIC), (216, 120, D.FMT_NV12, BIC)]
+    g = D.Graph(ctx, D.make_spec(w, h, D.FMT_YUV420P, outs))
+    n = 5
+    src = torch.empty((n, h * w + 2 * ((w + 1) // 2) * ((h + 1) // 2) + 64), dtype=torch.uint8, device="cuda")
+    fstride = src.stride(0)
+    assert fstride % 16 == 0
+    base = src.data_ptr()
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    sf = D.DevFrames()
+    sf.data[0], sf.data[1], sf.data[2] = base, base + h * w, base + h * w + cw * ch
+    sf.pitch[0], sf.pitch[1], sf.pitch[2] = w, cw, cw
+    sf.frame_stride = fstride
+    # cw = 320 and plane offsets are multiples of 16 for this geometry
+    ctx.synth_device(w, h, D.FMT_YUV420P, 0, 42, 0, sf, n, torch.cuda.current_stream().cuda_stream)
+    dsts, bufs = [], []
+    for (ow, oh, of, _m) in outs:
+        size = ow * oh + 2 * ((ow + 1) // 2) * ((oh + 1) // 2)
+        b = torch.empty((n, size + 60), dtype=torch.uint8, device="cuda")
+        d = D.DevFrames()
+        d.data[0], d.data[1], d.data[2] = b.data_ptr(), b.data_ptr() + ow * oh, 0
+        d.pitch[0], d.pitch[1], d.pitch[2] = ow, 2 * ((ow + 1) // 2), 0
+        d.frame_stride = b.stride(0)
+        dsts.append(d)
+        bufs.append(b)
+    g.run_device(sf, n, dsts, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for f in range(n):
+        host_src = D.synth_host(w, h, D.FMT_YUV420P, 0, 42, f)
+        got_src = src[f].cpu().numpy()
+        assert np.array_equal(got_src[:h * w].reshape(h, w), host_src[0]), "device synth != host synth"
+        for k, (ow, oh, of, m) in enumerate(outs):
+            raw = bufs[k][f].cpu().numpy()
+            y = raw[:ow * oh].reshape(oh, ow)
+            uv = raw[ow * oh: ow * oh + 2 * ((ow + 1) // 2) * ((oh + 1) // 2)].reshape((oh + 1) // 2, -1)
+            want = oracle_frame(host_src, w, h, D.FMT_YUV420P, ow, oh, of, m)
+            assert planes_equal([y, uv, None], want), first_diff([y, uv, None], want)

@@ -1,0 +1,96 @@
+"""GPU parity: vf_psnr / vf_ssim kernels vs the CPU oracle.
+
+SSE (hence MSE/PSNR) is integer-exact.  SSIM: per-window values are the same
+f32 expression as vf_ssim.c; only the summation order differs (f64 on the
+GPU), so the tolerance is the north-star 1e-4 (absolute on SSIM).
+"""
+import numpy as np
+import pytest
+
+import dtsffi as D
+import orc
+from _util import random_frame
+
+pytestmark = pytest.mark.gpu
+SSIM_TOL = 1e-4
+
+
+def check_q(got, want):
+    assert got["sse"] == want["sse"]
+    for c in range(3):
+        if np.isnan(want["ssim"][c]):
+            assert np.isnan(got["ssim"][c])
+            continue
+        assert got["ssim"][c] == pytest.approx(want["ssim"][c], abs=SSIM_TOL)
+        if np.isinf(want["psnr"][c]):
+            assert np.isinf(got["psnr"][c])
+        else:
+            assert got["psnr"][c] == pytest.approx(want["psnr"][c], rel=1e-12)
+    if not np.isnan(want["ssim_all"]):
+        assert got["ssim_all"] == pytest.approx(want["ssim_all"], abs=SSIM_TOL)
+
+
+@pytest.mark.parametrize("w,h", [(64, 36), (37, 23), (258, 146), (1001, 67), (8, 8), (4, 4)])
+def test_quality_vs_oracle(ctx, w, h):
+    import torch
+    rng = np.random.default_rng(w * h)
+    fr_a = [random_frame(w, h, D.FMT_YUV420P, rng) for _ in range(3)]
+    fr_b = [[np.clip(p.astype(np.int16) + rng.integers(-6, 7, p.shape), 0, 255).astype(np.uint8) for p in f]
+            for f in fr_a]
+    fr_b[1] = [p.copy() for p in fr_a[1]]          # identical frame -> inf PSNR, SSIM 1
+    got = gpu_quality(ctx, w, h, fr_a, fr_b, torch)
+    for i in range(3):
+        want = orc.quality_frame(w, h, fr_a[i], fr_b[i])
+        check_q(got[i], want)
+    assert got[1]["ssim_all"] == pytest.approx(1.0, abs=1e-12) or w < 8 or h < 8
+
+
+def gpu_quality(ctx, w, h, fa, fb, torch):
+    n = len(fa)
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    pitch = [(w + 15) // 16 * 16, (cw + 15) // 16 * 16, (cw + 15) // 16 * 16]
+    rows = [h, ch, ch]
+    offs = [0, pitch[0] * h, pitch[0] * h + pitch[1] * ch]
+    fsz = offs[2] + pitch[2] * ch
+
+    def upload(frames):
+        host = np.zeros((n, fsz), np.uint8)
+        for f, planes in enumerate(frames):
+            for p in range(3):
+                img = host[f, offs[p]:offs[p] + pitch[p] * rows[p]].reshape(rows[p], pitch[p])
+                img[:, :planes[p].shape[1]] = planes[p]
+        t = torch.from_numpy(host).cuda()
+        d = D.DevFrames()
+        for p in range(3):
+            d.data[p] = t.data_ptr() + offs[p]
+            d.pitch[p] = pitch[p]
+        d.frame_stride = fsz
+        return t, d
+    ta, da = upload(fa)
+    tb, db = upload(fb)
+    raw = torch.zeros((n, 6), dtype=torch.float64, device="cuda")   # 6 x 8 bytes = dts_qraw
+    ctx.quality_device(w, h, D.FMT_YUV420P, da, db, n, raw.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    host = raw.cpu().numpy()
+    recs = []
+    for i in range(n):
+        r = D.QRaw()
+        b = host[i].tobytes()
+        import ctypes
+        ctypes.memmove(ctypes.addressof(r), b, ctypes.sizeof(r))
+        recs.append(r)
+    return D.qstat_finalize(w, h, recs)
+
+
+def test_graph_quality_host_path(ctx):
+    """cfg-4 shape at small scale: lanczos 2:1 + PSNR/SSIM vs a reference rendition."""
+    sw, sh, w, h = 512, 288, 256, 144
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 5, f) for f in range(4)]
+    ref = [orc.scale_frame(f, sw, sh, 0, w, h, 0, D.SCALE_BICUBIC) for f in frames]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, [(w, h, D.FMT_YUV420P, D.SCALE_LANCZOS)],
+                                 quality=D.Q_BOTH, quality_out=0))
+    outs, qs = g.run_host(frames, qref=ref)
+    for f in range(4):
+        want_img = orc.scale_frame(frames[f], sw, sh, 0, w, h, 0, D.SCALE_LANCZOS)
+        assert all(np.array_equal(a, b) for a, b in zip(outs[f][0], want_img))
+        check_q(qs[f], orc.quality_frame(w, h, want_img, ref[f]))

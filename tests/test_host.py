@@ -1,0 +1,104 @@
+"""CPU: the product's host-side logic (libdts.so, no device needed) vs the oracle.
+
+- filter tables: dts_sws_filter (the tables every graph uploads) must equal the
+  oracle's initFilter restatement tap for tap;
+- fps map, synthetic source determinism, frame layout, qstat finishing.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import dtsffi as D
+import orc
+
+METHODS = [D.SCALE_BILINEAR, D.SCALE_BICUBIC, D.SCALE_LANCZOS, D.SCALE_POINT, D.SCALE_AREA, D.SCALE_GAUSS,
+           D.SCALE_SINC, D.SCALE_X]
+SIZES = [(3840, 1920), (3840, 1280), (3840, 854), (1920, 960), (1920, 640), (1920, 427), (2160, 1080),
+         (2160, 720), (2160, 480), (1080, 540), (1080, 360), (1080, 240), (7680, 3840), (4320, 2160),
+         (1920, 1280), (1080, 720), (640, 1280), (37, 19), (23, 11), (100, 150), (9, 20), (8, 5), (1000, 300)]
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_filter_tables_match_oracle(method):
+    for src, dst in SIZES:
+        for one, align in ((1 << 14, 4), (1 << 12, 2)):
+            for pos in (128,):
+                try:
+                    want_c, want_p = orc.init_filter(src, dst, method, one=one, align=align, pos=pos)
+                except RuntimeError:
+                    with pytest.raises(D.DtsError):
+                        D.sws_filter(src, dst, one, align, method, pos=pos)
+                    continue
+                got_c, got_p = D.sws_filter(src, dst, one, align, method, pos=pos)
+                assert got_c.shape == want_c.shape, (src, dst, one)
+                assert np.array_equal(got_c, want_c), (src, dst, one)
+                assert np.array_equal(got_p, want_p), (src, dst, one)
+
+
+def test_filter_params():
+    for par in ((1 / 3, 1 / 3), (0.0, 0.75), (D.PARAM_DEFAULT, 0.5)):
+        a, ap = orc.init_filter(1920, 1280, D.SCALE_BICUBIC, param=par)
+        b, bp = D.sws_filter(1920, 1280, 1 << 14, 4, D.SCALE_BICUBIC, param=par)
+        assert np.array_equal(a, b) and np.array_equal(ap, bp)
+    for p0 in (2.0, 4.0, 5.0):
+        a, _ = orc.init_filter(1920, 640, D.SCALE_LANCZOS, param=(p0, D.PARAM_DEFAULT))
+        b, _ = D.sws_filter(1920, 640, 1 << 14, 4, D.SCALE_LANCZOS, param=(p0, D.PARAM_DEFAULT))
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("rates", [((60, 1), (30, 1)), ((30, 1), (60, 1)), ((24000, 1001), (30, 1)),
+                                   ((30000, 1001), (24, 1)), ((25, 1), (29.97, 1))])
+def test_fps_map_matches_oracle(rates):
+    (a, b), (c, d) = rates
+    if isinstance(c, float):
+        c, d = 30000, 1001
+    for n in (0, 1, 7, 600, 1001):
+        got = D.fps_map(n, (a, b), (c, d))
+        want = orc.fps_map(n, (a, b), (c, d)) if n else np.zeros(0, np.int64)
+        assert np.array_equal(got, want), (n, rates)
+
+
+@pytest.mark.parametrize("fmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
+def test_synth_deterministic_and_in_range(fmt):
+    a = D.synth_host(130, 71, fmt, 0, 0x5EED, 3)
+    b = D.synth_host(130, 71, fmt, 0, 0x5EED, 3)
+    c = D.synth_host(130, 71, fmt, 0, 0x5EED, 4)
+    assert all(np.array_equal(x, y) for x, y in zip(a, b) if x is not None)
+    assert not np.array_equal(a[0], c[0])
+    if fmt == D.FMT_P010LE:
+        y = a[0].view(np.uint16)
+        assert np.all((y & 63) == 0) and (y >> 6).min() >= 64 and (y >> 6).max() <= 940
+    else:
+        assert a[0].min() >= 16 and a[0].max() <= 235
+
+
+def test_frame_layout():
+    import ctypes
+    pitch = (ctypes.c_int64 * 3)()
+    rows = (ctypes.c_int64 * 3)()
+    packed = ctypes.c_int64()
+    D.check(D.lib().dts_frame_layout(3840, 2160, D.FMT_YUV420P, pitch, rows, ctypes.byref(packed)))
+    assert packed.value == 12441600
+    D.check(D.lib().dts_frame_layout(1920, 1080, D.FMT_NV12, pitch, rows, ctypes.byref(packed)))
+    assert packed.value == 3110400 and list(pitch)[:2] == [1920, 1920]
+    D.check(D.lib().dts_frame_layout(3840, 2160, D.FMT_P010LE, pitch, rows, ctypes.byref(packed)))
+    assert packed.value == 24883200
+    assert D.lib().dts_frame_layout(0, 10, 0, pitch, rows, None) == D.E_INVAL
+
+
+def test_qstat_finalize_matches_vf_psnr_vf_ssim():
+    r = D.QRaw()
+    w, h = 64, 48
+    r.sse[0], r.sse[1], r.sse[2] = 64 * 48, 0, 32 * 24 * 4
+    r.ssim_sum[0], r.ssim_sum[1], r.ssim_sum[2] = 0.9 * 15 * 11, 7 * 5 * 1.0, 0.5 * 35
+    q = D.qstat_finalize(w, h, [r])[0]
+    assert q["mse"] == [1.0, 0.0, 4.0]
+    assert q["psnr"][0] == pytest.approx(10 * math.log10(255 ** 2)) and math.isinf(q["psnr"][1])
+    area = 64 * 48 * 1.5
+    mse = (1.0 * 64 * 48 + 0 + 4.0 * 32 * 24) / area
+    assert q["mse_avg"] == pytest.approx(mse)
+    assert q["psnr_avg"] == pytest.approx(10 * math.log10(255 ** 2 / mse))
+    assert q["ssim"] == pytest.approx([0.9, 1.0, 0.5])
+    ssim = (0.9 * 64 * 48 + 1.0 * 32 * 24 + 0.5 * 32 * 24) / area
+    assert q["ssim_all"] == pytest.approx(ssim) and q["ssim_db"] == pytest.approx(-10 * math.log10(1 - ssim))

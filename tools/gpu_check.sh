@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: warm torch, parity tests, smoke, short bench.
+# Stops at the first step that ends with a signal / timeout / abort
+# (exit >= 124 or a negative python status); plain test failures (exit 1)
+# do not stop the later steps.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name, timeout, command...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "=== stopping after $name (rc=$rc)"; exit $rc
+  fi
+  return 0
+}
+step warm 240 python -c "import torch; print(torch.__version__, torch.cuda.is_available(), torch.cuda.get_device_name(0))"
+for s in "$@"; do
+  case $s in
+    tests)  step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    quick)  step tests_quick 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "small or quality or identity or device_path" ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 300 python -u bench.py --steps 20 --warmup 3 ;;
+    benchq) step benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
