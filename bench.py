@@ -89,6 +89,37 @@ def cpu_baseline(budget_s, threads):
                       "ffmpeg is not installed on the box"}
 
 
+def hip_runtimes():
+    """Which libamdhip64 files this process mapped (must be exactly one)."""
+    libs = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                libs.add(line.split()[-1])
+    return sorted(libs)
+
+
+def verify_first_frame(src_index, outs):
+    """Bit-exact check of frame 0 of the last batch against the CPU oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import orc
+    host = D.synth_host(SRC_W, SRC_H, D.FMT_YUV420P, 0, 0x5EED, src_index)
+    for k, (w, h, fmt, m) in enumerate(LADDER):
+        want = orc.scale_frame(host, SRC_W, SRC_H, 0, w, h, fmt, m)
+        raw = outs[k][0].cpu().numpy()
+        off = 0
+        for p, shp in enumerate(D.plane_shapes(w, h, fmt)):
+            if shp is None:
+                continue
+            pitch = (shp[1] + 255) // 256 * 256
+            plane = raw[off:off + pitch * shp[0]].reshape(shp[0], pitch)[:, :shp[1]]
+            off += pitch * shp[0]
+            if not np.array_equal(plane, want[p]):
+                return False
+    return True
+
+
 def load_traffic():
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(ROOT, "profiles", "pmc_ladder.json")
@@ -111,6 +142,7 @@ def main():
     ap.add_argument("--ring", type=int, default=96, help="device-resident source frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,10 +152,16 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)          # a real (non-null) HIP stream shared by torch events and libdts
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    assert sptr, "libdts needs a non-null stream handle"
 
+    torch.zeros(1, device=dev)           # initialise torch's HIP runtime before libdts loads
     ctx = D.Context(local)
+    runtimes = hip_runtimes()
+    if len(runtimes) != 1:
+        print(f"WARNING: {len(runtimes)} HIP runtimes mapped: {runtimes}", file=sys.stderr)
     g = D.Graph(ctx, D.make_spec(SRC_W, SRC_H, D.FMT_YUV420P, LADDER))
     info = g.info
     B, R = args.batch, max(args.ring, 2 * args.batch)
@@ -184,6 +222,10 @@ def main():
         frames_total = int(rec[0].item())
     wall_max = float(wall_t.item())
 
+    verified = None
+    if rank == 0 and not args.no_verify:
+        last = args.warmup + args.steps - 1
+        verified = verify_first_frame(first + (last * B) % R, outs)
     if rank == 0:
         fps = frames_total / wall_max
         algo = info.algo_bytes_per_frame
@@ -200,6 +242,7 @@ def main():
                                                                       "854x480 nv12"],
                        "batch_frames": B, "parallelism": f"segments x{world} (one process per GPU)"},
             "mpixel_per_s": round(fps * SRC_W * SRC_H / 1e6, 1),
+            "verified_vs_oracle": verified, "hip_runtime": runtimes,
             "algo_bytes_per_frame": algo,
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),

@@ -734,12 +734,13 @@ static int finish_slot(dts_graph *g, int sl)
     const dts_graph_spec &s = g->spec;
     HIPCHK(ctx, hipEventSynchronize(g->done[sl]));
     const int f0 = g->p_chunk_first[sl], n = g->p_chunk_n[sl];
-    const uint8_t *hp = g->pin_out[sl];
-    for (int k = 0; k < s.nout; ++k)
-        for (int f = 0; f < n; ++f) {
-            unpack_frame(hp, g->p_dst[(int64_t)(f0 + f) * s.nout + k], s.out[k].w, s.out[k].h, s.out[k].fmt);
-            hp += g->info.out_frame_bytes[k];
-        }
+    const uint8_t *hp = g->pin_out[sl];          // per output: a region of `batch` packed frames
+    for (int k = 0; k < s.nout; ++k) {
+        for (int f = 0; f < n; ++f)
+            unpack_frame(hp + (int64_t)f * g->info.out_frame_bytes[k], g->p_dst[(int64_t)(f0 + f) * s.nout + k],
+                         s.out[k].w, s.out[k].h, s.out[k].fmt);
+        hp += (int64_t)g->batch * g->info.out_frame_bytes[k];
+    }
     if (s.quality && g->p_q) {
         const dts_output_spec &o = s.out[s.quality_out];
         dts_qstat_finalize(o.w, o.h, g->pin_qraw[sl], n, g->p_q + f0);

@@ -20,6 +20,15 @@ constexpr int kChromaCols = 128;   // output columns per chroma strip (U: t<128,
 constexpr int kMaxLoads = 4;       // uint4 staging loads per thread per step
 constexpr int kMaxRungs = DTS_MAX_OUTPUTS;
 
+// H tap-dword counts the ladder kernel has unrolled code for; the host pads a
+// filter's packed window with zero taps up to the next one.
+inline int ladder_nd_round(int nd)
+{
+    if (nd <= 8) return nd < 1 ? 1 : nd;
+    if (nd <= 16) return (nd + 1) & ~1;
+    return nd;              // > 16: rejected at graph creation
+}
+
 // source kinds: what the staging loads unpack
 enum SrcKind : int { kSrcPlanar8 = 0, kSrcNV12 = 1, kSrcP010 = 2 };
 

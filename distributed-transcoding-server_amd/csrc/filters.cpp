@@ -273,7 +273,7 @@ int pack_h_u8(const SwsFilter &f, int n, HTable &out)
         start[i] = (f.pos[i] + j0) & ~3;
         span = std::max(span, f.pos[i] + j1 - start[i] + 1);
     }
-    const int nd = (span + 3) / 4;
+    const int nd = ladder_nd_round((span + 3) / 4);
     out.nd = nd;
     out.span = span;
     out.pos = start;
@@ -311,7 +311,7 @@ int pack_h_p010(const SwsFilter &f, int n, HTable &out)
         start[i] = (f.pos[i] + j0) & ~1;
         span = std::max(span, f.pos[i] + j1 - start[i] + 1);
     }
-    const int nd = (span + 1) / 2;
+    const int nd = ladder_nd_round((span + 1) / 2);
     out.nd = nd;
     out.span = span;
     out.pos = start;

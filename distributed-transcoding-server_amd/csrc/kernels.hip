@@ -26,6 +26,16 @@ namespace dts {
 __constant__ uint8_t c_dither[8][8] = DTS_DITHER_8X8_128;
 
 typedef short short2v __attribute__((ext_vector_type(2)));
+// global (address space 1) views: keeps VMEM traffic off the flat path so LDS
+// waits (lgkmcnt) and global waits (vmcnt) stay independent
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+typedef __attribute__((address_space(1))) const int32_t g_ci32;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+#define GPTR(T, p) ((T *)(uintptr_t)(p))
 
 __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c)
 {
@@ -48,9 +58,45 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // ---------------------------------------------------------------------------
 // k_ladder
 // ---------------------------------------------------------------------------
+constexpr int kVPre = 4;     // output rows per wave whose V data is prefetched per step
+
+// Horizontal FIR of one thread's output column over the kBlkRows staged rows.
+// ND is a compile-time tap-dword count so every LDS read of a row issues
+// before the first dot product consumes it.
+template <int SRC, int ND, int NDMAX>
+__device__ __forceinline__ void hrows(const uint8_t *s, int swb, const uint32_t (&ch)[NDMAX],
+                                      const uint32_t (&cl)[NDMAX], int bias, int (&hv)[kBlkRows])
+{
+#pragma unroll
+    for (int r = 0; r < kBlkRows; ++r) {
+        const uint32_t *rp = reinterpret_cast<const uint32_t *>(s + r * swb);
+        uint32_t v[ND];
+#pragma unroll
+        for (int k = 0; k < ND; ++k) v[k] = rp[k];
+        int val;
+        if (SRC == kSrcP010) {
+            int a = 0;
+#pragma unroll
+            for (int k = 0; k < ND; ++k) a = dot2(v[k], ch[k], a);
+            val = a >> 9;                                   // hScale16To15: sh = depth - 1
+        } else {
+            int a = 0, c = bias;
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                a = dot4(v[k], ch[k], a);
+                c = dot4(v[k], cl[k], c);
+            }
+            val = (a * 256 + c) >> 7;                       // hScale8To15 (src ^ 0x80 bias folded in c)
+        }
+        hv[r] = val < 32767 ? val : 32767;
+    }
+}
+
 template <int SRC, int NDMAX>
 __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
 {
@@ -75,10 +121,10 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     const int n16 = swb >> 4;                        // 16-B chunks per row per plane
     const bool inter_chroma = kind && (SRC != kSrcPlanar8);
     const int per_row = inter_chroma ? 2 * n16 : n16;
-    const int pln = kind ? (SRC == kSrcPlanar8 ? 1 : 1) : 0;
-    const int64_t pitch = P.src.pitch[kind ? 1 : 0];
+    const int pln = kind ? 1 : 0;
+    const int64_t pitch = P.src.pitch[pln];
     const int64_t fbase = (int64_t)frame * P.src.fstride;
-    const uint8_t *gptr[kMaxLoads];
+    uint64_t gaddr[kMaxLoads];
     int srow[kMaxLoads], sofs[kMaxLoads];
     bool sok[kMaxLoads];
 #pragma unroll
@@ -94,18 +140,13 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
             plane += pr / kBlkRows;
             row = pr % kBlkRows;
         }
-        int64_t boff;        // byte offset of the chunk inside the source row
-        if (!inter_chroma)
-            boff = (int64_t)J.sx0 * (SRC == kSrcP010 ? 2 : 1) + 16 * c;
-        else
-            boff = (int64_t)J.sx0 * (SRC == kSrcP010 ? 4 : 2) + 16 * c;
-        gptr[k] = reinterpret_cast<const uint8_t *>(P.src.data[plane]) + fbase + row * P.src.pitch[plane] + boff;
+        if (plane > 2) plane = 2;
+        const int64_t boff = (int64_t)J.sx0 * (inter_chroma ? (SRC == kSrcP010 ? 4 : 2) : (SRC == kSrcP010 ? 2 : 1)) +
+                             16 * c;
+        gaddr[k] = P.src.data[plane] + fbase + row * P.src.pitch[plane] + boff;
         srow[k] = row;
         sok[k] = (i < J.nload) && (boff + 16 <= P.src.pitch[plane]);
-        if (inter_chroma)
-            sofs[k] = row * swb + 8 * c;                 // U at +0, V at +plane_stage
-        else
-            sofs[k] = (plane - pln) * plane_stage + row * swb + 16 * c;
+        sofs[k] = inter_chroma ? row * swb + 8 * c : (plane - pln) * plane_stage + row * swb + 16 * c;
     }
     const int64_t rowstep = (int64_t)kBlkRows * pitch;
 
@@ -113,10 +154,11 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     auto issue = [&](int b) {
 #pragma unroll
         for (int k = 0; k < kMaxLoads; ++k) {
-            if (sok[k] && b * kBlkRows + srow[k] < srcH)
-                pre[k] = *reinterpret_cast<const uint4 *>(gptr[k] + b * rowstep);
-            else
-                pre[k] = make_uint4(0, 0, 0, 0);
+            pre[k] = make_uint4(0, 0, 0, 0);
+            if (sok[k] && b * kBlkRows + srow[k] < srcH) {
+                const u32x4 v = *GPTR(g_cu32x4, gaddr[k] + b * rowstep);
+                pre[k] = make_uint4(v.x, v.y, v.z, v.w);
+            }
         }
     };
     auto commit = [&](uint8_t *stage) {
@@ -162,55 +204,44 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     const int hcol = kind ? (t & (kChromaCols - 1)) : t;
     const bool hact = hcol < J.ncols;
     const int hx = J.x0 + (hact ? hcol : 0);
+    const int nd = K.nd;
     uint32_t chv[NDMAX], clv[NDMAX];
     int bias = 0, lofs = 0;
     {
-        const int p = K.hpos[hx];
-        bias = SRC == kSrcP010 ? 0 : K.hbias[hx];
+        const int p = GPTR(g_ci32, K.hpos)[hx];
+        bias = SRC == kSrcP010 ? 0 : GPTR(g_ci32, K.hbias)[hx];
         lofs = hplane * plane_stage + (p - J.sx0) * (SRC == kSrcP010 ? 2 : 1);
 #pragma unroll
         for (int k = 0; k < NDMAX; ++k) {
-            chv[k] = k < K.nd ? K.hch[(int64_t)k * K.dstW + hx] : 0u;
-            clv[k] = (SRC != kSrcP010 && k < K.nd) ? K.hcl[(int64_t)k * K.dstW + hx] : 0u;
+            chv[k] = k < nd ? GPTR(g_cu32, K.hch)[(int64_t)k * K.dstW + hx] : 0u;
+            clv[k] = (SRC != kSrcP010 && k < nd) ? GPTR(g_cu32, K.hcl)[(int64_t)k * K.dstW + hx] : 0u;
         }
     }
-    const int nd = K.nd;
 
     auto hpass = [&](int b, const uint8_t *stage) {
         if (!hact) return;
+        int hv[kBlkRows];
+        const uint8_t *s = stage + lofs;
+        switch (nd) {                                        // wave-uniform
+#define DTS_HCASE(N)                                                           \
+    case N:                                                                    \
+        if (N <= NDMAX) hrows<SRC, (N <= NDMAX ? N : 1), NDMAX>(s, swb, chv, clv, bias, hv); \
+        break;
+            DTS_HCASE(1) DTS_HCASE(2) DTS_HCASE(3) DTS_HCASE(4) DTS_HCASE(5) DTS_HCASE(6) DTS_HCASE(7)
+            DTS_HCASE(8) DTS_HCASE(10) DTS_HCASE(12) DTS_HCASE(14) DTS_HCASE(16)
+#undef DTS_HCASE
+        default:
+            break;
+        }
 #pragma unroll
         for (int pr = 0; pr < kBlkRows / 2; ++pr) {
-            int hv[2];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const uint32_t *rp = reinterpret_cast<const uint32_t *>(stage + lofs + (2 * pr + s) * swb);
-                int val;
-                if (SRC == kSrcP010) {
-                    int a = 0;
-#pragma unroll
-                    for (int k = 0; k < NDMAX; ++k)
-                        if (k < nd) a = dot2(rp[k], chv[k], a);
-                    val = a >> 9;                                   // hScale16To15: sh = depth - 1
-                } else {
-                    int a = 0, c = bias;
-#pragma unroll
-                    for (int k = 0; k < NDMAX; ++k)
-                        if (k < nd) {
-                            const uint32_t v = rp[k];
-                            a = dot4(v, chv[k], a);
-                            c = dot4(v, clv[k], c);
-                        }
-                    val = (a * 256 + c) >> 7;                       // hScale8To15
-                }
-                hv[s] = val < 32767 ? val : 32767;
-            }
             const int slot = (b * (kBlkRows / 2) + pr) & (RP - 1);
-            ring[(hplane * RP + slot) * pcols + hcol] = (uint32_t)(hv[0] & 0xffff) | ((uint32_t)hv[1] << 16);
+            ring[(hplane * RP + slot) * pcols + hcol] = (uint32_t)(hv[2 * pr] & 0xffff) | ((uint32_t)hv[2 * pr + 1] << 16);
         }
     };
 
-    // ---- vertical: one output row per wave, wave-uniform coefficients ----
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    // ---- vertical: one output row per wave, coefficients via v_readlane ---
+    const int wave = uniform(t >> 6);
     const int lane = t & 63;
     const int rung = J.rung;
     DevPlanes dst = P.dst[0];
@@ -220,101 +251,152 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     if (rung == 3) { dst = P.dst[3]; dfmt = P.dst_fmt[3]; }
     const int64_t dbase = (int64_t)frame * dst.fstride;
     const bool hidepth = SRC == kSrcP010;
+    const int nv = K.nv;
+    const int nvl = lane < nv ? lane : nv - 1;
 
-    auto vpass = [&](int b) {
-        const int vlo = b ? K.vlim[b - 1] : 0;
-        const int vhi = K.vlim[b];
-        for (int y = vlo + wave; y < vhi; y += kThreads / 64) {
-            const int q0 = K.vpos[y] >> 1;
-            const uint32_t *vc = K.vcoef + (int64_t)y * K.nv;
-            if (kind == 0) {
-                const int c0 = 4 * lane;
-                int d[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) d[i] = (hidepth ? c_dither[y & 7][(c0 + i) & 7] : 64) << 12;
-                int a0 = d[0], a1 = d[1], a2 = d[2], a3 = d[3];
-                for (int k = 0; k < K.nv; ++k) {
-                    const int slot = (q0 + k) & (RP - 1);
-                    const uint4 v = *reinterpret_cast<const uint4 *>(ring + slot * kLumaCols + c0);
-                    const uint32_t c = vc[k];
-                    a0 = dot2(v.x, c, a0);
-                    a1 = dot2(v.y, c, a1);
-                    a2 = dot2(v.z, c, a2);
-                    a3 = dot2(v.w, c, a3);
-                }
-                const uint32_t o = clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24);
-                uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[0]) + dbase + (int64_t)y * dst.pitch[0] + J.x0;
-                if (c0 + 3 < J.ncols) {
-                    *reinterpret_cast<uint32_t *>(row + c0) = o;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (c0 + i < J.ncols) row[c0 + i] = (uint8_t)(o >> (8 * i));
-                }
+    // one output row y (wave-uniform) from the ring; cq: lane k holds tap pair k
+    auto vrow = [&](int y, int q0, uint32_t cq) {
+        if (kind == 0) {
+            const int c0 = 4 * lane;
+            int a0, a1, a2, a3;
+            if (hidepth) {
+                a0 = c_dither[y & 7][(c0 + 0) & 7] << 12;
+                a1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
+                a2 = c_dither[y & 7][(c0 + 2) & 7] << 12;
+                a3 = c_dither[y & 7][(c0 + 3) & 7] << 12;
             } else {
-                const int c0 = 2 * lane;
-                int du0 = 64 << 12, du1 = 64 << 12, dv0 = 64 << 12, dv1 = 64 << 12;
-                if (hidepth) {     // vscale.c: U dither offset 0, V offset 3 (x0 is a multiple of 8)
-                    du0 = c_dither[y & 7][(c0) & 7] << 12;
-                    du1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
-                    dv0 = c_dither[y & 7][(c0 + 3) & 7] << 12;
-                    dv1 = c_dither[y & 7][(c0 + 4) & 7] << 12;
-                }
-                int u0 = du0, u1 = du1, v0 = dv0, v1 = dv1;
-                for (int k = 0; k < K.nv; ++k) {
-                    const int slot = (q0 + k) & (RP - 1);
-                    const uint2 uu = *reinterpret_cast<const uint2 *>(ring + slot * kChromaCols + c0);
-                    const uint2 vv = *reinterpret_cast<const uint2 *>(ring + (RP + slot) * kChromaCols + c0);
-                    const uint32_t c = vc[k];
-                    u0 = dot2(uu.x, c, u0);
-                    u1 = dot2(uu.y, c, u1);
-                    v0 = dot2(vv.x, c, v0);
-                    v1 = dot2(vv.y, c, v1);
-                }
-                const uint32_t U0 = clip8(u0), U1 = clip8(u1), V0 = clip8(v0), V1 = clip8(v1);
-                if (dfmt == DTS_FMT_NV12) {
-                    uint8_t *row = reinterpret_cast<uint8_t *>(dst.data[1]) + dbase + (int64_t)y * dst.pitch[1] + 2 * J.x0;
-                    const uint32_t o = U0 | (V0 << 8) | (U1 << 16) | (V1 << 24);
-                    if (c0 + 1 < J.ncols)
-                        *reinterpret_cast<uint32_t *>(row + 2 * c0) = o;
-                    else if (c0 < J.ncols)
-                        *reinterpret_cast<uint16_t *>(row + 2 * c0) = (uint16_t)o;
-                } else {
-                    uint8_t *ru = reinterpret_cast<uint8_t *>(dst.data[1]) + dbase + (int64_t)y * dst.pitch[1] + J.x0;
-                    uint8_t *rv = reinterpret_cast<uint8_t *>(dst.data[2]) + dbase + (int64_t)y * dst.pitch[2] + J.x0;
-                    if (c0 + 1 < J.ncols) {
-                        *reinterpret_cast<uint16_t *>(ru + c0) = (uint16_t)(U0 | (U1 << 8));
-                        *reinterpret_cast<uint16_t *>(rv + c0) = (uint16_t)(V0 | (V1 << 8));
-                    } else if (c0 < J.ncols) {
-                        ru[c0] = (uint8_t)U0;
-                        rv[c0] = (uint8_t)V0;
-                    }
+                a0 = a1 = a2 = a3 = 64 << 12;
+            }
+            int slot = q0 & (RP - 1);
+#pragma unroll 2
+            for (int k = 0; k < nv; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(ring + slot * kLumaCols + c0);
+                const uint32_t c = __builtin_amdgcn_readlane(cq, k);
+                a0 = dot2(v.x, c, a0);
+                a1 = dot2(v.y, c, a1);
+                a2 = dot2(v.z, c, a2);
+                a3 = dot2(v.w, c, a3);
+                slot = (slot + 1) & (RP - 1);
+            }
+            const uint32_t o = clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24);
+            const uint64_t row = dst.data[0] + dbase + (int64_t)y * dst.pitch[0] + J.x0;
+            if (c0 + 3 < J.ncols) {
+                *GPTR(g_u32, row + c0) = o;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (c0 + i < J.ncols) *GPTR(g_u8, row + c0 + i) = (uint8_t)(o >> (8 * i));
+            }
+        } else {
+            const int c0 = 2 * lane;
+            int u0, u1, v0, v1;
+            if (hidepth) {     // vscale.c: U dither offset 0, V offset 3 (x0 is a multiple of 8)
+                u0 = c_dither[y & 7][(c0) & 7] << 12;
+                u1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
+                v0 = c_dither[y & 7][(c0 + 3) & 7] << 12;
+                v1 = c_dither[y & 7][(c0 + 4) & 7] << 12;
+            } else {
+                u0 = u1 = v0 = v1 = 64 << 12;
+            }
+            int slot = q0 & (RP - 1);
+#pragma unroll 2
+            for (int k = 0; k < nv; ++k) {
+                const uint2 uu = *reinterpret_cast<const uint2 *>(ring + slot * kChromaCols + c0);
+                const uint2 vv = *reinterpret_cast<const uint2 *>(ring + (RP + slot) * kChromaCols + c0);
+                const uint32_t c = __builtin_amdgcn_readlane(cq, k);
+                u0 = dot2(uu.x, c, u0);
+                u1 = dot2(uu.y, c, u1);
+                v0 = dot2(vv.x, c, v0);
+                v1 = dot2(vv.y, c, v1);
+                slot = (slot + 1) & (RP - 1);
+            }
+            const uint32_t U0 = clip8(u0), U1 = clip8(u1), V0 = clip8(v0), V1 = clip8(v1);
+            if (dfmt == DTS_FMT_NV12) {
+                const uint64_t row = dst.data[1] + dbase + (int64_t)y * dst.pitch[1] + 2 * J.x0;
+                const uint32_t o = U0 | (V0 << 8) | (U1 << 16) | (V1 << 24);
+                if (c0 + 1 < J.ncols)
+                    *GPTR(g_u32, row + 2 * c0) = o;
+                else if (c0 < J.ncols)
+                    *GPTR(g_u16, row + 2 * c0) = (uint16_t)o;
+            } else {
+                const uint64_t ru = dst.data[1] + dbase + (int64_t)y * dst.pitch[1] + J.x0;
+                const uint64_t rv = dst.data[2] + dbase + (int64_t)y * dst.pitch[2] + J.x0;
+                if (c0 + 1 < J.ncols) {
+                    *GPTR(g_u16, ru + c0) = (uint16_t)(U0 | (U1 << 8));
+                    *GPTR(g_u16, rv + c0) = (uint16_t)(V0 | (V1 << 8));
+                } else if (c0 < J.ncols) {
+                    *GPTR(g_u8, ru + c0) = (uint8_t)U0;
+                    *GPTR(g_u8, rv + c0) = (uint8_t)V0;
                 }
             }
         }
     };
 
     // ---- the walk ---------------------------------------------------------
+    // step b: issue the source rows of step b+1 and the V data (row positions,
+    // tap pairs) of the output rows step b+1 will finish, run H(b) into the
+    // ring, commit the rows of step b+1 to the other stage buffer, barrier,
+    // run V(b) from data loaded one step earlier, barrier.  Every global load
+    // is consumed one phase after it is issued.
     const int nb = K.nblocks;
+    g_ci32 *vlim = GPTR(g_ci32, K.vlim);
+    g_ci32 *vposg = GPTR(g_ci32, K.vpos);
+    g_cu32 *vcg = GPTR(g_cu32, K.vcoef);
+    uint32_t cqA[kVPre], cqB[kVPre];
+    int qpA[kVPre], qpB[kVPre];
+    auto vfetch = [&](int lo, int hi, uint32_t (&cq)[kVPre], int (&qp)[kVPre]) {
+#pragma unroll
+        for (int i = 0; i < kVPre; ++i) {
+            const int y = lo + wave + 4 * i;
+            cq[i] = 0;
+            qp[i] = 0;
+            if (y < hi) {
+                cq[i] = vcg[(int64_t)y * nv + nvl];
+                qp[i] = vposg[y];
+            }
+        }
+    };
     issue(0);
     commit(stage0);
+    int vlo = 0;
+    int vhi = uniform(vlim[0]);
+    int vhi_next = nb > 1 ? vlim[1] : vhi;
+    vfetch(0, vhi, cqA, qpA);
     __syncthreads();
     for (int b = 0; b < nb; ++b) {
         const uint8_t *cur = (b & 1) ? stage1 : stage0;
         uint8_t *nxt = (b & 1) ? stage0 : stage1;
         const bool more = b + 1 < nb;
-        if (more) issue(b + 1);
+        const int vhn = uniform(vhi_next);
+        if (more) {
+            issue(b + 1);
+            vfetch(vhi, vhn, cqB, qpB);
+            if (b + 2 < nb) vhi_next = vlim[b + 2];
+        }
         hpass(b, cur);
         if (more) commit(nxt);
         __syncthreads();
-        vpass(b);
+#pragma unroll
+        for (int i = 0; i < kVPre; ++i) {
+            const int y = vlo + wave + 4 * i;
+            if (y < vhi) vrow(y, uniform(qpA[i]) >> 1, cqA[i]);
+        }
+        for (int y = vlo + wave + 4 * kVPre; y < vhi; y += 4)      // rare: > kVPre rows per wave (upscaling)
+            vrow(y, uniform(vposg[y]) >> 1, vcg[(int64_t)y * nv + nvl]);
         __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kVPre; ++i) {
+            cqA[i] = cqB[i];
+            qpA[i] = qpB[i];
+        }
+        vlo = vhi;
+        vhi = vhn;
     }
 }
 
 int ladder_ndmax_for(int nd)
 {
-    static const int buckets[] = {2, 3, 4, 6, 8, 12, 16};
+    static const int buckets[] = {4, 8, 16};
     for (int b : buckets)
         if (nd <= b) return b;
     return 0;
@@ -329,7 +411,7 @@ static hipError_t launch_ladder_src(const LadderParams &p, int ndmax, int lds, h
     case N:                                                                          \
         hipLaunchKernelGGL((k_ladder<SRC, N>), grid, block, lds, s, p);            \
         break;
-        DTS_CASE(2) DTS_CASE(3) DTS_CASE(4) DTS_CASE(6) DTS_CASE(8) DTS_CASE(12) DTS_CASE(16)
+        DTS_CASE(4) DTS_CASE(8) DTS_CASE(16)
 #undef DTS_CASE
     default:
         return hipErrorInvalidValue;

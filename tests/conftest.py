@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:        # load torch's HIP runtime first so libdts binds to the same one (see bench.py)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "distributed-transcoding-server_amd")
 for p in (os.path.join(PKG, "python"), os.path.join(ROOT, "oracle"), ROOT):

@@ -42,7 +42,8 @@ def test_quality_vs_oracle(ctx, w, h):
     for i in range(3):
         want = orc.quality_frame(w, h, fr_a[i], fr_b[i])
         check_q(got[i], want)
-    assert got[1]["ssim_all"] == pytest.approx(1.0, abs=1e-12) or w < 8 or h < 8
+    if w >= 16 and h >= 16:       # chroma planes of >= 8x8 have SSIM windows
+        assert got[1]["ssim_all"] == pytest.approx(1.0, abs=1e-12)
 
 
 def gpu_quality(ctx, w, h, fa, fb, torch):

@@ -23,6 +23,7 @@ for s in "$@"; do
   case $s in
     tests)  step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     quick)  step tests_quick 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "small or quality or identity or device_path" ;;
+    all)    step tests_all 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 300 python -u bench.py --steps 20 --warmup 3 ;;
     benchq) step benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu ;;
