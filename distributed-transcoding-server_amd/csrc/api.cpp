@@ -31,6 +31,7 @@ struct dts_ctx {
 namespace {
 
 constexpr int kSwsAccurateRnd = 0x40000;
+constexpr int kQueueSlots = 64;
 constexpr int kSwsBitexact = 0x80000;
 
 #define HIPCHK(ctx, expr)                                  \
@@ -127,6 +128,9 @@ struct dts_graph {
     void *dev_tables = nullptr;           // all per-graph device tables
     Job *dev_jobs = nullptr;
     RungKind *dev_rk = nullptr;
+    unsigned int *dev_queue = nullptr;    // kQueueSlots work counters (one per in-flight launch)
+    unsigned int queue_next = 0;
+    int grid_cap = 0;                     // resident workgroups of the persistent ladder grid
 
     // host-path batch resources (2 slots)
     int batch = 32;
@@ -426,6 +430,24 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
             return DTS_E_HIP;
         }
 
+        // persistent grid: resident workgroups per CU x CUs; work counters
+        {
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+                cus = 256;
+            const int bpc = ladder_blocks_per_cu(g->src_kind, g->ndmax, g->lds_bytes);
+            if (bpc < 1) {
+                dts_graph_destroy(g);
+                return DTS_E_RANGE;
+            }
+            g->grid_cap = bpc * cus;
+            if (hipMalloc(&g->dev_queue, kQueueSlots * sizeof(unsigned int)) != hipSuccess) {
+                ctx->last_hip = (int)hipGetLastError();
+                dts_graph_destroy(g);
+                return DTS_E_HIP;
+            }
+        }
+
         // info
         g->info.src_frame_bytes = packed_bytes(s.src_w, s.src_h, s.src_fmt);
         int64_t algo = g->info.src_frame_bytes;
@@ -469,6 +491,7 @@ void dts_graph_destroy(dts_graph *g)
         if (g->done[sl]) hipEventDestroy(g->done[sl]);
     }
     if (g->dev_tables) hipFree(g->dev_tables);
+    if (g->dev_queue) hipFree(g->dev_queue);
     delete g;
 }
 
@@ -589,18 +612,21 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    // bound the grid (blocks = frames x jobs) per launch
+    // persistent grid over nframes x njobs items; items per launch bounded to 2^30
     const int max_frames = std::max(1, (1 << 30) / std::max(1, p.njobs));
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
         const int n = std::min(max_frames, nframes - f0);
         LadderParams pp = p;
         pp.nframes = n;
+        pp.nitems = n * p.njobs;
         pp.src.data[0] += (uint64_t)(f0 * src->frame_stride);
         pp.src.data[1] += (uint64_t)(f0 * src->frame_stride);
         pp.src.data[2] += (uint64_t)(f0 * src->frame_stride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
-        HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, st));
+        pp.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
+        HIPCHK(ctx, hipMemsetAsync(pp.queue, 0, sizeof(unsigned int), st));
+        HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, std::min(pp.nitems, g->grid_cap), st));
     }
     if (want_q) {
         const dts_output_spec &o = s.out[s.quality_out];

@@ -73,8 +73,10 @@ struct LadderParams {
     int32_t ring_pairs;             // power of two
     int32_t stage_bytes;            // one stage buffer (all planes), bytes
     int32_t nframes;
+    int32_t nitems;                 // nframes * njobs work items (frame-major, heavy jobs first)
     const Job *jobs;                // device [njobs]
     const RungKind *rk;             // device [nrungs][2]
+    unsigned int *queue;            // device work counter (zeroed before the launch)
 };
 
 // ---------------------------------------------------------------------------
@@ -161,7 +163,8 @@ __host__ __device__ inline int synth_sample(int pattern, uint32_t seed, int x, i
     }
 
 // kernels.hip entry points (host-side launchers)
-hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, hipStream_t s);
+hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, int grid, hipStream_t s);
+int ladder_blocks_per_cu(int src_kind, int ndmax, int lds_bytes);   // occupancy for the persistent grid
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s);
 hipError_t launch_synth(int w, int h, int fmt, int pattern, uint32_t seed, int64_t first,
                         const DevPlanes &dst, int nframes, hipStream_t s);

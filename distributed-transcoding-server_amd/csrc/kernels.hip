@@ -21,6 +21,13 @@
 // the other renditions hit the XCD L2 / Infinity Cache).
 #include "dts_internal.h"
 
+#ifndef DTS_ABLATE
+#define DTS_ABLATE 0
+#endif
+#ifndef DTS_V_UNROLL
+#define DTS_V_UNROLL 1
+#endif
+
 namespace dts {
 
 __constant__ uint8_t c_dither[8][8] = DTS_DITHER_8X8_128;
@@ -65,45 +72,137 @@ __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirs
 // ---------------------------------------------------------------------------
 constexpr int kVPre = 4;     // output rows per wave whose V data is prefetched per step
 
-// Horizontal FIR of one thread's output column over the kBlkRows staged rows.
-// ND is a compile-time tap-dword count so every LDS read of a row issues
-// before the first dot product consumes it.
+// Horizontal FIR of one thread's output column over the kBlkRows staged rows,
+// packed as int16x2 row pairs.  ND is a compile-time tap-dword count so all
+// LDS reads of a row issue before the first dot product consumes them.
+// v_cvt_pk_i16_i32 saturates, which is exactly FFMIN(val, 32767) here (val >=
+// -32768 always holds for normalised filters on 8/10-bit samples).
 template <int SRC, int ND, int NDMAX>
 __device__ __forceinline__ void hrows(const uint8_t *s, int swb, const uint32_t (&ch)[NDMAX],
-                                      const uint32_t (&cl)[NDMAX], int bias, int (&hv)[kBlkRows])
+                                      const uint32_t (&cl)[NDMAX], int bias, uint32_t (&hp)[kBlkRows / 2])
 {
 #pragma unroll
-    for (int r = 0; r < kBlkRows; ++r) {
-        const uint32_t *rp = reinterpret_cast<const uint32_t *>(s + r * swb);
-        uint32_t v[ND];
+    for (int pr = 0; pr < kBlkRows / 2; ++pr) {
+        int val[2];
 #pragma unroll
-        for (int k = 0; k < ND; ++k) v[k] = rp[k];
-        int val;
-        if (SRC == kSrcP010) {
-            int a = 0;
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t *rp = reinterpret_cast<const uint32_t *>(s + (2 * pr + q) * swb);
+            uint32_t v[ND];
 #pragma unroll
-            for (int k = 0; k < ND; ++k) a = dot2(v[k], ch[k], a);
-            val = a >> 9;                                   // hScale16To15: sh = depth - 1
-        } else {
-            int a = 0, c = bias;
+            for (int k = 0; k < ND; ++k) v[k] = rp[k];
+            if (SRC == kSrcP010) {
+                int a = 0;
 #pragma unroll
-            for (int k = 0; k < ND; ++k) {
-                a = dot4(v[k], ch[k], a);
-                c = dot4(v[k], cl[k], c);
+                for (int k = 0; k < ND; ++k) a = dot2(v[k], ch[k], a);
+                val[q] = a >> 9;                            // hScale16To15: sh = depth - 1
+            } else {
+                int a = 0, c = bias;
+#pragma unroll
+                for (int k = 0; k < ND; ++k) {
+                    a = dot4(v[k], ch[k], a);
+                    c = dot4(v[k], cl[k], c);
+                }
+                val[q] = (a * 256 + c) >> 7;                // hScale8To15 (src ^ 0x80 bias folded in c)
             }
-            val = (a * 256 + c) >> 7;                       // hScale8To15 (src ^ 0x80 bias folded in c)
         }
-        hv[r] = val < 32767 ? val : 32767;
+        hp[pr] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(val[0], val[1]));
     }
 }
 
-template <int SRC, int NDMAX>
-__global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
+// Vertical FIR of one output row for one wave.  Luma: each lane owns 4
+// consecutive columns (one ds_read_b128 per row pair); chroma: 2 columns of U
+// and of V.  NV row pairs, tap pair k read from lane k of cq by v_readlane.
+template <int KIND, int NV>
+__device__ __forceinline__ void vtaps(const uint32_t *ring, int RP, int q0, int lane, uint32_t cq, int (&acc)[4])
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int cols = KIND ? kChromaCols : kLumaCols;
+    const int s0 = q0 & (RP - 1);
+    if (s0 + NV <= RP) {                     // no wrap: one base address, immediate offsets
+        const uint32_t *b = ring + s0 * cols;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const uint32_t c = __builtin_amdgcn_readlane(cq, k);
+            if (KIND == 0) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(b + k * cols + 4 * lane);
+                acc[0] = dot2(v.x, c, acc[0]);
+                acc[1] = dot2(v.y, c, acc[1]);
+                acc[2] = dot2(v.z, c, acc[2]);
+                acc[3] = dot2(v.w, c, acc[3]);
+            } else {
+                const uint2 u = *reinterpret_cast<const uint2 *>(b + k * cols + 2 * lane);
+                const uint2 w = *reinterpret_cast<const uint2 *>(b + (RP + k) * cols + 2 * lane);
+                acc[0] = dot2(u.x, c, acc[0]);
+                acc[1] = dot2(u.y, c, acc[1]);
+                acc[2] = dot2(w.x, c, acc[2]);
+                acc[3] = dot2(w.y, c, acc[3]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const int sl = (s0 + k) & (RP - 1);
+            const uint32_t c = __builtin_amdgcn_readlane(cq, k);
+            if (KIND == 0) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(ring + sl * cols + 4 * lane);
+                acc[0] = dot2(v.x, c, acc[0]);
+                acc[1] = dot2(v.y, c, acc[1]);
+                acc[2] = dot2(v.z, c, acc[2]);
+                acc[3] = dot2(v.w, c, acc[3]);
+            } else {
+                const uint2 u = *reinterpret_cast<const uint2 *>(ring + sl * cols + 2 * lane);
+                const uint2 w = *reinterpret_cast<const uint2 *>(ring + (RP + sl) * cols + 2 * lane);
+                acc[0] = dot2(u.x, c, acc[0]);
+                acc[1] = dot2(u.y, c, acc[1]);
+                acc[2] = dot2(w.x, c, acc[2]);
+                acc[3] = dot2(w.y, c, acc[3]);
+            }
+        }
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void vtaps_any(const uint32_t *ring, int RP, int q0, int lane, int nv, uint32_t cq,
+                                          int (&acc)[4])
+{
+#if DTS_V_UNROLL
+    switch (nv) {                                            // wave-uniform
+#define DTS_VCASE(N) \
+    case N: vtaps<KIND, N>(ring, RP, q0, lane, cq, acc); return;
+        DTS_VCASE(1) DTS_VCASE(2) DTS_VCASE(3) DTS_VCASE(4) DTS_VCASE(5) DTS_VCASE(6) DTS_VCASE(7) DTS_VCASE(8)
+        DTS_VCASE(9) DTS_VCASE(10) DTS_VCASE(11) DTS_VCASE(12) DTS_VCASE(13) DTS_VCASE(14) DTS_VCASE(15) DTS_VCASE(16)
+#undef DTS_VCASE
+    default:
+        break;
+    }
+#endif
+    // wide vertical filters (> 32 taps): generic loop (the pair table is
+    // read from registers of up to 64 lanes)
+    constexpr int cols = KIND ? kChromaCols : kLumaCols;
+    for (int k = 0; k < nv; ++k) {
+        const int sl = ((q0 + k) & (RP - 1));
+        const uint32_t c = __builtin_amdgcn_readlane(cq, k);
+        if (KIND == 0) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(ring + sl * cols + 4 * lane);
+            acc[0] = dot2(v.x, c, acc[0]);
+            acc[1] = dot2(v.y, c, acc[1]);
+            acc[2] = dot2(v.z, c, acc[2]);
+            acc[3] = dot2(v.w, c, acc[3]);
+        } else {
+            const uint2 u = *reinterpret_cast<const uint2 *>(ring + sl * cols + 2 * lane);
+            const uint2 w = *reinterpret_cast<const uint2 *>(ring + (RP + sl) * cols + 2 * lane);
+            acc[0] = dot2(u.x, c, acc[0]);
+            acc[1] = dot2(u.y, c, acc[1]);
+            acc[2] = dot2(w.x, c, acc[2]);
+            acc[3] = dot2(w.y, c, acc[3]);
+        }
+    }
+}
+
+// One work item: a (frame, rung, plane kind, column strip) walked top to bottom.
+template <int SRC, int NDMAX>
+__device__ __forceinline__ void ladder_item(const LadderParams &P, int frame, int jid, uint8_t *smem)
+{
     const int t = threadIdx.x;
-    const int jid = blockIdx.x % P.njobs;
-    const int frame = blockIdx.x / P.njobs;
     const Job J = P.jobs[jid];
     const int kind = J.kind;
     const RungKind K = P.rk[J.rung * 2 + kind];
@@ -220,12 +319,20 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
 
     auto hpass = [&](int b, const uint8_t *stage) {
         if (!hact) return;
-        int hv[kBlkRows];
+#if DTS_ABLATE & 1      // diagnostic builds only: skip the H arithmetic
+        {
+#pragma unroll
+            for (int pr = 0; pr < kBlkRows / 2; ++pr)
+                ring[(hplane * RP + ((b * (kBlkRows / 2) + pr) & (RP - 1))) * pcols + hcol] = (uint32_t)b;
+            return;
+        }
+#endif
+        uint32_t hp[kBlkRows / 2];
         const uint8_t *s = stage + lofs;
         switch (nd) {                                        // wave-uniform
 #define DTS_HCASE(N)                                                           \
     case N:                                                                    \
-        if (N <= NDMAX) hrows<SRC, (N <= NDMAX ? N : 1), NDMAX>(s, swb, chv, clv, bias, hv); \
+        if (N <= NDMAX) hrows<SRC, (N <= NDMAX ? N : 1), NDMAX>(s, swb, chv, clv, bias, hp); \
         break;
             DTS_HCASE(1) DTS_HCASE(2) DTS_HCASE(3) DTS_HCASE(4) DTS_HCASE(5) DTS_HCASE(6) DTS_HCASE(7)
             DTS_HCASE(8) DTS_HCASE(10) DTS_HCASE(12) DTS_HCASE(14) DTS_HCASE(16)
@@ -236,11 +343,11 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
 #pragma unroll
         for (int pr = 0; pr < kBlkRows / 2; ++pr) {
             const int slot = (b * (kBlkRows / 2) + pr) & (RP - 1);
-            ring[(hplane * RP + slot) * pcols + hcol] = (uint32_t)(hv[2 * pr] & 0xffff) | ((uint32_t)hv[2 * pr + 1] << 16);
+            ring[(hplane * RP + slot) * pcols + hcol] = hp[pr];
         }
     };
 
-    // ---- vertical: one output row per wave, coefficients via v_readlane ---
+    // ---- vertical: one output row per wave, taps via v_readlane -----------
     const int wave = uniform(t >> 6);
     const int lane = t & 63;
     const int rung = J.rung;
@@ -254,31 +361,17 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     const int nv = K.nv;
     const int nvl = lane < nv ? lane : nv - 1;
 
-    // one output row y (wave-uniform) from the ring; cq: lane k holds tap pair k
     auto vrow = [&](int y, int q0, uint32_t cq) {
+#if DTS_ABLATE & 2      // diagnostic builds only: skip the V arithmetic and stores
+        return;
+#endif
+        int acc[4];
         if (kind == 0) {
             const int c0 = 4 * lane;
-            int a0, a1, a2, a3;
-            if (hidepth) {
-                a0 = c_dither[y & 7][(c0 + 0) & 7] << 12;
-                a1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
-                a2 = c_dither[y & 7][(c0 + 2) & 7] << 12;
-                a3 = c_dither[y & 7][(c0 + 3) & 7] << 12;
-            } else {
-                a0 = a1 = a2 = a3 = 64 << 12;
-            }
-            int slot = q0 & (RP - 1);
-#pragma unroll 2
-            for (int k = 0; k < nv; ++k) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(ring + slot * kLumaCols + c0);
-                const uint32_t c = __builtin_amdgcn_readlane(cq, k);
-                a0 = dot2(v.x, c, a0);
-                a1 = dot2(v.y, c, a1);
-                a2 = dot2(v.z, c, a2);
-                a3 = dot2(v.w, c, a3);
-                slot = (slot + 1) & (RP - 1);
-            }
-            const uint32_t o = clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = (hidepth ? c_dither[y & 7][(c0 + i) & 7] : 64) << 12;
+            vtaps_any<0>(ring, RP, q0, lane, nv, cq, acc);
+            const uint32_t o = clip8(acc[0]) | (clip8(acc[1]) << 8) | (clip8(acc[2]) << 16) | (clip8(acc[3]) << 24);
             const uint64_t row = dst.data[0] + dbase + (int64_t)y * dst.pitch[0] + J.x0;
             if (c0 + 3 < J.ncols) {
                 *GPTR(g_u32, row + c0) = o;
@@ -289,28 +382,16 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
             }
         } else {
             const int c0 = 2 * lane;
-            int u0, u1, v0, v1;
             if (hidepth) {     // vscale.c: U dither offset 0, V offset 3 (x0 is a multiple of 8)
-                u0 = c_dither[y & 7][(c0) & 7] << 12;
-                u1 = c_dither[y & 7][(c0 + 1) & 7] << 12;
-                v0 = c_dither[y & 7][(c0 + 3) & 7] << 12;
-                v1 = c_dither[y & 7][(c0 + 4) & 7] << 12;
+                acc[0] = c_dither[y & 7][(c0) & 7] << 12;
+                acc[1] = c_dither[y & 7][(c0 + 1) & 7] << 12;
+                acc[2] = c_dither[y & 7][(c0 + 3) & 7] << 12;
+                acc[3] = c_dither[y & 7][(c0 + 4) & 7] << 12;
             } else {
-                u0 = u1 = v0 = v1 = 64 << 12;
+                acc[0] = acc[1] = acc[2] = acc[3] = 64 << 12;
             }
-            int slot = q0 & (RP - 1);
-#pragma unroll 2
-            for (int k = 0; k < nv; ++k) {
-                const uint2 uu = *reinterpret_cast<const uint2 *>(ring + slot * kChromaCols + c0);
-                const uint2 vv = *reinterpret_cast<const uint2 *>(ring + (RP + slot) * kChromaCols + c0);
-                const uint32_t c = __builtin_amdgcn_readlane(cq, k);
-                u0 = dot2(uu.x, c, u0);
-                u1 = dot2(uu.y, c, u1);
-                v0 = dot2(vv.x, c, v0);
-                v1 = dot2(vv.y, c, v1);
-                slot = (slot + 1) & (RP - 1);
-            }
-            const uint32_t U0 = clip8(u0), U1 = clip8(u1), V0 = clip8(v0), V1 = clip8(v1);
+            vtaps_any<1>(ring, RP, q0, lane, nv, cq, acc);
+            const uint32_t U0 = clip8(acc[0]), U1 = clip8(acc[1]), V0 = clip8(acc[2]), V1 = clip8(acc[3]);
             if (dfmt == DTS_FMT_NV12) {
                 const uint64_t row = dst.data[1] + dbase + (int64_t)y * dst.pitch[1] + 2 * J.x0;
                 const uint32_t o = U0 | (V0 << 8) | (U1 << 16) | (V1 << 24);
@@ -333,11 +414,11 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     };
 
     // ---- the walk ---------------------------------------------------------
-    // step b: issue the source rows of step b+1 and the V data (row positions,
-    // tap pairs) of the output rows step b+1 will finish, run H(b) into the
-    // ring, commit the rows of step b+1 to the other stage buffer, barrier,
-    // run V(b) from data loaded one step earlier, barrier.  Every global load
-    // is consumed one phase after it is issued.
+    // step b: commit the rows of step b+1 (loaded during step b-1) to the
+    // other stage buffer, issue the rows of step b+2 and the V data of the
+    // output rows step b+1 finishes, run H(b), barrier, run V(b) (data
+    // fetched during step b-1), barrier.  Every global load has one whole step
+    // to land before it is consumed.
     const int nb = K.nblocks;
     g_ci32 *vlim = GPTR(g_ci32, K.vlim);
     g_ci32 *vposg = GPTR(g_ci32, K.vpos);
@@ -358,6 +439,7 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     };
     issue(0);
     commit(stage0);
+    if (nb > 1) issue(1);
     int vlo = 0;
     int vhi = uniform(vlim[0]);
     int vhi_next = nb > 1 ? vlim[1] : vhi;
@@ -366,23 +448,29 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     for (int b = 0; b < nb; ++b) {
         const uint8_t *cur = (b & 1) ? stage1 : stage0;
         uint8_t *nxt = (b & 1) ? stage0 : stage1;
-        const bool more = b + 1 < nb;
         const int vhn = uniform(vhi_next);
-        if (more) {
-            issue(b + 1);
+        if (b + 1 < nb) {
+            commit(nxt);
+            if (b + 2 < nb) {
+                issue(b + 2);
+                vhi_next = vlim[b + 2];
+            }
             vfetch(vhi, vhn, cqB, qpB);
-            if (b + 2 < nb) vhi_next = vlim[b + 2];
         }
         hpass(b, cur);
-        if (more) commit(nxt);
         __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kVPre; ++i) {
-            const int y = vlo + wave + 4 * i;
-            if (y < vhi) vrow(y, uniform(qpA[i]) >> 1, cqA[i]);
+        for (int y = vlo + wave, i = 0; y < vhi; y += 4, ++i) {   // one call site keeps the code small
+            int q;
+            uint32_t cq;
+            if (i < kVPre) {
+                q = i == 0 ? qpA[0] : i == 1 ? qpA[1] : i == 2 ? qpA[2] : qpA[3];
+                cq = i == 0 ? cqA[0] : i == 1 ? cqA[1] : i == 2 ? cqA[2] : cqA[3];
+            } else {                                                // rare: > kVPre rows per wave (upscaling)
+                q = vposg[y];
+                cq = vcg[(int64_t)y * nv + nvl];
+            }
+            vrow(y, uniform(q) >> 1, cq);
         }
-        for (int y = vlo + wave + 4 * kVPre; y < vhi; y += 4)      // rare: > kVPre rows per wave (upscaling)
-            vrow(y, uniform(vposg[y]) >> 1, vcg[(int64_t)y * nv + nvl]);
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < kVPre; ++i) {
@@ -394,6 +482,25 @@ __global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
     }
 }
 
+// Persistent workgroups pull (frame, strip) items from a device counter:
+// frame-major so the renditions of a frame run together (source re-reads
+// hit L2 / MALL), heaviest strips first within a frame (short tail).
+template <int SRC, int NDMAX>
+__global__ void __launch_bounds__(kThreads) k_ladder(const LadderParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t *slot = reinterpret_cast<uint32_t *>(smem + 2 * P.stage_bytes);   // ring word 0, free between items
+    for (;;) {
+        if (threadIdx.x == 0) *slot = atomicAdd(P.queue, 1u);
+        __syncthreads();
+        const int item = uniform((int)*slot);
+        __syncthreads();
+        if (item >= P.nitems) return;
+        ladder_item<SRC, NDMAX>(P, item / P.njobs, item % P.njobs, smem);
+        __syncthreads();
+    }
+}
+
 int ladder_ndmax_for(int nd)
 {
     static const int buckets[] = {4, 8, 16};
@@ -402,30 +509,62 @@ int ladder_ndmax_for(int nd)
     return 0;
 }
 
-template <int SRC>
-static hipError_t launch_ladder_src(const LadderParams &p, int ndmax, int lds, hipStream_t s)
+template <int SRC, int N>
+static hipError_t launch_one(const LadderParams &p, int grid, int lds, hipStream_t s)
 {
-    const dim3 grid((unsigned)(p.njobs * p.nframes)), block(kThreads);
-    switch (ndmax) {
-#define DTS_CASE(N)                                                                  \
-    case N:                                                                          \
-        hipLaunchKernelGGL((k_ladder<SRC, N>), grid, block, lds, s, p);            \
-        break;
-        DTS_CASE(4) DTS_CASE(8) DTS_CASE(16)
-#undef DTS_CASE
-    default:
-        return hipErrorInvalidValue;
-    }
+    hipLaunchKernelGGL((k_ladder<SRC, N>), dim3((unsigned)grid), dim3(kThreads), lds, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, hipStream_t s)
+template <int SRC>
+static hipError_t launch_ladder_src(const LadderParams &p, int ndmax, int lds, int grid, hipStream_t s)
+{
+    switch (ndmax) {
+    case 4: return launch_one<SRC, 4>(p, grid, lds, s);
+    case 8: return launch_one<SRC, 8>(p, grid, lds, s);
+    case 16: return launch_one<SRC, 16>(p, grid, lds, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, int grid, hipStream_t s)
 {
     switch (p.src_kind) {
-    case kSrcPlanar8: return launch_ladder_src<kSrcPlanar8>(p, ndmax, lds_bytes, s);
-    case kSrcNV12: return launch_ladder_src<kSrcNV12>(p, ndmax, lds_bytes, s);
-    case kSrcP010: return launch_ladder_src<kSrcP010>(p, ndmax, lds_bytes, s);
+    case kSrcPlanar8: return launch_ladder_src<kSrcPlanar8>(p, ndmax, lds_bytes, grid, s);
+    case kSrcNV12: return launch_ladder_src<kSrcNV12>(p, ndmax, lds_bytes, grid, s);
+    case kSrcP010: return launch_ladder_src<kSrcP010>(p, ndmax, lds_bytes, grid, s);
     default: return hipErrorInvalidValue;
+    }
+}
+
+template <int SRC, int N>
+static int occ_one(int lds)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&k_ladder<SRC, N>), kThreads,
+                                                     (size_t)lds) != hipSuccess)
+        return 0;
+    return n;
+}
+
+template <int SRC>
+static int occ_src(int ndmax, int lds)
+{
+    switch (ndmax) {
+    case 4: return occ_one<SRC, 4>(lds);
+    case 8: return occ_one<SRC, 8>(lds);
+    case 16: return occ_one<SRC, 16>(lds);
+    default: return 0;
+    }
+}
+
+int ladder_blocks_per_cu(int src_kind, int ndmax, int lds_bytes)
+{
+    switch (src_kind) {
+    case kSrcPlanar8: return occ_src<kSrcPlanar8>(ndmax, lds_bytes);
+    case kSrcNV12: return occ_src<kSrcNV12>(ndmax, lds_bytes);
+    case kSrcP010: return occ_src<kSrcP010>(ndmax, lds_bytes);
+    default: return 0;
     }
 }
 

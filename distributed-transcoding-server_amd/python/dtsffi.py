@@ -15,7 +15,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libdts.so")
+LIB_PATH = os.environ.get("DTS_LIB") or os.path.join(PKG, "lib", "libdts.so")
 
 FMT_YUV420P, FMT_NV12, FMT_P010LE = 0, 1, 2
 FMT_NAMES = {"yuv420p": FMT_YUV420P, "nv12": FMT_NV12, "p010le": FMT_P010LE, "p010": FMT_P010LE}

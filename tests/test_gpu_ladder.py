@@ -135,3 +135,36 @@ def test_device_path_matches_host_path(ctx):
             uv = raw[ow * oh: ow * oh + 2 * ((ow + 1) // 2) * ((oh + 1) // 2)].reshape((oh + 1) // 2, -1)
             want = oracle_frame(host_src, w, h, D.FMT_YUV420P, ow, oh, of, m)
             assert planes_equal([y, uv, None], want), first_diff([y, uv, None], want)
+
+
+@pytest.mark.parametrize("method", [BIC, LAN, D.SCALE_GAUSS])
+def test_clip_stress(ctx, method):
+    """Patterns that drive the 15-bit horizontal clip (FFMIN(val >> 7, 32767)) and the
+    u8 output clip at both ends: bright samples on the positive lobes, black on the
+    negative ones, plus single-pixel spikes."""
+    w, h = 256, 64
+    y = np.zeros((h, w), np.uint8)
+    y[:, 1::4] = 255
+    y[:, 2::4] = 255
+    y[::7, ::5] = 255
+    y[3::9] = 0
+    u = np.full(((h + 1) // 2, (w + 1) // 2), 255, np.uint8)
+    u[:, ::3] = 0
+    v = np.zeros_like(u)
+    v[::2] = 255
+    frames = [[y, u, v], [255 - y, 255 - u, 255 - v]]
+    run_and_check(ctx, w, h, D.FMT_YUV420P, [(128, 32, D.FMT_NV12, method), (85, 21, D.FMT_YUV420P, method),
+                                             (300, 70, D.FMT_NV12, method)], frames)
+
+
+def test_many_batches_device_queue(ctx):
+    """Persistent grid + work queue across several launches with different frame counts."""
+    outs = [(96, 54, D.FMT_NV12, BIC), (64, 36, D.FMT_NV12, BIC)]
+    g = D.Graph(ctx, D.make_spec(192, 108, D.FMT_YUV420P, outs, max_batch=3))
+    for n in (1, 7, 3):
+        frames = [D.synth_host(192, 108, D.FMT_YUV420P, 0, 77, 100 * n + f) for f in range(n)]
+        got, _ = g.run_host(frames)
+        for f in range(n):
+            for k, o in enumerate(outs):
+                want = oracle_frame(frames[f], 192, 108, D.FMT_YUV420P, *o)
+                assert planes_equal(got[f][k], want), first_diff(got[f][k], want)
