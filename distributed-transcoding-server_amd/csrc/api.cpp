@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -131,6 +132,12 @@ struct dts_graph {
     unsigned int *dev_queue = nullptr;    // kQueueSlots work counters (one per in-flight launch)
     unsigned int queue_next = 0;
     int grid_cap = 0;                     // resident workgroups of the persistent ladder grid
+    // v4 ladder (ladder4.hip) for the (rendition, kind) pairs it fits; the rest run on v3
+    uint32_t v4_mask = 0;                 // bit 2*rung+kind
+    void *dev_tables4 = nullptr;
+    Job4 *dev_jobs4 = nullptr;
+    RungKind4 *dev_rk4 = nullptr;
+    int njobs4 = 0, lds4 = 0, grid4 = 0;
 
     // host-path batch resources (2 slots)
     int batch = 32;
@@ -154,6 +161,7 @@ struct dts_graph {
 namespace {
 
 struct KindTables {
+    SwsFilter fh;                         // the libswscale H filter (v4 plans from it)
     HTable h;
     VTable v;
     std::vector<int32_t> vlim;
@@ -180,6 +188,7 @@ int build_kind(const dts_graph_spec &s, int k, int kind, KindTables &kt)
     kt.sws_v = fv.size;
     e = s.src_fmt == DTS_FMT_P010LE ? pack_h_p010(fh, kt.dstW, kt.h) : pack_h_u8(fh, kt.dstW, kt.h);
     if (e) return e;
+    kt.fh = std::move(fh);
     return pack_v(fv, kt.dstH, kt.v);
 }
 
@@ -234,6 +243,145 @@ size_t push_blob(std::vector<uint8_t> &blob, const std::vector<T> &v)
     blob.resize(off + v.size() * sizeof(T));
     if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
     return off;
+}
+
+// ---- planning: everything graph_create decides on the host (dts_graph_plan
+// runs it without a device) ----------------------------------------------
+struct GraphPlan {
+    int src_kind = 0, ndmax = 4, ring_pairs = 8, stage_bytes = 0, lds_bytes = 0, lds4 = 0;
+    uint32_t v4_mask = 0;                 // bit 2*rung+kind: that (rendition, kind) runs on k_ladder4
+    std::vector<KindTables> kts;
+    std::vector<Plan4> p4;
+    std::vector<Job> jobs;                // v3 strips (the kinds not on v4)
+    std::vector<Job4> jobs4;              // v4 strips
+    dts_graph_info info{};
+};
+
+int validate_spec(const dts_graph_spec &s)
+{
+    if (s.src_w < 4 || s.src_h < 4 || s.src_w > 16384 || s.src_h > 16384 || !fmt_in_ok(s.src_fmt)) return DTS_E_INVAL;
+    if (s.nout < 1 || s.nout > DTS_MAX_OUTPUTS) return DTS_E_INVAL;
+    for (int k = 0; k < s.nout; ++k) {
+        const dts_output_spec &o = s.out[k];
+        if (o.w < 2 || o.h < 2 || o.w > 16384 || o.h > 16384) return DTS_E_INVAL;
+        if (!fmt_out_ok(o.fmt)) return DTS_E_UNSUPPORTED;
+        if (!method_ok(o.method)) return DTS_E_UNSUPPORTED;
+    }
+    if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
+    if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
+    return DTS_OK;
+}
+
+// DTS_LADDER=3 keeps every (rendition, kind) on the v3 kernel (A/B runs, tests)
+bool v4_enabled()
+{
+    const char *f = std::getenv("DTS_LADDER");
+    return !(f && f[0] == '3');
+}
+
+bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
+{
+    const bool p010 = s.src_fmt == DTS_FMT_P010LE, nv12 = s.src_fmt == DTS_FMT_NV12;
+    int64_t rowb[3], rows[3];
+    plane_geom(s.src_w, s.src_h, s.src_fmt, rowb, rows);
+    // bytes per sample in the (maybe interleaved) source row, 16-B loads per row and plane the
+    // kernel holds, sample pairs its H code addresses (ladder4.hip item4: CAP)
+    const int bps = kind ? (p010 ? 4 : (nv12 ? 2 : 1)) : (p010 ? 2 : 1);
+    const int nlmax = (kind && !p010 && !nv12) ? 4 : 8;
+    const int cap = kind ? (p010 ? 16 : 32) : (p010 ? 32 : 64);
+    return plan4_kind(kt.fh, kt.v, kt.srcH, kt.dstW, kt.dstH, bps, nlmax, cap, kind ? kRing4ColsC : kRing4ColsL,
+                      rowb[kind ? 1 : 0], kRing4Slots, pl);
+}
+
+int make_plan(const dts_graph_spec &s, GraphPlan &gp)
+{
+    int e = validate_spec(s);
+    if (e) return e;
+    gp.src_kind = s.src_fmt == DTS_FMT_P010LE ? kSrcP010 : (s.src_fmt == DTS_FMT_NV12 ? kSrcNV12 : kSrcPlanar8);
+    const bool p010 = s.src_fmt == DTS_FMT_P010LE;
+    const bool use4 = v4_enabled();
+    gp.kts.resize((size_t)s.nout * 2);
+    gp.p4.resize(gp.kts.size());
+    int ndmax_need = 1;
+    for (int k = 0; k < s.nout; ++k)
+        for (int kind = 0; kind < 2; ++kind) {
+            const size_t i = (size_t)k * 2 + kind;
+            KindTables &kt = gp.kts[i];
+            e = build_kind(s, k, kind, kt);
+            if (e) return e;
+            if (use4 && plan4_for(s, kt, kind, gp.p4[i]))
+                gp.v4_mask |= 1u << i;
+            else
+                ndmax_need = std::max(ndmax_need, kt.h.nd);
+            gp.info.h_taps[k][kind] = kt.h.span;
+            gp.info.v_taps[k][kind] = kt.v.span;
+            gp.info.sws_h_size[k][kind] = kt.sws_h;
+            gp.info.sws_v_size[k][kind] = kt.sws_v;
+            gp.info.h_pairs4[k][kind] = (gp.v4_mask >> i) & 1 ? gp.p4[i].N : 0;
+        }
+    gp.ndmax = ladder_ndmax_for(ndmax_need);
+    if (!gp.ndmax) return DTS_E_RANGE;
+    const bool on3 = gp.v4_mask != (1u << gp.kts.size()) - 1;
+    if (on3) {
+        // v3 ring: smallest power of two holding every V window of the kinds v3 runs
+        int rp = 8;
+        for (; rp <= 256; rp *= 2) {
+            bool ok = true;
+            for (size_t i = 0; i < gp.kts.size(); ++i)
+                if (!((gp.v4_mask >> i) & 1))
+                    ok = ok && plan_vlimits(gp.kts[i].v, gp.kts[i].srcH, gp.kts[i].dstH, rp, gp.kts[i].vlim);
+            if (ok) break;
+        }
+        if (rp > 256) return DTS_E_RANGE;
+        gp.ring_pairs = rp;
+        int max_stage = 0;
+        for (size_t i = 0; i < gp.kts.size(); ++i)
+            if (!((gp.v4_mask >> i) & 1)) make_jobs(gp.kts[i], (int)(i >> 1), (int)(i & 1), p010, gp.jobs, max_stage);
+        // heaviest strips first (H taps x columns x source rows)
+        std::stable_sort(gp.jobs.begin(), gp.jobs.end(), [&](const Job &a, const Job &b) {
+            const KindTables &ka = gp.kts[(size_t)a.rung * 2 + a.kind], &kb = gp.kts[(size_t)b.rung * 2 + b.kind];
+            const int64_t ca = (int64_t)ka.h.nd * a.ncols * ka.srcH * (a.kind ? 2 : 1);
+            const int64_t cb = (int64_t)kb.h.nd * b.ncols * kb.srcH * (b.kind ? 2 : 1);
+            return ca > cb;
+        });
+        gp.stage_bytes = (int)align_up(max_stage, 16);
+        gp.lds_bytes = 2 * gp.stage_bytes + gp.ring_pairs * kLumaCols * 4;
+        if (gp.lds_bytes > 160 * 1024) return DTS_E_RANGE;
+    }
+    for (size_t i = 0; i < gp.kts.size(); ++i) {
+        if (!((gp.v4_mask >> i) & 1)) continue;
+        const Plan4 &pl = gp.p4[i];
+        for (int st = 0; st < pl.nstrips; ++st) {
+            Job4 j{};
+            j.rk = (int16_t)i;
+            j.kind = (int16_t)(i & 1);
+            j.rung = (int16_t)(i >> 1);
+            j.x0 = st * pl.C;
+            j.ncols = std::min(pl.C, gp.kts[i].dstW - j.x0);
+            j.group0 = st * 4;
+            gp.jobs4.push_back(j);
+        }
+    }
+    // heaviest strips first (H tap pairs x columns x source rows): a short tail
+    auto cost4 = [&](const Job4 &j) {
+        return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH * (j.kind ? 2 : 1);
+    };
+    std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(), [&](const Job4 &a, const Job4 &b) { return cost4(a) > cost4(b); });
+    if (gp.v4_mask) gp.lds4 = 4 * std::max(kRing4Slots * (kRing4ColsL + 1), 2 * kRing4Slots * (kRing4ColsC + 1));
+
+    dts_graph_info &in = gp.info;
+    in.src_frame_bytes = packed_bytes(s.src_w, s.src_h, s.src_fmt);
+    int64_t algo = in.src_frame_bytes;
+    for (int k = 0; k < s.nout; ++k) {
+        in.out_frame_bytes[k] = packed_bytes(s.out[k].w, s.out[k].h, s.out[k].fmt);
+        algo += in.out_frame_bytes[k];
+    }
+    if (s.quality) algo += in.out_frame_bytes[s.quality_out];
+    in.algo_bytes_per_frame = algo;
+    in.njobs = (int)(gp.jobs.size() + gp.jobs4.size());
+    in.lds_bytes = std::max(gp.lds_bytes, gp.lds4);
+    in.ladder_v4_mask = (int32_t)gp.v4_mask;
+    return DTS_OK;
 }
 
 } // namespace
@@ -307,163 +455,166 @@ int dts_frame_layout(int w, int h, int fmt, int64_t pitch[3], int64_t rows[3], i
 
 void dts_graph_destroy(dts_graph *g);
 
+// v3 tables (every kind; the v3 jobs cover the kinds not on v4) + its grid
+static int upload_v3(dts_graph *g, std::vector<KindTables> &kts)
+{
+    dts_ctx *ctx = g->ctx;
+    std::vector<uint8_t> blob;
+    struct Offs { size_t hpos, hbias, hch, hcl, vpos, vcoef, vlim; };
+    std::vector<Offs> offs(kts.size());
+    for (size_t i = 0; i < kts.size(); ++i) {
+        KindTables &kt = kts[i];
+        offs[i].hpos = push_blob(blob, kt.h.pos);
+        offs[i].hbias = push_blob(blob, kt.h.bias);
+        offs[i].hch = push_blob(blob, kt.h.hi);
+        offs[i].hcl = push_blob(blob, kt.h.lo);
+        offs[i].vpos = push_blob(blob, kt.v.pos);
+        offs[i].vcoef = push_blob(blob, kt.v.coef);
+        offs[i].vlim = push_blob(blob, kt.vlim);
+    }
+    const size_t jobs_off = push_blob(blob, g->jobs);
+    const size_t rk_off = align_up((int64_t)blob.size(), 256);
+    blob.resize(rk_off + kts.size() * sizeof(RungKind));
+    HIPCHK(ctx, hipMalloc(&g->dev_tables, blob.size()));
+    uint8_t *base = static_cast<uint8_t *>(g->dev_tables);
+    g->rk.resize(kts.size());
+    for (size_t i = 0; i < kts.size(); ++i) {
+        KindTables &kt = kts[i];
+        RungKind &r = g->rk[i];
+        r.dstW = kt.dstW;
+        r.dstH = kt.dstH;
+        r.nd = kt.h.nd;
+        r.nv = kt.v.nv;
+        r.nblocks = (int)kt.vlim.size();
+        r.hpos = reinterpret_cast<const int32_t *>(base + offs[i].hpos);
+        r.hbias = reinterpret_cast<const int32_t *>(base + offs[i].hbias);
+        r.hch = reinterpret_cast<const uint32_t *>(base + offs[i].hch);
+        r.hcl = reinterpret_cast<const uint32_t *>(base + offs[i].hcl);
+        r.vpos = reinterpret_cast<const int32_t *>(base + offs[i].vpos);
+        r.vcoef = reinterpret_cast<const uint32_t *>(base + offs[i].vcoef);
+        r.vlim = reinterpret_cast<const int32_t *>(base + offs[i].vlim);
+    }
+    std::memcpy(blob.data() + rk_off, g->rk.data(), kts.size() * sizeof(RungKind));
+    g->dev_jobs = reinterpret_cast<Job *>(base + jobs_off);
+    g->dev_rk = reinterpret_cast<RungKind *>(base + rk_off);
+    HIPCHK(ctx, hipMemcpy(g->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    if (!g->jobs.empty()) {      // persistent grid: resident workgroups per CU x CUs
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+            cus = 256;
+        const int bpc = ladder_blocks_per_cu(g->src_kind, g->ndmax, g->lds_bytes);
+        if (bpc < 1) return DTS_E_RANGE;
+        g->grid_cap = bpc * cus;
+    }
+    return DTS_OK;
+}
+
+// v4 tables of the kinds in v4_mask -> one device blob, plus its grid
+static int upload_v4(dts_graph *g, const GraphPlan &gp)
+{
+    dts_ctx *ctx = g->ctx;
+    const size_t nk = gp.p4.size();
+    std::vector<uint8_t> blob;
+    struct Offs { size_t groups = 0, hcoef = 0, vslot = 0, vcoef = 0, vlim = 0; };
+    std::vector<Offs> offs(nk);
+    for (size_t i = 0; i < nk; ++i) {
+        if (!((gp.v4_mask >> i) & 1)) continue;
+        const Plan4 &pl = gp.p4[i];
+        offs[i].groups = push_blob(blob, pl.groups);
+        offs[i].hcoef = push_blob(blob, pl.hcoef);
+        offs[i].vslot = push_blob(blob, pl.vslot);
+        offs[i].vcoef = push_blob(blob, pl.vcoef);
+        offs[i].vlim = push_blob(blob, pl.vlim);
+    }
+    const size_t jobs_off = push_blob(blob, gp.jobs4);
+    const size_t rk_off = (size_t)align_up((int64_t)blob.size(), 256);
+    blob.resize(rk_off + nk * sizeof(RungKind4));
+    HIPCHK(ctx, hipMalloc(&g->dev_tables4, blob.size()));
+    uint8_t *base = static_cast<uint8_t *>(g->dev_tables4);
+    std::vector<RungKind4> rk(nk);
+    for (size_t i = 0; i < nk; ++i) {
+        if (!((gp.v4_mask >> i) & 1)) continue;
+        const Plan4 &pl = gp.p4[i];
+        RungKind4 &r = rk[i];
+        r.N = pl.N;
+        r.NV = pl.NV;
+        r.nsteps = pl.nsteps;
+        r.groups = reinterpret_cast<const HGroup4 *>(base + offs[i].groups);
+        r.hcoef = reinterpret_cast<const uint32_t *>(base + offs[i].hcoef);
+        r.vslot = reinterpret_cast<const int32_t *>(base + offs[i].vslot);
+        r.vcoef = reinterpret_cast<const uint32_t *>(base + offs[i].vcoef);
+        r.vlim = reinterpret_cast<const int32_t *>(base + offs[i].vlim);
+    }
+    std::memcpy(blob.data() + rk_off, rk.data(), nk * sizeof(RungKind4));
+    HIPCHK(ctx, hipMemcpy(g->dev_tables4, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    g->dev_jobs4 = reinterpret_cast<Job4 *>(base + jobs_off);
+    g->dev_rk4 = reinterpret_cast<RungKind4 *>(base + rk_off);
+    g->njobs4 = (int)gp.jobs4.size();
+    g->lds4 = gp.lds4;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+        cus = 256;
+    const int bpc = ladder4_blocks_per_cu(g->src_kind, g->lds4);
+    if (bpc < 1) return DTS_E_RANGE;
+    g->grid4 = bpc * cus;
+    return DTS_OK;
+}
+
 int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
 {
     if (!ctx || !spec || !out) return DTS_E_INVAL;
     *out = nullptr;
-    const dts_graph_spec &s = *spec;
-    if (s.src_w < 4 || s.src_h < 4 || s.src_w > 16384 || s.src_h > 16384 || !fmt_in_ok(s.src_fmt)) return DTS_E_INVAL;
-    if (s.nout < 1 || s.nout > DTS_MAX_OUTPUTS) return DTS_E_INVAL;
-    for (int k = 0; k < s.nout; ++k) {
-        const dts_output_spec &o = s.out[k];
-        if (o.w < 2 || o.h < 2 || o.w > 16384 || o.h > 16384) return DTS_E_INVAL;
-        if (!fmt_out_ok(o.fmt)) return DTS_E_UNSUPPORTED;
-        if (!method_ok(o.method)) return DTS_E_UNSUPPORTED;
-    }
-    if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
-    if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
+    dts_graph *g = nullptr;
     try {
-        dts_graph *g = new dts_graph();
+        GraphPlan gp;
+        int e = make_plan(*spec, gp);
+        if (e) return e;
+        const dts_graph_spec &s = *spec;
+        g = new dts_graph();
         g->ctx = ctx;
         g->spec = s;
         g->batch = s.max_batch > 0 ? s.max_batch : 32;
-        g->src_kind = s.src_fmt == DTS_FMT_P010LE ? kSrcP010 : (s.src_fmt == DTS_FMT_NV12 ? kSrcNV12 : kSrcPlanar8);
-        const bool p010 = s.src_fmt == DTS_FMT_P010LE;
-
-        std::vector<KindTables> kts((size_t)s.nout * 2);
-        int ndmax_need = 1;
-        for (int k = 0; k < s.nout; ++k)
-            for (int kind = 0; kind < 2; ++kind) {
-                KindTables &kt = kts[(size_t)k * 2 + kind];
-                const int e = build_kind(s, k, kind, kt);
-                if (e) {
-                    delete g;
-                    return e;
-                }
-                ndmax_need = std::max(ndmax_need, kt.h.nd);
-                g->info.h_taps[k][kind] = kt.h.span;
-                g->info.v_taps[k][kind] = kt.v.span;
-                g->info.sws_h_size[k][kind] = kt.sws_h;
-                g->info.sws_v_size[k][kind] = kt.sws_v;
-            }
-        g->ndmax = ladder_ndmax_for(ndmax_need);
-        if (!g->ndmax) {
-            delete g;
-            return DTS_E_RANGE;
-        }
-        // ring size: smallest power of two holding every V window
-        int rp = 8;
-        for (; rp <= 256; rp *= 2) {
-            bool ok = true;
-            for (auto &kt : kts) ok = ok && plan_vlimits(kt.v, kt.srcH, kt.dstH, rp, kt.vlim);
-            if (ok) break;
-        }
-        if (rp > 256) {
-            delete g;
-            return DTS_E_RANGE;
-        }
-        g->ring_pairs = rp;
-        int max_stage = 0;
-        for (int k = 0; k < s.nout; ++k)
-            for (int kind = 0; kind < 2; ++kind) make_jobs(kts[(size_t)k * 2 + kind], k, kind, p010, g->jobs, max_stage);
-        // heaviest strips first (H taps x columns x source rows)
-        std::stable_sort(g->jobs.begin(), g->jobs.end(), [&](const Job &a, const Job &b) {
-            const KindTables &ka = kts[(size_t)a.rung * 2 + a.kind], &kb = kts[(size_t)b.rung * 2 + b.kind];
-            const int64_t ca = (int64_t)ka.h.nd * a.ncols * ka.srcH * (a.kind ? 2 : 1);
-            const int64_t cb = (int64_t)kb.h.nd * b.ncols * kb.srcH * (b.kind ? 2 : 1);
-            return ca > cb;
-        });
-        g->stage_bytes = (int)align_up(max_stage, 16);
-        g->lds_bytes = 2 * g->stage_bytes + rp * kLumaCols * 4;
-        if (g->lds_bytes > 160 * 1024) {
-            delete g;
-            return DTS_E_RANGE;
-        }
-
-        // upload tables
-        std::vector<uint8_t> blob;
-        struct Offs { size_t hpos, hbias, hch, hcl, vpos, vcoef, vlim; };
-        std::vector<Offs> offs(kts.size());
-        for (size_t i = 0; i < kts.size(); ++i) {
-            KindTables &kt = kts[i];
-            offs[i].hpos = push_blob(blob, kt.h.pos);
-            offs[i].hbias = push_blob(blob, kt.h.bias);
-            offs[i].hch = push_blob(blob, kt.h.hi);
-            offs[i].hcl = push_blob(blob, kt.h.lo);
-            offs[i].vpos = push_blob(blob, kt.v.pos);
-            offs[i].vcoef = push_blob(blob, kt.v.coef);
-            offs[i].vlim = push_blob(blob, kt.vlim);
-        }
-        const size_t jobs_off = push_blob(blob, g->jobs);
-        const size_t rk_off = align_up((int64_t)blob.size(), 256);
-        blob.resize(rk_off + kts.size() * sizeof(RungKind));
+        g->src_kind = gp.src_kind;
+        g->ndmax = gp.ndmax;
+        g->ring_pairs = gp.ring_pairs;
+        g->stage_bytes = gp.stage_bytes;
+        g->lds_bytes = gp.lds_bytes;
+        g->jobs = gp.jobs;
+        g->v4_mask = gp.v4_mask;
+        g->info = gp.info;
         hipSetDevice(ctx->device);
-        if (hipMalloc(&g->dev_tables, blob.size()) != hipSuccess) {
+        e = upload_v3(g, gp.kts);
+        if (!e && gp.v4_mask) e = upload_v4(g, gp);
+        if (!e && hipMalloc(&g->dev_queue, kQueueSlots * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
-            delete g;
-            return DTS_E_HIP;
+            e = DTS_E_HIP;
         }
-        uint8_t *base = static_cast<uint8_t *>(g->dev_tables);
-        g->rk.resize(kts.size());
-        for (size_t i = 0; i < kts.size(); ++i) {
-            KindTables &kt = kts[i];
-            RungKind &r = g->rk[i];
-            r.dstW = kt.dstW;
-            r.dstH = kt.dstH;
-            r.nd = kt.h.nd;
-            r.nv = kt.v.nv;
-            r.nblocks = (int)kt.vlim.size();
-            r.hpos = reinterpret_cast<const int32_t *>(base + offs[i].hpos);
-            r.hbias = reinterpret_cast<const int32_t *>(base + offs[i].hbias);
-            r.hch = reinterpret_cast<const uint32_t *>(base + offs[i].hch);
-            r.hcl = reinterpret_cast<const uint32_t *>(base + offs[i].hcl);
-            r.vpos = reinterpret_cast<const int32_t *>(base + offs[i].vpos);
-            r.vcoef = reinterpret_cast<const uint32_t *>(base + offs[i].vcoef);
-            r.vlim = reinterpret_cast<const int32_t *>(base + offs[i].vlim);
-        }
-        std::memcpy(blob.data() + rk_off, g->rk.data(), kts.size() * sizeof(RungKind));
-        g->dev_jobs = reinterpret_cast<Job *>(base + jobs_off);
-        g->dev_rk = reinterpret_cast<RungKind *>(base + rk_off);
-        if (hipMemcpy(g->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
-            ctx->last_hip = (int)hipGetLastError();
+        if (e) {
             dts_graph_destroy(g);
-            return DTS_E_HIP;
+            return e;
         }
-
-        // persistent grid: resident workgroups per CU x CUs; work counters
-        {
-            int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
-                cus = 256;
-            const int bpc = ladder_blocks_per_cu(g->src_kind, g->ndmax, g->lds_bytes);
-            if (bpc < 1) {
-                dts_graph_destroy(g);
-                return DTS_E_RANGE;
-            }
-            g->grid_cap = bpc * cus;
-            if (hipMalloc(&g->dev_queue, kQueueSlots * sizeof(unsigned int)) != hipSuccess) {
-                ctx->last_hip = (int)hipGetLastError();
-                dts_graph_destroy(g);
-                return DTS_E_HIP;
-            }
-        }
-
-        // info
-        g->info.src_frame_bytes = packed_bytes(s.src_w, s.src_h, s.src_fmt);
-        int64_t algo = g->info.src_frame_bytes;
-        for (int k = 0; k < s.nout; ++k) {
-            g->info.out_frame_bytes[k] = packed_bytes(s.out[k].w, s.out[k].h, s.out[k].fmt);
-            algo += g->info.out_frame_bytes[k];
-        }
-        if (s.quality) algo += g->info.out_frame_bytes[s.quality_out];
-        g->info.algo_bytes_per_frame = algo;
-        g->info.njobs = (int)g->jobs.size();
-        g->info.lds_bytes = g->lds_bytes;
-
         g->lay_src.init(s.src_w, s.src_h, s.src_fmt);
         for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt);
         if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt);
         *out = g;
+        return DTS_OK;
+    } catch (const std::bad_alloc &) {
+        if (g) dts_graph_destroy(g);
+        return DTS_E_NOMEM;
+    } catch (...) {
+        if (g) dts_graph_destroy(g);
+        return DTS_E_INVAL;
+    }
+}
+
+int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info)
+{
+    if (!spec || !info) return DTS_E_INVAL;
+    try {
+        GraphPlan gp;
+        const int e = make_plan(*spec, gp);
+        if (e) return e;
+        *info = gp.info;
         return DTS_OK;
     } catch (const std::bad_alloc &) {
         return DTS_E_NOMEM;
@@ -491,6 +642,7 @@ void dts_graph_destroy(dts_graph *g)
         if (g->done[sl]) hipEventDestroy(g->done[sl]);
     }
     if (g->dev_tables) hipFree(g->dev_tables);
+    if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_queue) hipFree(g->dev_queue);
     delete g;
 }
@@ -612,8 +764,9 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    // persistent grid over nframes x njobs items; items per launch bounded to 2^30
-    const int max_frames = std::max(1, (1 << 30) / std::max(1, p.njobs));
+    // persistent grids over nframes x njobs items (v4 kinds, then v3 kinds); items per launch < 2^30
+    const int njobs_max = std::max(1, std::max(p.njobs, g->njobs4));
+    const int max_frames = std::max(1, (1 << 30) / njobs_max);
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
         const int n = std::min(max_frames, nframes - f0);
         LadderParams pp = p;
@@ -624,9 +777,31 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
         pp.src.data[2] += (uint64_t)(f0 * src->frame_stride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
-        pp.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
-        HIPCHK(ctx, hipMemsetAsync(pp.queue, 0, sizeof(unsigned int), st));
-        HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, std::min(pp.nitems, g->grid_cap), st));
+        if (g->njobs4) {
+            Ladder4Params q{};
+            q.src = pp.src;
+            for (int k = 0; k < kMaxRungs; ++k) {
+                q.dst[k] = pp.dst[k];
+                q.dst_fmt[k] = pp.dst_fmt[k];
+            }
+            q.srcH = s.src_h;
+            q.chrH = (s.src_h + 1) >> 1;
+            q.ring = kRing4Slots;
+            q.src_kind = g->src_kind;
+            q.njobs = g->njobs4;
+            q.nframes = n;
+            q.nitems = n * g->njobs4;
+            q.jobs = g->dev_jobs4;
+            q.rk = g->dev_rk4;
+            q.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
+            HIPCHK(ctx, hipMemsetAsync(q.queue, 0, sizeof(unsigned int), st));
+            HIPCHK(ctx, launch_ladder4(q, g->lds4, std::min(q.nitems, g->grid4), st));
+        }
+        if (p.njobs) {
+            pp.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
+            HIPCHK(ctx, hipMemsetAsync(pp.queue, 0, sizeof(unsigned int), st));
+            HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, std::min(pp.nitems, g->grid_cap), st));
+        }
     }
     if (want_q) {
         const dts_output_spec &o = s.out[s.quality_out];

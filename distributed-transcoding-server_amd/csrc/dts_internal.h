@@ -80,6 +80,55 @@ struct LadderParams {
 };
 
 // ---------------------------------------------------------------------------
+// v4 ladder (ladder4.hip): row-pair H from VGPRs, LDS ring, per-column V
+// ---------------------------------------------------------------------------
+constexpr int kRing4ColsL = 64;     // luma output columns per strip (V: lane = column)
+constexpr int kRing4ColsC = 32;     // chroma output columns per strip and plane (lanes 0-31 U, 32-63 V)
+constexpr int kRing4Slots = 96;     // ring row pairs: one 64-pair step + up to 32 pairs of V reach
+
+struct HGroup4 {                    // one wave's share of a strip
+    uint64_t mask;                  // bit q: an output's window starts at sample pair q
+    int32_t lofs;                   // byte offset of the window in the source row (16-aligned, may be < 0)
+    int16_t nload;                  // 16-byte loads per row (per plane)
+    int16_t qend;                   // 1 + last start pair (0: no outputs)
+    int32_t coef;                   // first tap-pair dword of the group in its H table
+    int32_t col0;                   // ring column of the group's first output
+};
+
+struct Job4 {                       // one strip of one (rendition, kind)
+    int16_t rk;                     // rung * 2 + kind
+    int16_t kind;
+    int16_t rung;
+    int16_t pad_;
+    int32_t x0, ncols, group0;      // first output column, columns, first HGroup4
+};
+
+struct RungKind4 {
+    int32_t N;                      // H tap pairs per output (kernel bucket)
+    int32_t NV;                     // V row pairs per output row
+    int32_t nsteps;                 // 128-row source steps
+    int32_t pad_;
+    const HGroup4 *groups;          // [strips][4]
+    const uint32_t *hcoef;          // int16x2 tap pairs, group after group
+    const int32_t *vslot;           // [dstH] ring slot of the first row pair
+    const uint32_t *vcoef;          // [dstH][NV] int16x2
+    const int32_t *vlim;            // [nsteps] output rows finished after step b
+};
+
+struct Ladder4Params {
+    DevPlanes src;
+    DevPlanes dst[kMaxRungs];
+    int32_t dst_fmt[kMaxRungs];
+    int32_t srcH, chrH, ring, src_kind, njobs, nitems, nframes, pad_;
+    const Job4 *jobs;
+    const RungKind4 *rk;
+    unsigned int *queue;
+};
+
+hipError_t launch_ladder4(const Ladder4Params &p, int lds_bytes, int grid, hipStream_t s);
+int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
+
+// ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
 // ---------------------------------------------------------------------------
 constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x

@@ -351,6 +351,147 @@ int pack_v(const SwsFilter &f, int n, VTable &out)
     return DTS_OK;
 }
 
+namespace {
+const int kN4[] = {2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 14, 16};   // ladder4.hip hdispatch cases
+
+// pair positions the unrolled H code of ladder4.hip handles (its qmax4)
+int qmax4(int n, int cap) { return std::min(std::min(4 * n + 8, cap - n + 1), 64); }
+
+struct Group4Ctx {
+    const SwsFilter &fh;
+    const std::vector<int> &a, &z;   // first / last nonzero source sample per output
+    int bps, nlmax, cap, N;
+    int64_t row_bytes;
+};
+
+// Fits outputs [i0, i1) into one wave group: a 16-B aligned window whose
+// sample pairs hold every output's taps, one output per start pair (earlier
+// starts for outputs whose first taps coincide, e.g. at the left edge where
+// initFilter folds taps onto sample 0; the window may begin left of the row,
+// those chunks read as zero).  Fills h and p (start pair per output).
+bool fit_group(const Group4Ctx &c, int i0, int i1, HGroup4 &h, std::vector<int> &p)
+{
+    const int64_t L = ((int64_t)c.a[i0] * c.bps) & ~(int64_t)15;
+    for (int64_t pad = 0; pad <= 32; pad += 16) {
+        const int64_t lofs = L - pad;
+        const int X0 = (int)(lofs / c.bps);
+        bool ok = true;
+        for (int i = i1 - 1; i >= i0 && ok; --i) {
+            if (c.a[i] < X0) {
+                ok = false;
+                break;
+            }
+            int pi = (c.a[i] - X0) >> 1;
+            if (i + 1 < i1) pi = std::min(pi, p[i + 1] - 1);
+            if (pi < 0 || ((c.z[i] - X0) >> 1) - pi + 1 > c.N) ok = false;
+            p[i] = pi;
+        }
+        if (!ok) continue;
+        const int last = p[i1 - 1];
+        const int pairs = last + c.N;
+        if (last + 1 > qmax4(c.N, c.cap) || pairs > c.cap) continue;
+        int64_t nload = ((int64_t)pairs * 2 * c.bps + 15) / 16;
+        nload = std::min(nload, (c.row_bytes - lofs + 15) / 16);
+        if (nload > c.nlmax || nload < 1) continue;
+        h.lofs = (int32_t)lofs;
+        h.nload = (int16_t)nload;
+        h.qend = (int16_t)(last + 1);
+        h.mask = 0;
+        for (int i = i0; i < i1; ++i) h.mask |= 1ull << p[i];
+        return true;
+    }
+    return false;
+}
+
+uint32_t pack_pair(int c0, int c1)
+{
+    return (uint32_t)(uint16_t)(int16_t)c0 | ((uint32_t)(uint16_t)(int16_t)c1 << 16);
+}
+} // namespace
+
+bool plan4_kind(const SwsFilter &fh, const VTable &v, int srcH, int dstW, int dstH, int bps, int nlmax, int cap,
+                int maxcols, int64_t row_bytes, int ring, Plan4 &out)
+{
+    if (v.nv < 1 || v.nv > 16 || v.nv > ring - 64 || dstW < 1 || dstH < 1) return false;
+    if ((int64_t)dstW * bps > row_bytes) return false;      // horizontal upscale: v3
+    std::vector<int> a(dstW), z(dstW), p(dstW);
+    int nmin = 1;
+    for (int i = 0; i < dstW; ++i) {
+        int j0, j1;
+        nonzero_extent(fh, i, j0, j1);
+        a[i] = fh.pos[i] + j0;
+        z[i] = fh.pos[i] + j1;
+        nmin = std::max(nmin, (z[i] - (a[i] & ~1)) / 2 + 1);
+    }
+    // V: ring slots and the output rows each 64-pair step completes
+    Plan4 base;
+    base.NV = v.nv;
+    const int pairs_total = (srcH + 1) / 2;
+    base.nsteps = (pairs_total + 63) / 64;
+    base.vslot.resize(dstH);
+    for (int y = 0; y < dstH; ++y) base.vslot[y] = (v.pos[y] / 2) % ring;
+    base.vcoef = v.coef;
+    base.vlim.assign(base.nsteps, 0);
+    {
+        int y = 0;
+        for (int b = 0; b < base.nsteps; ++b) {
+            const int done = std::min(64 * (b + 1), pairs_total);
+            while (y < dstH && std::min(v.pos[y] / 2 + v.nv, pairs_total) <= done) {
+                if (v.pos[y] / 2 < 64 * (b + 1) - ring) return false;   // window left the ring
+                ++y;
+            }
+            base.vlim[b] = y;
+        }
+        if (y != dstH) return false;
+    }
+    // H: smallest tap-pair bucket, then the widest strip whose columns fit four wave groups
+    for (int N : kN4) {
+        if (N < nmin) continue;
+        // outputs whose starts crowd into the same pair (ratios < 2, upscaling) are pushed to
+        // earlier pairs at the price of wider windows; past 2 wasted tap pairs v3 is cheaper
+        if (N > nmin + 2) break;
+        const Group4Ctx c{fh, a, z, bps, nlmax, cap, N, row_bytes};
+        for (int C = maxcols; C >= maxcols / 2; C -= 8) {   // narrower strips idle too many V lanes
+            Plan4 pl = base;
+            pl.N = N;
+            pl.C = C;
+            pl.nstrips = (dstW + C - 1) / C;
+            bool ok = true;
+            for (int s = 0; s < pl.nstrips && ok; ++s) {
+                const int x0 = s * C, x1 = std::min(x0 + C, dstW);
+                int i = x0;
+                for (int g = 0; g < 4; ++g) {
+                    HGroup4 h{};
+                    h.col0 = i - x0;
+                    h.coef = (int32_t)pl.hcoef.size();
+                    const int rem = x1 - i;
+                    if (rem > 0) {
+                        int k = (rem + (3 - g)) / (4 - g);
+                        while (k > 0 && !fit_group(c, i, i + k, h, p)) --k;
+                        if (k == 0) {
+                            ok = false;
+                            break;
+                        }
+                        const int X0 = (int)(h.lofs / bps);
+                        for (int o = i; o < i + k; ++o)
+                            for (int t = 0; t < N; ++t) {
+                                const int x = X0 + 2 * (p[o] + t);
+                                pl.hcoef.push_back(pack_pair(tap_at(fh, o, x), tap_at(fh, o, x + 1)));
+                            }
+                        i += k;
+                    }
+                    pl.groups.push_back(h);
+                }
+                if (i < x1) ok = false;
+            }
+            if (!ok) continue;
+            out = std::move(pl);
+            return true;
+        }
+    }
+    return false;
+}
+
 bool plan_vlimits(const VTable &v, int srcH, int dstH, int ring_pairs, std::vector<int32_t> &vlim)
 {
     const int srcHe = (srcH + 1) & ~1;

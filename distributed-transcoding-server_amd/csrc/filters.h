@@ -14,6 +14,8 @@
 #include <stdint.h>
 #include <vector>
 
+#include "dts_internal.h"
+
 namespace dts {
 
 struct SwsFilter {
@@ -52,5 +54,26 @@ int pack_v(const SwsFilter &f, int dstN, VTable &out);
 // available, for each pipeline step of kBlkRows rows.  Also checks the ring
 // capacity (pairs); returns false if the ring is too small.
 bool plan_vlimits(const VTable &v, int srcH, int dstH, int ring_pairs, std::vector<int32_t> &vlim);
+
+// v4 ladder plan of one (rendition, plane kind) (ladder4.hip): strips of C
+// output columns, each split into four wave groups.
+struct Plan4 {
+    int N = 0;                       // H tap pairs per output (kernel bucket)
+    int NV = 0;                      // V row pairs per output row
+    int C = 0, nstrips = 0, nsteps = 0;
+    std::vector<HGroup4> groups;     // [nstrips][4]
+    std::vector<uint32_t> hcoef;     // int16x2 tap pairs, group after group
+    std::vector<int32_t> vslot, vlim;
+    std::vector<uint32_t> vcoef;     // [dstH][NV]
+};
+
+// fh: the libswscale H filter; v: the packed V table; bps: bytes per sample
+// in the source row (1 u8, 2 nv12 chroma / p010 luma, 4 p010 chroma); nlmax:
+// 16-B loads per row the kernel holds; cap: sample pairs its H code
+// addresses; row_bytes: source row bytes; ring: ring slots.  Returns false
+// when the geometry does not fit k_ladder4 (upscaling, > 16 tap pairs ...):
+// that (rendition, kind) then runs on the v3 kernel.
+bool plan4_kind(const SwsFilter &fh, const VTable &v, int srcH, int dstW, int dstH, int bps, int nlmax, int cap,
+                int maxcols, int64_t row_bytes, int ring, Plan4 &out);
 
 } // namespace dts

@@ -71,7 +71,8 @@ class GraphInfo(ctypes.Structure):
                 ("lds_bytes", ctypes.c_int32), ("h_taps", (ctypes.c_int32 * 2) * MAX_OUTPUTS),
                 ("v_taps", (ctypes.c_int32 * 2) * MAX_OUTPUTS),
                 ("sws_h_size", (ctypes.c_int32 * 2) * MAX_OUTPUTS),
-                ("sws_v_size", (ctypes.c_int32 * 2) * MAX_OUTPUTS)]
+                ("sws_v_size", (ctypes.c_int32 * 2) * MAX_OUTPUTS), ("ladder_v4_mask", ctypes.c_int32),
+                ("h_pairs4", (ctypes.c_int32 * 2) * MAX_OUTPUTS)]
 
 
 # Every symbol include/dts.h declares (checked by tests/test_abi.py).
@@ -79,7 +80,7 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_ctx_last_hip_error", "dts_graph_create", "dts_graph_destroy", "dts_graph_info_get",
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
-           "dts_sws_filter", "dts_fps_map"]
+           "dts_sws_filter", "dts_fps_map", "dts_graph_plan"]
 
 _lib = None
 
@@ -105,6 +106,7 @@ def lib():
     L.dts_graph_destroy.argtypes = [vp]
     L.dts_graph_destroy.restype = None
     L.dts_graph_info_get.argtypes = [vp, ctypes.POINTER(GraphInfo)]
+    L.dts_graph_plan.argtypes = [ctypes.POINTER(GraphSpec), ctypes.POINTER(GraphInfo)]
     L.dts_graph_submit.argtypes = [vp, ctypes.POINTER(Frame), i32, ctypes.POINTER(Frame),
                                    ctypes.POINTER(Frame), ctypes.POINTER(QStat)]
     L.dts_graph_wait.argtypes = [vp]
@@ -203,6 +205,13 @@ def qstat_finalize(w, h, raws):
     out = (QStat * n)()
     check(lib().dts_qstat_finalize(w, h, arr, n, out), "qstat_finalize")
     return [out[i].as_dict() for i in range(n)]
+
+
+def graph_plan(spec):
+    """dts_graph_plan: the graph's info (filter sizes, kernel choice) without a device."""
+    info = GraphInfo()
+    check(lib().dts_graph_plan(ctypes.byref(spec), ctypes.byref(info)), "graph_plan")
+    return info
 
 
 def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0):

@@ -133,6 +133,9 @@ typedef struct dts_graph_info {
     int32_t v_taps[DTS_MAX_OUTPUTS][2]; /* GPU V tap span (luma, chroma) per output */
     int32_t sws_h_size[DTS_MAX_OUTPUTS][2]; /* libswscale filter sizes (luma, chroma) */
     int32_t sws_v_size[DTS_MAX_OUTPUTS][2];
+    int32_t ladder_v4_mask;             /* bit 2*output+kind: that plane kind runs on the v4
+                                           ladder kernel (the rest on v3; DTS_LADDER=3 forces v3) */
+    int32_t h_pairs4[DTS_MAX_OUTPUTS][2]; /* v4 H tap pairs per output (luma, chroma), 0 = v3 */
 } dts_graph_info;
 
 const char *dts_version(void);
@@ -146,6 +149,9 @@ int dts_ctx_last_hip_error(const dts_ctx *ctx);
 int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out);
 void dts_graph_destroy(dts_graph *g);
 int dts_graph_info_get(const dts_graph *g, dts_graph_info *info);
+/* Plan only: validates spec and fills info (filter sizes, kernel choice,
+ * work items) exactly as dts_graph_create would, without a device. */
+int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info);
 
 /* Host-memory path (the Node worker's path).  dst holds nframes*nout frames,
  * frame-major (dst[f*nout + k]).  qref/q may be NULL when quality is off.

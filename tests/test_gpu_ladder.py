@@ -16,6 +16,17 @@ pytestmark = pytest.mark.gpu
 BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
 
 
+@pytest.fixture(autouse=True, params=["v4", "v3"])
+def ladder_kernel(request, monkeypatch):
+    """Every parity case runs twice: with the v4 kernel wherever the geometry
+    fits it (the default) and with DTS_LADDER=3 (v3 kernel for every plane)."""
+    if request.param == "v3":
+        monkeypatch.setenv("DTS_LADDER", "3")
+    else:
+        monkeypatch.delenv("DTS_LADDER", raising=False)
+    return request.param
+
+
 def run_and_check(ctx, sw, sh, sfmt, outs, frames):
     g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, outs))
     got, _ = g.run_host(frames)
@@ -72,11 +83,25 @@ def test_params_bicubic_b_c(ctx):
                                                  (90, 50, D.FMT_NV12, LAN, (2.0, D.PARAM_DEFAULT))], frames)
 
 
-def test_ladder_4k_one_frame(ctx):
+def test_ladder_4k_one_frame(ctx, ladder_kernel):
     """BASELINE config 2 geometry at full size, one frame, bit-exact."""
     frames = [D.synth_host(3840, 2160, D.FMT_YUV420P, 0, 0x5EED, 0)]
     outs = [(1920, 1080, D.FMT_NV12, BIC), (1280, 720, D.FMT_NV12, BIC), (854, 480, D.FMT_NV12, BIC)]
+    g = D.Graph(ctx, D.make_spec(3840, 2160, D.FMT_YUV420P, outs))
+    assert g.info.ladder_v4_mask == (0x3f if ladder_kernel == "v4" else 0)
+    g.close()
     run_and_check(ctx, 3840, 2160, D.FMT_YUV420P, outs, frames)
+
+
+@pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
+@pytest.mark.parametrize("method", [BIC, LAN, BIL, D.SCALE_GAUSS])
+def test_downscales_every_source(ctx, sfmt, method):
+    """Downscale ratios 1.5 .. 5 from every source format, odd output sizes (the
+    v4 kernel's domain: strips, wave groups, left-edge folded taps, ring wrap)."""
+    rng = np.random.default_rng(11 + sfmt + method)
+    frames = [random_frame(520, 300, sfmt, rng), D.synth_host(520, 300, sfmt, 0, 5, 2)]
+    run_and_check(ctx, 520, 300, sfmt, [(346, 200, D.FMT_NV12, method), (260, 150, D.FMT_YUV420P, method),
+                                        (171, 97, D.FMT_NV12, method), (104, 60, D.FMT_NV12, method)], frames)
 
 
 def test_p010_4k_to_1080p(ctx):

@@ -102,3 +102,33 @@ def test_qstat_finalize_matches_vf_psnr_vf_ssim():
     assert q["ssim"] == pytest.approx([0.9, 1.0, 0.5])
     ssim = (0.9 * 64 * 48 + 1.0 * 32 * 24 + 0.5 * 32 * 24) / area
     assert q["ssim_all"] == pytest.approx(ssim) and q["ssim_db"] == pytest.approx(-10 * math.log10(1 - ssim))
+
+
+LADDER4K = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_NV12, D.SCALE_BICUBIC),
+            (854, 480, D.FMT_NV12, D.SCALE_BICUBIC)]
+
+
+@pytest.mark.parametrize("fmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
+def test_plan_bench_ladder_runs_on_v4(fmt, monkeypatch):
+    """The BASELINE cfg2/cfg3 geometries plan every plane kind onto the v4 kernel;
+    DTS_LADDER=3 moves them all back to v3."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    info = D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K))
+    # p010 chroma of the 480p rung: 4-byte (U16,V16) samples leave the v4 window too few pairs
+    assert info.ladder_v4_mask == (0x1f if fmt == D.FMT_P010LE else 0x3f)
+    assert [list(p) for p in info.h_pairs4][:3] == [[5, 5], [6, 6], [10, 0 if fmt == D.FMT_P010LE else 10]]
+    assert info.njobs > 0 and info.lds_bytes <= 64 * 1024
+    monkeypatch.setenv("DTS_LADDER", "3")
+    assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v4_mask == 0
+
+
+def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
+    """Upscales stay on v3; the downscale output of the same graph still plans to v4."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    info = D.graph_plan(D.make_spec(640, 360, D.FMT_YUV420P, [(1280, 720, D.FMT_NV12, D.SCALE_BICUBIC),
+                                                              (320, 180, D.FMT_NV12, D.SCALE_BICUBIC)]))
+    assert info.ladder_v4_mask & 0x3 == 0 and info.ladder_v4_mask & 0xc == 0xc
+    assert D.graph_plan(D.make_spec(7680, 4320, D.FMT_YUV420P,
+                                    [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)])).ladder_v4_mask == 0x3
+    with pytest.raises(D.DtsError):
+        D.graph_plan(D.make_spec(2, 2, D.FMT_YUV420P, LADDER4K))

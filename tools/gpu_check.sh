@@ -27,6 +27,8 @@ for s in "$@"; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 300 python -u bench.py --steps 20 --warmup 3 ;;
     benchq) step benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu ;;
+    benchv3) DTS_LADDER=3 step benchv3 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
+    v4small) step v4small 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "v4 and (small or 4k_one)" ;;
     *) echo "unknown step $s" ;;
   esac
 done
