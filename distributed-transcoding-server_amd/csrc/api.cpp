@@ -367,7 +367,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
         return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH * (j.kind ? 2 : 1);
     };
     std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(), [&](const Job4 &a, const Job4 &b) { return cost4(a) > cost4(b); });
-    if (gp.v4_mask) gp.lds4 = 4 * std::max(kRing4Slots * (kRing4ColsL + 1), 2 * kRing4Slots * (kRing4ColsC + 1));
+    if (gp.v4_mask) gp.lds4 = kLds4Bytes;
 
     dts_graph_info &in = gp.info;
     in.src_frame_bytes = packed_bytes(s.src_w, s.src_h, s.src_fmt);

@@ -85,6 +85,11 @@ struct LadderParams {
 constexpr int kRing4ColsL = 64;     // luma output columns per strip (V: lane = column)
 constexpr int kRing4ColsC = 32;     // chroma output columns per strip and plane (lanes 0-31 U, 32-63 V)
 constexpr int kRing4Slots = 96;     // ring row pairs: one 64-pair step + up to 32 pairs of V reach
+constexpr int kRing4Dw = 2 * kRing4Slots * (kRing4ColsC + 1);   // ring dwords (chroma: 2 planes, >= luma)
+constexpr int kH4CoefDw = 256;      // LDS tap pairs per wave group (outputs x N rounded up to 4)
+constexpr int kV4CoefDw = 1152;     // LDS V tap pairs per step buffer (rows x NV rounded up to 4)
+constexpr int kV4SlotMax = 144;     // output rows per step buffer
+constexpr int kLds4Bytes = 4 * (kRing4Dw + 4 * kH4CoefDw + 2 * kV4CoefDw + 2 * kV4SlotMax);
 
 struct HGroup4 {                    // one wave's share of a strip
     uint64_t mask;                  // bit q: an output's window starts at sample pair q
@@ -109,9 +114,9 @@ struct RungKind4 {
     int32_t nsteps;                 // 128-row source steps
     int32_t pad_;
     const HGroup4 *groups;          // [strips][4]
-    const uint32_t *hcoef;          // int16x2 tap pairs, group after group
+    const uint32_t *hcoef;          // int16x2 tap pairs, round_up(N, 4) per output, group after group
     const int32_t *vslot;           // [dstH] ring slot of the first row pair
-    const uint32_t *vcoef;          // [dstH][NV] int16x2
+    const uint32_t *vcoef;          // [dstH][round_up(NV, 4)] int16x2
     const int32_t *vlim;            // [nsteps] output rows finished after step b
 };
 

@@ -390,6 +390,7 @@ bool fit_group(const Group4Ctx &c, int i0, int i1, HGroup4 &h, std::vector<int> 
         const int last = p[i1 - 1];
         const int pairs = last + c.N;
         if (last + 1 > qmax4(c.N, c.cap) || pairs > c.cap) continue;
+        if ((i1 - i0) * ((c.N + 3) & ~3) > kH4CoefDw) continue;          // the group's taps in LDS
         int64_t nload = ((int64_t)pairs * 2 * c.bps + 15) / 16;
         nload = std::min(nload, (c.row_bytes - lofs + 15) / 16);
         if (nload > c.nlmax || nload < 1) continue;
@@ -428,18 +429,23 @@ bool plan4_kind(const SwsFilter &fh, const VTable &v, int srcH, int dstW, int ds
     base.NV = v.nv;
     const int pairs_total = (srcH + 1) / 2;
     base.nsteps = (pairs_total + 63) / 64;
+    const int nvp = (v.nv + 3) & ~3;                          // LDS rows are 16-B aligned
     base.vslot.resize(dstH);
     for (int y = 0; y < dstH; ++y) base.vslot[y] = (v.pos[y] / 2) % ring;
-    base.vcoef = v.coef;
+    base.vcoef.assign((size_t)dstH * nvp, 0);
+    for (int y = 0; y < dstH; ++y)
+        for (int t = 0; t < v.nv; ++t) base.vcoef[(size_t)y * nvp + t] = v.coef[(size_t)y * v.nv + t];
     base.vlim.assign(base.nsteps, 0);
     {
         int y = 0;
         for (int b = 0; b < base.nsteps; ++b) {
-            const int done = std::min(64 * (b + 1), pairs_total);
+            const int done = std::min(64 * (b + 1), pairs_total), y0 = y;
             while (y < dstH && std::min(v.pos[y] / 2 + v.nv, pairs_total) <= done) {
                 if (v.pos[y] / 2 < 64 * (b + 1) - ring) return false;   // window left the ring
                 ++y;
             }
+            // the step's V taps and slots are staged in LDS
+            if (y - y0 > kV4SlotMax || (y - y0) * nvp > kV4CoefDw) return false;
             base.vlim[b] = y;
         }
         if (y != dstH) return false;
@@ -474,9 +480,9 @@ bool plan4_kind(const SwsFilter &fh, const VTable &v, int srcH, int dstW, int ds
                         }
                         const int X0 = (int)(h.lofs / bps);
                         for (int o = i; o < i + k; ++o)
-                            for (int t = 0; t < N; ++t) {
+                            for (int t = 0; t < ((N + 3) & ~3); ++t) {    // rows of 16 B in LDS
                                 const int x = X0 + 2 * (p[o] + t);
-                                pl.hcoef.push_back(pack_pair(tap_at(fh, o, x), tap_at(fh, o, x + 1)));
+                                pl.hcoef.push_back(t < N ? pack_pair(tap_at(fh, o, x), tap_at(fh, o, x + 1)) : 0u);
                             }
                         i += k;
                     }

@@ -24,6 +24,10 @@
 //  The next step's source rows are in flight while V runs on the ring.
 #include "dts_internal.h"
 
+#ifndef DTS_L4_ABLATE
+#define DTS_L4_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads
+#endif
+
 namespace dts {
 
 __constant__ uint8_t c_dither_l4[8][8] = DTS_DITHER_8X8_128;
@@ -54,10 +58,10 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ uint32_t shr6(uint32_t d)
+__device__ __forceinline__ uint32_t shr(uint32_t d, uint32_t sh)
 {
     ushort2v v = __builtin_bit_cast(ushort2v, d);
-    v = v >> (ushort2v){6, 6};
+    v = v >> (ushort2v){(unsigned short)sh, (unsigned short)sh};
     return __builtin_bit_cast(uint32_t, v);
 }
 
@@ -66,13 +70,16 @@ __device__ __forceinline__ uint32_t shr6(uint32_t d)
 //   NV  : nv12 interleaved chroma, sel picks U or V (input.c nv12ToUV_c)
 //   P16 : p010 luma, LE16 >> 6 (input.c p010LEToY_c)
 //   P16C: p010 interleaved chroma (U16,V16 dwords) >> 6, sel picks U or V (p010LEToUV_c)
+// z is an opaque zero private to each hpass instantiation: without it the
+// identical conversions of every tap-count variant are merged and hoisted in
+// front of hdispatch's switch, where they all stay live at once.
 template <int CVT>
-__device__ __forceinline__ uint32_t pair_at(const uint32_t (&r)[32], int q, uint32_t sel)
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&r)[32], int q, uint32_t sel, uint32_t z)
 {
-    if (CVT == kCvtP8) return perm(0u, r[q >> 1], (q & 1) ? 0x0c030c02u : 0x0c010c00u);
-    if (CVT == kCvtNV) return perm(0u, r[q], sel);
-    if (CVT == kCvtP16) return shr6(r[q]);
-    return shr6(perm(r[2 * q + 1], r[2 * q], sel));
+    if (CVT == kCvtP8) return perm(0u, r[q >> 1], ((q & 1) ? 0x0c030c02u : 0x0c010c00u) ^ z);
+    if (CVT == kCvtNV) return perm(0u, r[q], sel ^ z);
+    if (CVT == kCvtP16) return shr(r[q], 6u + z);
+    return shr(perm(r[2 * q + 1], r[2 * q], sel ^ z), 6u + z);
 }
 
 // pair positions the unrolled H code handles (= filters.cpp qmax4)
@@ -84,36 +91,53 @@ constexpr int qmax4(int n, int cap)
 
 // Horizontal FIR of one wave over its row pair for every output whose window
 // starts at a pair position q < qend with bit q of mask set.  Outputs are
-// visited in column order; their N int16x2 tap pairs follow each other at cp,
-// their ring dwords follow each other at wp.
+// visited in column order; their N int16x2 tap pairs (rows of NP = N rounded
+// up to 4 dwords) follow each other in LDS at cl and are read with wave-wide
+// broadcast ds_read_b128; their ring dwords follow each other at wp.
 template <int CVT, int N, int QMAX, int SH>
 __device__ __forceinline__ void hpass(const uint32_t (&ra)[32], const uint32_t (&rb)[32], uint32_t sel,
-                                      uint64_t mask, int qend, k_u32 *cp, uint32_t *wp)
+                                      uint64_t mask, int qend, const uint32_t *cl, uint32_t *wp)
 {
-    uint32_t pa[QMAX + N - 1], pb[QMAX + N - 1];
+    constexpr int NP = (N + 3) & ~3;
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    uint32_t pa[QMAX + N + 7], pb[QMAX + N + 7];
 #pragma unroll
     for (int q = 0; q < N - 1; ++q) {
-        pa[q] = pair_at<CVT>(ra, q, sel);
-        pb[q] = pair_at<CVT>(rb, q, sel);
+        pa[q] = pair_at<CVT>(ra, q, sel, z);
+        pb[q] = pair_at<CVT>(rb, q, sel, z);
     }
+    const uint4 *cv = reinterpret_cast<const uint4 *>(cl);
     // a constant trip count (no early exit) keeps the loop fully unrolled, so
-    // every pa/pb index is a compile-time register
+    // every pa/pb index is a compile-time register; qend is tested once per 8
+    // positions, the output mask once per position
 #pragma unroll
-    for (int q = 0; q < QMAX; ++q) {
-        if (q < qend) {
-            pa[q + N - 1] = pair_at<CVT>(ra, q + N - 1, sel);
-            pb[q + N - 1] = pair_at<CVT>(rb, q + N - 1, sel);
-            if ((mask >> q) & 1) {
-                int a = 0, b = 0;
+    for (int q8 = 0; q8 < QMAX; q8 += 8) {
+        if (q8 < qend) {
 #pragma unroll
-                for (int t = 0; t < N; ++t) {
-                    const uint32_t c = cp[t];
-                    a = dot2(pa[q + t], c, a);
-                    b = dot2(pb[q + t], c, b);
+            for (int q = q8; q < q8 + 8 && q < QMAX; ++q) {
+                pa[q + N - 1] = pair_at<CVT>(ra, q + N - 1, sel, z);
+                pb[q + N - 1] = pair_at<CVT>(rb, q + N - 1, sel, z);
+                if ((uint32_t)(mask >> q) & 1u) {
+                    uint32_t c[NP];
+#pragma unroll
+                    for (int i = 0; i < NP / 4; ++i) {
+                        const uint4 v = cv[i];
+                        c[4 * i + 0] = v.x;
+                        c[4 * i + 1] = v.y;
+                        c[4 * i + 2] = v.z;
+                        c[4 * i + 3] = v.w;
+                    }
+                    cv += NP / 4;
+                    int a = 0, b = 0;
+#pragma unroll
+                    for (int t = 0; t < N; ++t) {
+                        a = dot2(pa[q + t], c[t], a);
+                        b = dot2(pb[q + t], c[t], b);
+                    }
+                    // FFMIN(val >> sh, 32767) for both rows (val >> sh >= -32768 always holds)
+                    *wp++ = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(a >> SH, b >> SH));
                 }
-                cp += N;
-                // FFMIN(val >> sh, 32767) for both rows (val >> sh >= -32768 always holds)
-                *wp++ = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(a >> SH, b >> SH));
             }
         }
     }
@@ -133,7 +157,7 @@ __device__ __forceinline__ T kload(const T *p)
 
 template <int CVT, int CAP, int SH>
 __device__ __forceinline__ void hdispatch(int N, const uint32_t (&ra)[32], const uint32_t (&rb)[32], uint32_t sel,
-                                          uint64_t mask, int qend, k_u32 *cp, uint32_t *wp)
+                                          uint64_t mask, int qend, const uint32_t *cp, uint32_t *wp)
 {
     switch (N) {                                             // wave-uniform
 #define DTS_H4(n) \
@@ -147,36 +171,88 @@ __device__ __forceinline__ void hdispatch(int N, const uint32_t (&ra)[32], const
 }
 
 // Vertical FIR of one output row for one lane: NV ring dwords (row pairs)
-// from slot s0 on (wrapping at R), wave-uniform tap pairs at cq.
+// from slot s0 on (wrapping at R), wave-uniform tap pairs in LDS at cq
+// (broadcast reads).
 template <int CP, int NV>
-__device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, k_u32 *cq, int acc)
+__device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, const uint32_t *cq, int acc)
 {
+    constexpr int NVP = (NV + 3) & ~3;
+    uint32_t c[NVP];
+#pragma unroll
+    for (int i = 0; i < NVP / 4; ++i) {
+        const uint4 v = reinterpret_cast<const uint4 *>(cq)[i];
+        c[4 * i + 0] = v.x;
+        c[4 * i + 1] = v.y;
+        c[4 * i + 2] = v.z;
+        c[4 * i + 3] = v.w;
+    }
     if (s0 + NV <= R) {
         const uint32_t *b = rl + s0 * CP;
 #pragma unroll
-        for (int t = 0; t < NV; ++t) acc = dot2(b[t * CP], cq[t], acc);
+        for (int t = 0; t < NV; ++t) acc = dot2(b[t * CP], c[t], acc);
     } else {
 #pragma unroll
         for (int t = 0; t < NV; ++t) {
             int s = s0 + t;
             if (s >= R) s -= R;
-            acc = dot2(rl[s * CP], cq[t], acc);
+            acc = dot2(rl[s * CP], c[t], acc);
         }
     }
     return acc;
 }
 
-template <int CP>
-__device__ __forceinline__ int vtaps_any(const uint32_t *rl, int R, int s0, int nv, k_u32 *cq, int acc)
+// yuv2planeX_8 / yuv2nv12cX accumulator start for output row y: the dither
+// (flat 64 for 8-bit sources, this lane's ff_dither_8x8_128 column, packed in
+// dlo/dhi, for >8-bit sources) << 12
+template <int SRC>
+__device__ __forceinline__ int vinit(int y, uint32_t dlo, uint32_t dhi)
 {
-    switch (nv) {                                            // wave-uniform
+    if (SRC != kSrcP010) return 64 << 12;
+    const uint32_t dw = (y & 4) ? dhi : dlo;
+    return (int)((dw >> (8 * (y & 3))) & 255u) << 12;
+}
+
+__device__ __forceinline__ void vstore(uint64_t p, int acc)
+{
+    int v = acc >> 19;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    *GP(g_u8, p) = (uint8_t)v;
+}
+
+// The output rows [vlo, vhi) of one V step, rows vlo + wave + 4i for this
+// wave, two rows per iteration.  vsl / vco: the step's ring slots and tap
+// pairs staged in LDS (row y at index y - vlo).
+template <int SRC, int CP, int NV>
+__device__ __forceinline__ void vrows(const uint32_t *rl, int R, const int *vsl, const uint32_t *vco, int vlo,
+                                      int vhi, int wave, bool vact, uint64_t obase, int64_t opitch, uint32_t dlo,
+                                      uint32_t dhi)
+{
+    constexpr int NVP = (NV + 3) & ~3;
+    for (int y = vlo + wave; y < vhi; y += 8) {
+        const int y2 = min(y + 4, vhi - 1);
+        const int i0 = y - vlo, i1 = y2 - vlo;
+        const int a0 = vtaps<CP, NV>(rl, R, vsl[i0], vco + i0 * NVP, vinit<SRC>(y, dlo, dhi));
+        const int a1 = vtaps<CP, NV>(rl, R, vsl[i1], vco + i1 * NVP, vinit<SRC>(y2, dlo, dhi));
+        if (vact) {
+            vstore(obase + (int64_t)y * opitch, a0);
+            if (y + 4 < vhi) vstore(obase + (int64_t)y2 * opitch, a1);
+        }
+    }
+}
+
+template <int SRC, int CP>
+__device__ __forceinline__ void vpass_any(int nv, const uint32_t *rl, int R, const int *vsl, const uint32_t *vco,
+                                          int vlo, int vhi, int wave, bool vact, uint64_t obase, int64_t opitch,
+                                          uint32_t dlo, uint32_t dhi)
+{
+    switch (nv) {                                            // wave-uniform, once per V step
 #define DTS_V4(n) \
-    case n: return vtaps<CP, n>(rl, R, s0, cq, acc);
+    case n: vrows<SRC, CP, n>(rl, R, vsl, vco, vlo, vhi, wave, vact, obase, opitch, dlo, dhi); break;
         DTS_V4(1) DTS_V4(2) DTS_V4(3) DTS_V4(4) DTS_V4(5) DTS_V4(6) DTS_V4(7) DTS_V4(8)
         DTS_V4(9) DTS_V4(10) DTS_V4(11) DTS_V4(12) DTS_V4(13) DTS_V4(14) DTS_V4(15) DTS_V4(16)
 #undef DTS_V4
     default:
-        return acc;                                          // nv > 16 is rejected at graph creation
+        break;                                               // nv > 16 is rejected at graph creation
     }
 }
 
@@ -205,7 +281,15 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
     const uint64_t base1 = P.src.data[2] + fb + hg.lofs;
     const int nload = hg.nload;
     const int lofs = hg.lofs;
-    k_u32 *hcoef = GP(k_u32, K.hcoef) + hg.coef;
+    // LDS: [ring][H taps: 4 waves][V taps: 2 step buffers][V slots: 2 step buffers]
+    uint32_t *const hco = ring + kRing4Dw + wave * kH4CoefDw;
+    uint32_t *const vco_base = ring + kRing4Dw + 4 * kH4CoefDw;
+    int *const vsl_base = reinterpret_cast<int *>(vco_base + 2 * kV4CoefDw);
+    {   // this wave's output taps for the whole walk: global -> LDS once per item
+        const int ndw = __builtin_popcountll(hg.mask) * ((K.N + 3) & ~3);
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(K.hcoef + hg.coef);
+        for (int i = lane; i < ndw / 4; i += 64) reinterpret_cast<uint4 *>(hco)[i] = g4[i];
+    }
 
     // V-side constants of this lane
     const int vpl = KIND ? (lane >> 5) : 0;
@@ -239,28 +323,20 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
             dhi |= (uint32_t)c_dither_l4[r + 4][dx] << (8 * r);
         }
     }
-    k_i32 *vslot = GP(k_i32, K.vslot);
     k_i32 *vlim = GP(k_i32, K.vlim);
-    k_u32 *vcoef = GP(k_u32, K.vcoef);
-    const int nv = K.NV;
+    const int nv = K.NV, nvp = (nv + 3) & ~3;
 
+    auto vstage = [&](int b) {                                 // step b's V taps and slots -> LDS buffer b & 1
+        const int vlo = b > 0 ? vlim[b - 1] : 0, nr = vlim[b] - vlo;
+        uint4 *d4 = reinterpret_cast<uint4 *>(vco_base + (b & 1) * kV4CoefDw);
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(K.vcoef + (int64_t)vlo * nvp);
+        for (int i = t; i < nr * nvp / 4; i += kThreads) d4[i] = g4[i];
+        for (int i = t; i < nr; i += kThreads) vsl_base[(b & 1) * kV4SlotMax + i] = K.vslot[vlo + i];
+    };
     auto vpass = [&](int b) {                                  // the output rows step b completes
         const int vlo = b > 0 ? vlim[b - 1] : 0;
-        const int vhi = vlim[b];
-        for (int y = vlo + wave; y < vhi; y += 4) {
-            const int s0 = vslot[y];
-            int acc = 64 << 12;                                // flat dither (8-bit sources)
-            if (SRC == kSrcP010) {
-                const uint32_t dw = (y & 4) ? dhi : dlo;
-                acc = (int)((dw >> (8 * (y & 3))) & 255u) << 12;
-            }
-            acc = vtaps_any<CP>(rl, R, s0, nv, vcoef + (int64_t)y * nv, acc);
-            if (vact) {
-                int v = acc >> 19;
-                v = v < 0 ? 0 : (v > 255 ? 255 : v);
-                *GP(g_u8, obase + (int64_t)y * opitch) = (uint8_t)v;
-            }
-        }
+        vpass_any<SRC, CP>(nv, rl, R, vsl_base + (b & 1) * kV4SlotMax, vco_base + (b & 1) * kV4CoefDw, vlo,
+                           vlim[b], wave, vact, obase, opitch, dlo, dhi);
     };
 
     const int nsteps = K.nsteps;
@@ -275,7 +351,7 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
             for (int k = 0; k < 8; ++k) {
                 const int kk = planar2 ? (k & 3) : k;
                 u32x4 v = {0u, 0u, 0u, 0u}, w = {0u, 0u, 0u, 0u};
-                if (kk < nload && lofs + 16 * kk >= 0) {       // chunks left of the row hold zero taps
+                if (!(DTS_L4_ABLATE & 4) && kk < nload && lofs + 16 * kk >= 0) {   // chunks left of the row: zero taps
                     const uint64_t a = (planar2 && k >= 4 ? base1 : base0) + 16 * kk;
                     v = *GP(g_cu32x4, a + ro0);
                     w = *GP(g_cu32x4, a + ro1);
@@ -284,9 +360,10 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
                 rb[4 * k + 0] = w.x; rb[4 * k + 1] = w.y; rb[4 * k + 2] = w.z; rb[4 * k + 3] = w.w;
             }
         }
-        if (b > 0) vpass(b - 1);
+        if (b < nsteps) vstage(b);
+        if (!(DTS_L4_ABLATE & 2) && b > 0) vpass(b - 1);
         __syncthreads();
-        if (b < nsteps) {
+        if (!(DTS_L4_ABLATE & 1) && b < nsteps) {
             int s = slot0 + lane;
             if (s >= R) s -= R;
             uint32_t *wp = ring + s * CP + hg.col0;
@@ -297,7 +374,7 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
                 uint64_t mask = hg.mask;
                 int qend = hg.qend;
                 asm volatile("" : "+s"(mask), "+s"(qend));
-                hdispatch<CVT, CAP, SH>(K.N, ra, rb, pass ? kSelV : kSelU, mask, qend, hcoef,
+                hdispatch<CVT, CAP, SH>(K.N, ra, rb, pass ? kSelV : kSelU, mask, qend, hco,
                                         wp + pass * (R * CP));
                 if (planar2) {                                 // the V plane's window moves down
 #pragma unroll
@@ -319,8 +396,11 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
 // Persistent workgroups pull (frame, job) items from a device counter,
 // frame-major so the renditions of one frame run together (source re-reads
 // across renditions and strip halos hit L2 / the Infinity Cache).
+#ifndef DTS_L4_WAVES
+#define DTS_L4_WAVES 3          // waves per SIMD the register budget is cut for (<= 168 VGPRs)
+#endif
 template <int SRC>
-__global__ void __launch_bounds__(kThreads) k_ladder4(const Ladder4Params P)
+__global__ void __launch_bounds__(kThreads, DTS_L4_WAVES) k_ladder4(const Ladder4Params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
     volatile int *slot = reinterpret_cast<volatile int *>(ring);   // ring dword 0: idle between items
