@@ -284,13 +284,12 @@ bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &p
     const bool p010 = s.src_fmt == DTS_FMT_P010LE, nv12 = s.src_fmt == DTS_FMT_NV12;
     int64_t rowb[3], rows[3];
     plane_geom(s.src_w, s.src_h, s.src_fmt, rowb, rows);
-    // bytes per sample in the (maybe interleaved) source row, 16-B loads per row and plane the
-    // kernel holds, sample pairs its H code addresses (ladder4.hip item4: CAP)
+    // bytes per sample in the (maybe interleaved) source row and the sample pairs the kernel's
+    // eight 16-B loads per row hold (ladder4.hip item4: CAP)
     const int bps = kind ? (p010 ? 4 : (nv12 ? 2 : 1)) : (p010 ? 2 : 1);
-    const int nlmax = (kind && !p010 && !nv12) ? 4 : 8;
-    const int cap = kind ? (p010 ? 16 : 32) : (p010 ? 32 : 64);
-    return plan4_kind(kt.fh, kt.v, kt.srcH, kt.dstW, kt.dstH, bps, nlmax, cap, kind ? kRing4ColsC : kRing4ColsL,
-                      rowb[kind ? 1 : 0], kRing4Slots, pl);
+    const int cap = 64 / bps;
+    return plan4_kind(kt.fh, kt.v, kt.srcH, kt.dstW, kt.dstH, bps, 8, cap, kRing4Cols, rowb[kind ? 1 : 0],
+                      kRing4Slots, pl);
 }
 
 int make_plan(const dts_graph_spec &s, GraphPlan &gp)
@@ -351,20 +350,22 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     for (size_t i = 0; i < gp.kts.size(); ++i) {
         if (!((gp.v4_mask >> i) & 1)) continue;
         const Plan4 &pl = gp.p4[i];
-        for (int st = 0; st < pl.nstrips; ++st) {
-            Job4 j{};
-            j.rk = (int16_t)i;
-            j.kind = (int16_t)(i & 1);
-            j.rung = (int16_t)(i >> 1);
-            j.x0 = st * pl.C;
-            j.ncols = std::min(pl.C, gp.kts[i].dstW - j.x0);
-            j.group0 = st * 4;
-            gp.jobs4.push_back(j);
-        }
+        for (int st = 0; st < pl.nstrips; ++st)
+            for (int plane = 0; plane < ((i & 1) ? 2 : 1); ++plane) {   // chroma: U and V items side by side
+                Job4 j{};
+                j.rk = (int16_t)i;
+                j.kind = (int16_t)(i & 1);
+                j.rung = (int16_t)(i >> 1);
+                j.plane = (int16_t)plane;
+                j.x0 = st * pl.C;
+                j.ncols = std::min(pl.C, gp.kts[i].dstW - j.x0);
+                j.group0 = st * 4;
+                gp.jobs4.push_back(j);
+            }
     }
     // heaviest strips first (H tap pairs x columns x source rows): a short tail
     auto cost4 = [&](const Job4 &j) {
-        return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH * (j.kind ? 2 : 1);
+        return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH;
     };
     std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(), [&](const Job4 &a, const Job4 &b) { return cost4(a) > cost4(b); });
     if (gp.v4_mask) gp.lds4 = kLds4Bytes;

@@ -82,10 +82,9 @@ struct LadderParams {
 // ---------------------------------------------------------------------------
 // v4 ladder (ladder4.hip): row-pair H from VGPRs, LDS ring, per-column V
 // ---------------------------------------------------------------------------
-constexpr int kRing4ColsL = 64;     // luma output columns per strip (V: lane = column)
-constexpr int kRing4ColsC = 32;     // chroma output columns per strip and plane (lanes 0-31 U, 32-63 V)
+constexpr int kRing4Cols = 64;      // output columns per strip (V: lane = column)
 constexpr int kRing4Slots = 96;     // ring row pairs: one 64-pair step + up to 32 pairs of V reach
-constexpr int kRing4Dw = 2 * kRing4Slots * (kRing4ColsC + 1);   // ring dwords (chroma: 2 planes, >= luma)
+constexpr int kRing4Dw = kRing4Slots * (kRing4Cols + 1);        // ring dwords (odd column pitch)
 constexpr int kH4CoefDw = 256;      // LDS tap pairs per wave group (outputs x N rounded up to 4)
 constexpr int kV4CoefDw = 1152;     // LDS V tap pairs per step buffer (rows x NV rounded up to 4)
 constexpr int kV4SlotMax = 144;     // output rows per step buffer
@@ -100,11 +99,11 @@ struct HGroup4 {                    // one wave's share of a strip
     int32_t col0;                   // ring column of the group's first output
 };
 
-struct Job4 {                       // one strip of one (rendition, kind)
+struct Job4 {                       // one strip of one plane of one rendition
     int16_t rk;                     // rung * 2 + kind
-    int16_t kind;
+    int16_t kind;                   // 0 = luma, 1 = chroma
     int16_t rung;
-    int16_t pad_;
+    int16_t plane;                  // chroma: 0 = U, 1 = V
     int32_t x0, ncols, group0;      // first output column, columns, first HGroup4
 };
 

@@ -5,23 +5,25 @@
 // yuv2planeX_8_c / yuv2nv12cX_c under SWS_BITEXACT|SWS_ACCURATE_RND
 // (bit-exact; DESIGN.md "Oracle"), organised for CDNA4:
 //
-//  * one work item = (frame, rendition, plane kind, strip of C output
-//    columns), walked top to bottom in steps of 128 source rows;
+//  * one work item = (frame, rendition, plane Y/U/V, strip of up to 64
+//    output columns), walked top to bottom in steps of 128 source rows;
 //  * H: lane = source row pair.  Each wave owns a contiguous share of the
-//    strip's output columns (an HGroup4); its lanes load their two rows'
-//    window straight into VGPRs (global_load_dwordx4), widen u8 / p010
-//    samples to int16x2 sample pairs, and evaluate every output whose window
-//    starts at a pair position (positions unrolled at compile time; a
-//    wave-uniform bit mask says which hold an output).  The taps are
-//    wave-uniform, so they come from SGPRs (s_load) and one v_dot2_i32_i16
+//    strip's output columns (an HGroup4); its lanes hold their two rows'
+//    window in VGPRs (global_load_dwordx4), widen u8 / p010 samples to
+//    int16x2 sample pairs, and evaluate every output whose window starts at a
+//    pair position (positions unrolled at compile time; a wave-uniform bit
+//    mask says which hold an output).  Taps are wave-uniform: staged in LDS
+//    once per item and read with broadcast ds_read_b128; one v_dot2_i32_i16
 //    does 2 taps of one row; v_cvt_pk_i16_i32 applies the 15-bit clip and
-//    packs the row pair into the int16x2 dword the V pass consumes;
+//    packs the row pair into the int16x2 dword the V pass consumes.  As soon
+//    as the walk has converted the last sample pair of a 16-byte load, its
+//    registers are refilled with the next step's rows, so the next step's
+//    source streams in under the rest of this step's H and V work;
 //  * the row-pair dwords go to an LDS ring [slot][column] with an odd column
 //    pitch (conflict-free writes down a column, reads across a row);
-//  * V: lane = output column (chroma: lanes 0-31 U, 32-63 V), one output row
-//    per wave, v_dot2_i32_i16 over ring dwords with SGPR tap pairs, then
-//    dither/round, >> 19, clip and a byte store.
-//  The next step's source rows are in flight while V runs on the ring.
+//  * V: lane = output column, two output rows per wave and iteration,
+//    v_dot2_i32_i16 over ring dwords with the rows' tap pairs (staged in LDS
+//    one step ahead), then dither/round, >> 19, clip and a byte store.
 #include "dts_internal.h"
 
 #ifndef DTS_L4_ABLATE
@@ -65,11 +67,20 @@ __device__ __forceinline__ uint32_t shr(uint32_t d, uint32_t sh)
     return __builtin_bit_cast(uint32_t, v);
 }
 
+// Conversion kinds (what one row's 8 x 16-byte loads hold):
+//   P8  : planar u8, 8 sample pairs per load (the 8-bit planes are read as they are)
+//   NV  : nv12 interleaved chroma, 4 pairs per load, sel picks U or V (input.c nv12ToUV_c)
+//   P16 : p010 luma, LE16 >> 6, 4 pairs per load (input.c p010LEToY_c)
+//   P16C: p010 interleaved chroma (U16,V16 dwords) >> 6, 2 pairs per load, sel picks U or V
+//         (input.c p010LEToUV_c)
+template <int CVT>
+constexpr int pairs_per_load() { return CVT == kCvtP8 ? 8 : (CVT == kCvtP16C ? 2 : 4); }
+
+// sample pairs the 8 loads of one row hold (= api.cpp plan4_for cap)
+template <int CVT>
+constexpr int cap_pairs() { return 8 * pairs_per_load<CVT>(); }
+
 // Sample pair q (samples 2q, 2q+1 past the window base) of one row as int16x2.
-//   P8  : planar u8 (the 8-bit planes are read as they are)
-//   NV  : nv12 interleaved chroma, sel picks U or V (input.c nv12ToUV_c)
-//   P16 : p010 luma, LE16 >> 6 (input.c p010LEToY_c)
-//   P16C: p010 interleaved chroma (U16,V16 dwords) >> 6, sel picks U or V (p010LEToUV_c)
 // z is an opaque zero private to each hpass instantiation: without it the
 // identical conversions of every tap-count variant are merged and hoisted in
 // front of hdispatch's switch, where they all stay live at once.
@@ -89,16 +100,47 @@ constexpr int qmax4(int n, int cap)
                                        : ((cap - n + 1) < 64 ? cap - n + 1 : 64);
 }
 
+// One lane's source window (its two rows) for one step, read through a
+// buffer descriptor over the source plane: voffsets o0/o1 are the rows' byte
+// offsets plus the window offset, load k adds 16k (an immediate).  The range
+// check turns every read past the plane (and the wrapped negative offsets of
+// row 0 when the window starts left of it) into zeros; a window starting left
+// of a later row reads the previous row's tail instead.  Both only ever meet
+// zero taps, as do loads k >= nload, which keep whatever the slot held.
+struct Window {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t o0, o1;
+    int nload;
+};
+
+// z: an opaque zero (soffset), keeps the loads of different hpass
+// instantiations apart like pair_at's
+__device__ __forceinline__ void load_chunk(uint32_t (&ra)[32], uint32_t (&rb)[32], const Window &w, int k,
+                                           uint32_t z = 0)
+{
+    if (DTS_L4_ABLATE & 4) return;
+    if (k < w.nload) {                                       // wave-uniform
+        const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.o0 + 16 * k, z, 0));
+        const u32x4 x = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.o1 + 16 * k, z, 0));
+        ra[4 * k + 0] = v.x; ra[4 * k + 1] = v.y; ra[4 * k + 2] = v.z; ra[4 * k + 3] = v.w;
+        rb[4 * k + 0] = x.x; rb[4 * k + 1] = x.y; rb[4 * k + 2] = x.z; rb[4 * k + 3] = x.w;
+    }
+}
+
 // Horizontal FIR of one wave over its row pair for every output whose window
 // starts at a pair position q < qend with bit q of mask set.  Outputs are
 // visited in column order; their N int16x2 tap pairs (rows of NP = N rounded
 // up to 4 dwords) follow each other in LDS at cl and are read with wave-wide
-// broadcast ds_read_b128; their ring dwords follow each other at wp.
+// broadcast ds_read_b128; their ring dwords follow each other at wp.  Every
+// load slot of ra/rb is refilled from nw (the next step) once its last sample
+// pair has been converted; slots the walk never reaches are refilled at its end.
 template <int CVT, int N, int QMAX, int SH>
-__device__ __forceinline__ void hpass(const uint32_t (&ra)[32], const uint32_t (&rb)[32], uint32_t sel,
-                                      uint64_t mask, int qend, const uint32_t *cl, uint32_t *wp)
+__device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], uint32_t sel, uint64_t mask,
+                                      int qend, const uint32_t *cl, uint32_t *wp, const Window &nw)
 {
     constexpr int NP = (N + 3) & ~3;
+    constexpr int PPL = pairs_per_load<CVT>();
+    static_assert(QMAX + N - 1 <= 8 * PPL, "window exceeds the 8 loads");
     uint32_t z;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));
     uint32_t pa[QMAX + N + 7], pb[QMAX + N + 7];
@@ -106,18 +148,21 @@ __device__ __forceinline__ void hpass(const uint32_t (&ra)[32], const uint32_t (
     for (int q = 0; q < N - 1; ++q) {
         pa[q] = pair_at<CVT>(ra, q, sel, z);
         pb[q] = pair_at<CVT>(rb, q, sel, z);
+        if (q % PPL == PPL - 1) load_chunk(ra, rb, nw, q / PPL, z);
     }
     const uint4 *cv = reinterpret_cast<const uint4 *>(cl);
     // a constant trip count (no early exit) keeps the loop fully unrolled, so
-    // every pa/pb index is a compile-time register; qend is tested once per 8
-    // positions, the output mask once per position
+    // every pa/pb/ra/rb index is a compile-time register; qend is tested once
+    // per 8 positions, the output mask once per position
 #pragma unroll
     for (int q8 = 0; q8 < QMAX; q8 += 8) {
         if (q8 < qend) {
 #pragma unroll
             for (int q = q8; q < q8 + 8 && q < QMAX; ++q) {
-                pa[q + N - 1] = pair_at<CVT>(ra, q + N - 1, sel, z);
-                pb[q + N - 1] = pair_at<CVT>(rb, q + N - 1, sel, z);
+                const int pn = q + N - 1;                    // the pair this position converts
+                pa[pn] = pair_at<CVT>(ra, pn, sel, z);
+                pb[pn] = pair_at<CVT>(rb, pn, sel, z);
+                if (pn % PPL == PPL - 1) load_chunk(ra, rb, nw, pn / PPL, z);
                 if ((uint32_t)(mask >> q) & 1u) {
                     uint32_t c[NP];
 #pragma unroll
@@ -141,6 +186,11 @@ __device__ __forceinline__ void hpass(const uint32_t (&ra)[32], const uint32_t (
             }
         }
     }
+    // pairs [0, conv) were converted above; refill the slots holding any later pair
+    const int conv = min((qend + 7) & ~7, QMAX) + N - 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if ((k + 1) * PPL - 1 >= conv) load_chunk(ra, rb, nw, k, z);
 }
 
 // Wave-uniform struct read through the constant address space (s_load).
@@ -155,47 +205,34 @@ __device__ __forceinline__ T kload(const T *p)
     return __builtin_bit_cast(T, w);
 }
 
-template <int CVT, int CAP, int SH>
-__device__ __forceinline__ void hdispatch(int N, const uint32_t (&ra)[32], const uint32_t (&rb)[32], uint32_t sel,
-                                          uint64_t mask, int qend, const uint32_t *cp, uint32_t *wp)
-{
-    switch (N) {                                             // wave-uniform
-#define DTS_H4(n) \
-    case n: hpass<CVT, n, qmax4(n, CAP), SH>(ra, rb, sel, mask, qend, cp, wp); break;
-        DTS_H4(2) DTS_H4(3) DTS_H4(4) DTS_H4(5) DTS_H4(6) DTS_H4(7) DTS_H4(8) DTS_H4(9) DTS_H4(10)
-        DTS_H4(11) DTS_H4(12) DTS_H4(14) DTS_H4(16)
-#undef DTS_H4
-    default:
-        break;
-    }
-}
+constexpr int kCP = kRing4Cols + 1;   // ring column pitch (dwords)
 
-// Vertical FIR of one output row for one lane: NV ring dwords (row pairs)
-// from slot s0 on (wrapping at R), wave-uniform tap pairs in LDS at cq
-// (broadcast reads).
-template <int CP, int NV>
-__device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, const uint32_t *cq, int acc)
+// Vertical FIR of one output row for one lane: ng groups of 4 ring dwords
+// (row pairs) from slot s0 on (wrapping at R), with the row's tap pairs in LDS
+// at cq (broadcast ds_read_b128; rows are zero-padded to groups of 4, so the
+// ring dwords past the window only meet zero taps).  s0 is wave-uniform.
+__device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, int ng, const uint32_t *cq, int acc)
 {
-    constexpr int NVP = (NV + 3) & ~3;
-    uint32_t c[NVP];
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(cq);
+    if (s0 + 4 * ng <= R) {
+        const uint32_t *p = rl + s0 * kCP;
+        for (int g = 0; g < ng; ++g, p += 4 * kCP) {
+            const uint4 c = c4[g];
+            acc = dot2(p[0], c.x, acc);
+            acc = dot2(p[kCP], c.y, acc);
+            acc = dot2(p[2 * kCP], c.z, acc);
+            acc = dot2(p[3 * kCP], c.w, acc);
+        }
+    } else {                                                 // the window wraps round the ring
+        for (int g = 0; g < ng; ++g) {
+            const uint4 c = c4[g];
+            const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-    for (int i = 0; i < NVP / 4; ++i) {
-        const uint4 v = reinterpret_cast<const uint4 *>(cq)[i];
-        c[4 * i + 0] = v.x;
-        c[4 * i + 1] = v.y;
-        c[4 * i + 2] = v.z;
-        c[4 * i + 3] = v.w;
-    }
-    if (s0 + NV <= R) {
-        const uint32_t *b = rl + s0 * CP;
-#pragma unroll
-        for (int t = 0; t < NV; ++t) acc = dot2(b[t * CP], c[t], acc);
-    } else {
-#pragma unroll
-        for (int t = 0; t < NV; ++t) {
-            int s = s0 + t;
-            if (s >= R) s -= R;
-            acc = dot2(rl[s * CP], c[t], acc);
+            for (int i = 0; i < 4; ++i) {
+                int s = s0 + 4 * g + i;
+                if (s >= R) s -= R;
+                acc = dot2(rl[s * kCP], cc[i], acc);
+            }
         }
     }
     return acc;
@@ -219,189 +256,215 @@ __device__ __forceinline__ void vstore(uint64_t p, int acc)
     *GP(g_u8, p) = (uint8_t)v;
 }
 
-// The output rows [vlo, vhi) of one V step, rows vlo + wave + 4i for this
-// wave, two rows per iteration.  vsl / vco: the step's ring slots and tap
-// pairs staged in LDS (row y at index y - vlo).
-template <int SRC, int CP, int NV>
-__device__ __forceinline__ void vrows(const uint32_t *rl, int R, const int *vsl, const uint32_t *vco, int vlo,
-                                      int vhi, int wave, bool vact, uint64_t obase, int64_t opitch, uint32_t dlo,
-                                      uint32_t dhi)
+// Per-item state shared by the H and V halves of a walk.
+struct Item {
+    const uint32_t *hco;                 // this wave's H taps (LDS)
+    uint32_t *vco_base;                  // V taps, 2 step buffers (LDS)
+    int *vsl_base;                       // V ring slots, 2 step buffers (LDS)
+    const uint32_t *rl;                  // ring column of this lane (V)
+    __amdgpu_buffer_rsrc_t rsrc;         // source plane of the frame
+    int64_t pitch;
+    int64_t opitch;
+    uint64_t obase;                      // output sample of this lane in row 0
+    uint64_t mask;
+    const uint32_t *vcoef;
+    const int32_t *vslot;
+    const int32_t *vlim;
+    uint32_t sel, dlo, dhi;
+    int R, srcH, nsteps, nvp, lofs, nload, qend, col0, wave, lane, t;
+    bool vact;
+};
+
+// The output rows step b completes, rows vlo + wave + 4i for this wave, two
+// rows per iteration; the step's ring slots and tap pairs are staged in LDS
+// (row y at index y - vlo).
+template <int SRC>
+__device__ __forceinline__ void vpass(const Item &I, int b)
 {
-    constexpr int NVP = (NV + 3) & ~3;
-    for (int y = vlo + wave; y < vhi; y += 8) {
+    k_i32 *vlim = GP(k_i32, I.vlim);
+    const int vlo = b > 0 ? vlim[b - 1] : 0, vhi = vlim[b];
+    const int *vsl = I.vsl_base + (b & 1) * kV4SlotMax;
+    const uint32_t *vco = I.vco_base + (b & 1) * kV4CoefDw;
+    const int ng = I.nvp >> 2;
+    for (int y = vlo + I.wave; y < vhi; y += 8) {
         const int y2 = min(y + 4, vhi - 1);
         const int i0 = y - vlo, i1 = y2 - vlo;
-        const int a0 = vtaps<CP, NV>(rl, R, vsl[i0], vco + i0 * NVP, vinit<SRC>(y, dlo, dhi));
-        const int a1 = vtaps<CP, NV>(rl, R, vsl[i1], vco + i1 * NVP, vinit<SRC>(y2, dlo, dhi));
-        if (vact) {
-            vstore(obase + (int64_t)y * opitch, a0);
-            if (y + 4 < vhi) vstore(obase + (int64_t)y2 * opitch, a1);
+        const int a0 = vtaps(I.rl, I.R, uni(vsl[i0]), ng, vco + i0 * I.nvp, vinit<SRC>(y, I.dlo, I.dhi));
+        const int a1 = vtaps(I.rl, I.R, uni(vsl[i1]), ng, vco + i1 * I.nvp, vinit<SRC>(y2, I.dlo, I.dhi));
+        if (I.vact) {
+            vstore(I.obase + (int64_t)y * I.opitch, a0);
+            if (y + 4 < vhi) vstore(I.obase + (int64_t)y2 * I.opitch, a1);
         }
     }
 }
 
-template <int SRC, int CP>
-__device__ __forceinline__ void vpass_any(int nv, const uint32_t *rl, int R, const int *vsl, const uint32_t *vco,
-                                          int vlo, int vhi, int wave, bool vact, uint64_t obase, int64_t opitch,
-                                          uint32_t dlo, uint32_t dhi)
+// step b's V taps and slots -> LDS buffer b & 1
+__device__ __forceinline__ void vstage(const Item &I, int b)
 {
-    switch (nv) {                                            // wave-uniform, once per V step
-#define DTS_V4(n) \
-    case n: vrows<SRC, CP, n>(rl, R, vsl, vco, vlo, vhi, wave, vact, obase, opitch, dlo, dhi); break;
-        DTS_V4(1) DTS_V4(2) DTS_V4(3) DTS_V4(4) DTS_V4(5) DTS_V4(6) DTS_V4(7) DTS_V4(8)
-        DTS_V4(9) DTS_V4(10) DTS_V4(11) DTS_V4(12) DTS_V4(13) DTS_V4(14) DTS_V4(15) DTS_V4(16)
-#undef DTS_V4
-    default:
-        break;                                               // nv > 16 is rejected at graph creation
+    k_i32 *vlim = GP(k_i32, I.vlim);
+    const int vlo = b > 0 ? vlim[b - 1] : 0, nr = vlim[b] - vlo;
+    uint4 *d4 = reinterpret_cast<uint4 *>(I.vco_base + (b & 1) * kV4CoefDw);
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(I.vcoef + (int64_t)vlo * I.nvp);
+    for (int i = I.t; i < nr * I.nvp / 4; i += kThreads) d4[i] = g4[i];
+    for (int i = I.t; i < nr; i += kThreads) I.vsl_base[(b & 1) * kV4SlotMax + i] = I.vslot[vlo + i];
+}
+
+// this lane's two source rows of step b (rows past the plane re-read its last
+// row: their H results only meet zero V taps); step nsteps (loaded by the last
+// step) reads nothing
+__device__ __forceinline__ Window window(const Item &I, int b)
+{
+    Window w;
+    w.rs = I.rsrc;
+    const int r0 = min(128 * b + 2 * I.lane, I.srcH - 1), r1 = min(128 * b + 2 * I.lane + 1, I.srcH - 1);
+    const bool on = b < I.nsteps;
+    w.o0 = on ? (uint32_t)(r0 * I.pitch + I.lofs) : 0x80000000u;
+    w.o1 = on ? (uint32_t)(r1 * I.pitch + I.lofs) : 0x80000000u;
+    w.nload = I.nload;
+    return w;
+}
+
+// The walk of one item down its plane with N tap pairs per output.
+template <int SRC, int CVT, int N>
+__device__ __forceinline__ void walk(const Item &I, uint32_t *ring)
+{
+    constexpr int SH = SRC == kSrcP010 ? 9 : 7;                    // hScale16To15: sh = depth - 1
+    constexpr int QMAX = qmax4(N, cap_pairs<CVT>());
+    uint32_t ra[32], rb[32];
+    {
+        const Window w0 = window(I, 0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) load_chunk(ra, rb, w0, k);
+    }
+    int slot0 = 0;
+    for (int b = 0; b <= I.nsteps; ++b) {
+        if (b < I.nsteps) vstage(I, b);
+        if (!(DTS_L4_ABLATE & 2) && b > 0) vpass<SRC>(I, b - 1);
+        __syncthreads();
+        if (b < I.nsteps) {
+            const Window nw = window(I, b + 1);
+            int s = slot0 + I.lane;
+            if (s >= I.R) s -= I.R;
+            // opaque per step: keeps the compiler from hoisting the ~2 x QMAX
+            // position tests out of the walk as long-lived SGPR lane masks
+            uint64_t mask = I.mask;
+            int qend = I.qend;
+            asm volatile("" : "+s"(mask), "+s"(qend));
+            if (!(DTS_L4_ABLATE & 1)) {
+                hpass<CVT, N, QMAX, SH>(ra, rb, I.sel, mask, qend, I.hco, ring + s * kCP + I.col0, nw);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) load_chunk(ra, rb, nw, k);
+            }
+            slot0 += 64;
+            if (slot0 >= I.R) slot0 -= I.R;
+        }
+        __syncthreads();
     }
 }
 
-// One item: a strip of one plane kind of one rendition of one frame.
-template <int SRC, int KIND>
+// One item: a strip of one plane (Y, U or V) of one rendition of one frame.
+// CVT is the plane's source conversion; planar u8 sources share one
+// instantiation for all three planes.  The walk is instantiated per tap-pair
+// count, so each one's loop holds only its own unrolled H code.
+template <int SRC, int CVT>
 __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const Job4 &J, uint32_t *ring)
 {
-    constexpr int CVT = KIND == 0 ? (SRC == kSrcP010 ? kCvtP16 : kCvtP8)
-                                  : (SRC == kSrcPlanar8 ? kCvtP8 : (SRC == kSrcNV12 ? kCvtNV : kCvtP16C));
-    constexpr bool planar2 = KIND == 1 && SRC == kSrcPlanar8;     // U and V in separate planes
-    constexpr int CAP = planar2 ? 32 : (CVT == kCvtP8 ? 64 : (CVT == kCvtP16C ? 16 : 32));
-    constexpr int CP = KIND ? kRing4ColsC + 1 : kRing4ColsL + 1;
-    constexpr int SH = SRC == kSrcP010 ? 9 : 7;                    // hScale16To15: sh = depth - 1
-    constexpr uint32_t kSelU = CVT == kCvtNV ? 0x0c020c00u : 0x05040100u;
-    constexpr uint32_t kSelV = CVT == kCvtNV ? 0x0c030c01u : 0x07060302u;
-
-    const int t = threadIdx.x, lane = t & 63, wave = uni(t >> 6);
+    const int kind = J.kind;
+    const int cpl = kind ? J.plane : 0;                            // chroma: 0 = U, 1 = V
+    Item I;
+    I.sel = CVT == kCvtNV ? (cpl ? 0x0c030c01u : 0x0c020c00u) : (cpl ? 0x07060302u : 0x05040100u);
+    I.t = threadIdx.x;
+    I.lane = I.t & 63;
+    I.wave = uni(I.t >> 6);
     const RungKind4 K = kload(P.rk + J.rk);
-    const HGroup4 hg = kload(K.groups + J.group0 + wave);
-    const int R = P.ring;
-    const int srcH = KIND ? P.chrH : P.srcH;
-    const int pl0 = KIND ? 1 : 0;
-    const int64_t pitch = P.src.pitch[pl0];
-    const uint64_t fb = (uint64_t)frame * P.src.fstride;
-    const uint64_t base0 = P.src.data[pl0] + fb + hg.lofs;
-    const uint64_t base1 = P.src.data[2] + fb + hg.lofs;
-    const int nload = hg.nload;
-    const int lofs = hg.lofs;
+    const HGroup4 hg = kload(K.groups + J.group0 + I.wave);
+    I.R = P.ring;
+    I.srcH = kind ? P.chrH : P.srcH;
+    I.nsteps = K.nsteps;
+    I.nvp = (K.NV + 3) & ~3;
+    I.lofs = hg.lofs;
+    I.nload = hg.nload;
+    I.qend = hg.qend;
+    I.col0 = hg.col0;
+    I.mask = hg.mask;
+    I.vcoef = K.vcoef;
+    I.vslot = K.vslot;
+    I.vlim = K.vlim;
+    const int spl = kind ? (SRC == kSrcPlanar8 ? 1 + cpl : 1) : 0; // source plane
+    I.pitch = spl == 0 ? P.src.pitch[0] : (spl == 1 ? P.src.pitch[1] : P.src.pitch[2]);
+    {   // the source plane of this frame as a buffer (descriptor inputs made provably uniform)
+        const uint64_t pbase = (spl == 0 ? P.src.data[0] : (spl == 1 ? P.src.data[1] : P.src.data[2])) +
+                               (uint64_t)frame * P.src.fstride;
+        const uint32_t lo = (uint32_t)uni((int)(uint32_t)pbase), hi = (uint32_t)uni((int)(uint32_t)(pbase >> 32));
+        const int bytes = uni((int)(I.pitch * I.srcH));
+        I.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes,
+                                                   0x00020000);
+    }
     // LDS: [ring][H taps: 4 waves][V taps: 2 step buffers][V slots: 2 step buffers]
-    uint32_t *const hco = ring + kRing4Dw + wave * kH4CoefDw;
-    uint32_t *const vco_base = ring + kRing4Dw + 4 * kH4CoefDw;
-    int *const vsl_base = reinterpret_cast<int *>(vco_base + 2 * kV4CoefDw);
+    uint32_t *const hco = ring + kRing4Dw + I.wave * kH4CoefDw;
+    I.hco = hco;
+    I.vco_base = ring + kRing4Dw + 4 * kH4CoefDw;
+    I.vsl_base = reinterpret_cast<int *>(I.vco_base + 2 * kV4CoefDw);
     {   // this wave's output taps for the whole walk: global -> LDS once per item
         const int ndw = __builtin_popcountll(hg.mask) * ((K.N + 3) & ~3);
         const uint4 *g4 = reinterpret_cast<const uint4 *>(K.hcoef + hg.coef);
-        for (int i = lane; i < ndw / 4; i += 64) reinterpret_cast<uint4 *>(hco)[i] = g4[i];
+        for (int i = I.lane; i < ndw / 4; i += 64) reinterpret_cast<uint4 *>(hco)[i] = g4[i];
     }
 
     // V-side constants of this lane
-    const int vpl = KIND ? (lane >> 5) : 0;
-    const int col = KIND ? (lane & 31) : lane;
-    const bool vact = col < J.ncols;
-    const uint32_t *rl = ring + vpl * (R * CP) + col;
+    I.vact = I.lane < J.ncols;
+    I.rl = ring + I.lane;
     // indexed by the item's rung: read per item from the kernarg segment, not held in SGPRs
     const DevPlanes dst = P.dst[J.rung];
     const int dfmt = P.dst_fmt[J.rung];
     const uint64_t dfb = (uint64_t)frame * dst.fstride;
-    uint64_t obase;
-    int64_t opitch;
-    if (KIND == 0) {
-        obase = dst.data[0] + dfb + J.x0 + col;
-        opitch = dst.pitch[0];
+    if (kind == 0) {
+        I.obase = dst.data[0] + dfb + J.x0 + I.lane;
+        I.opitch = dst.pitch[0];
     } else if (dfmt == DTS_FMT_NV12) {
-        obase = dst.data[1] + dfb + 2 * (J.x0 + col) + vpl;
-        opitch = dst.pitch[1];
+        I.obase = dst.data[1] + dfb + 2 * (J.x0 + I.lane) + cpl;
+        I.opitch = dst.pitch[1];
     } else {
-        obase = (vpl ? dst.data[2] : dst.data[1]) + dfb + J.x0 + col;
-        opitch = dst.pitch[1];
+        I.obase = (cpl ? dst.data[2] : dst.data[1]) + dfb + J.x0 + I.lane;
+        I.opitch = cpl ? dst.pitch[2] : dst.pitch[1];
     }
     // yuv2planeX_8 / yuv2nv12cX dither for >8-bit sources: ff_dither_8x8_128[y & 7][(x + off) & 7],
     // off = 0 for Y and U, 3 for V; x0 is a multiple of 8
-    uint32_t dlo = 0, dhi = 0;
+    I.dlo = 0;
+    I.dhi = 0;
     if (SRC == kSrcP010) {
-        const int dx = (col + (vpl ? 3 : 0)) & 7;
+        const int dx = (I.lane + (cpl ? 3 : 0)) & 7;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            dlo |= (uint32_t)c_dither_l4[r][dx] << (8 * r);
-            dhi |= (uint32_t)c_dither_l4[r + 4][dx] << (8 * r);
+            I.dlo |= (uint32_t)c_dither_l4[r][dx] << (8 * r);
+            I.dhi |= (uint32_t)c_dither_l4[r + 4][dx] << (8 * r);
         }
     }
-    k_i32 *vlim = GP(k_i32, K.vlim);
-    const int nv = K.NV, nvp = (nv + 3) & ~3;
-
-    auto vstage = [&](int b) {                                 // step b's V taps and slots -> LDS buffer b & 1
-        const int vlo = b > 0 ? vlim[b - 1] : 0, nr = vlim[b] - vlo;
-        uint4 *d4 = reinterpret_cast<uint4 *>(vco_base + (b & 1) * kV4CoefDw);
-        const uint4 *g4 = reinterpret_cast<const uint4 *>(K.vcoef + (int64_t)vlo * nvp);
-        for (int i = t; i < nr * nvp / 4; i += kThreads) d4[i] = g4[i];
-        for (int i = t; i < nr; i += kThreads) vsl_base[(b & 1) * kV4SlotMax + i] = K.vslot[vlo + i];
-    };
-    auto vpass = [&](int b) {                                  // the output rows step b completes
-        const int vlo = b > 0 ? vlim[b - 1] : 0;
-        vpass_any<SRC, CP>(nv, rl, R, vsl_base + (b & 1) * kV4SlotMax, vco_base + (b & 1) * kV4CoefDw, vlo,
-                           vlim[b], wave, vact, obase, opitch, dlo, dhi);
-    };
-
-    const int nsteps = K.nsteps;
-    int slot0 = 0;
-    for (int b = 0; b <= nsteps; ++b) {
-        uint32_t ra[32], rb[32];
-        if (b < nsteps) {                                      // this step's source rows -> VGPRs
-            // rows past the plane re-read its last row: their H results only meet zero V taps
-            const int r0 = min(128 * b + 2 * lane, srcH - 1), r1 = min(128 * b + 2 * lane + 1, srcH - 1);
-            const int64_t ro0 = (int64_t)r0 * pitch, ro1 = (int64_t)r1 * pitch;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int kk = planar2 ? (k & 3) : k;
-                u32x4 v = {0u, 0u, 0u, 0u}, w = {0u, 0u, 0u, 0u};
-                if (!(DTS_L4_ABLATE & 4) && kk < nload && lofs + 16 * kk >= 0) {   // chunks left of the row: zero taps
-                    const uint64_t a = (planar2 && k >= 4 ? base1 : base0) + 16 * kk;
-                    v = *GP(g_cu32x4, a + ro0);
-                    w = *GP(g_cu32x4, a + ro1);
-                }
-                ra[4 * k + 0] = v.x; ra[4 * k + 1] = v.y; ra[4 * k + 2] = v.z; ra[4 * k + 3] = v.w;
-                rb[4 * k + 0] = w.x; rb[4 * k + 1] = w.y; rb[4 * k + 2] = w.z; rb[4 * k + 3] = w.w;
-            }
-        }
-        if (b < nsteps) vstage(b);
-        if (!(DTS_L4_ABLATE & 2) && b > 0) vpass(b - 1);
-        __syncthreads();
-        if (!(DTS_L4_ABLATE & 1) && b < nsteps) {
-            int s = slot0 + lane;
-            if (s >= R) s -= R;
-            uint32_t *wp = ring + s * CP + hg.col0;
-#pragma unroll 1
-            for (int pass = 0; pass < (KIND ? 2 : 1); ++pass) {
-                // opaque per pass: keeps the compiler from hoisting the ~2 x QMAX
-                // position tests out of the walk as long-lived SGPR lane masks
-                uint64_t mask = hg.mask;
-                int qend = hg.qend;
-                asm volatile("" : "+s"(mask), "+s"(qend));
-                hdispatch<CVT, CAP, SH>(K.N, ra, rb, pass ? kSelV : kSelU, mask, qend, hco,
-                                        wp + pass * (R * CP));
-                if (planar2) {                                 // the V plane's window moves down
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        ra[i] = ra[i + 16];
-                        rb[i] = rb[i + 16];
-                    }
-                }
-            }
-            slot0 += 64;
-            if (slot0 >= R) slot0 -= R;
-        }
-        __syncthreads();
+    switch (K.N) {                                                 // wave-uniform, once per item
+#define DTS_W4(n) \
+    case n: walk<SRC, CVT, n>(I, ring); break;
+        DTS_W4(2) DTS_W4(3) DTS_W4(4) DTS_W4(5) DTS_W4(6) DTS_W4(7) DTS_W4(8) DTS_W4(9) DTS_W4(10)
+        DTS_W4(11) DTS_W4(12) DTS_W4(14) DTS_W4(16)
+#undef DTS_W4
+    default:
+        break;                                                     // other counts are never planned
     }
 }
 
 } // namespace
 
-// Persistent workgroups pull (frame, job) items from a device counter,
-// frame-major so the renditions of one frame run together (source re-reads
-// across renditions and strip halos hit L2 / the Infinity Cache).
 #ifndef DTS_L4_WAVES
 #define DTS_L4_WAVES 3          // waves per SIMD the register budget is cut for (<= 168 VGPRs)
 #endif
+// Persistent workgroups pull (frame, job) items from a device counter,
+// frame-major so the renditions of one frame run together (source re-reads
+// across renditions and strip halos hit L2 / the Infinity Cache).
 template <int SRC>
 __global__ void __launch_bounds__(kThreads, DTS_L4_WAVES) k_ladder4(const Ladder4Params P)
 {
+    constexpr int kLumaCvt = SRC == kSrcP010 ? kCvtP16 : kCvtP8;
+    constexpr int kChromaCvt = SRC == kSrcPlanar8 ? kCvtP8 : (SRC == kSrcNV12 ? kCvtNV : kCvtP16C);
     extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
     volatile int *slot = reinterpret_cast<volatile int *>(ring);   // ring dword 0: idle between items
     for (;;) {
@@ -412,10 +475,10 @@ __global__ void __launch_bounds__(kThreads, DTS_L4_WAVES) k_ladder4(const Ladder
         if (item >= P.nitems) return;
         const int frame = item / P.njobs, jid = item - frame * P.njobs;
         const Job4 J = kload(P.jobs + jid);
-        if (J.kind == 0)
-            item4<SRC, 0>(P, frame, J, ring);
+        if (kLumaCvt == kChromaCvt || J.kind == 0)
+            item4<SRC, kLumaCvt>(P, frame, J, ring);
         else
-            item4<SRC, 1>(P, frame, J, ring);
+            item4<SRC, kChromaCvt>(P, frame, J, ring);
     }
 }
 
