@@ -121,16 +121,17 @@ def verify_first_frame(src_index, outs):
 
 
 def load_traffic():
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_ladder.json")
+    """(HBM bytes per frame, profile tag) from the newest committed rocprofv3 PMC
+    summary (tools/prof_summary.py writes profiles/pmc_latest.json), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
             j = json.load(f)
-        return j.get("hbm_bytes_per_frame")
+        return j.get("hbm_bytes_per_frame"), j.get("tag")
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -230,7 +231,10 @@ def main():
         fps = frames_total / wall_max
         algo = info.algo_bytes_per_frame
         achieved = algo * B / (kern_ms * 1e-3)
-        traffic = load_traffic()
+        traffic_pf, traffic_tag = load_traffic()
+        # PMC bytes (FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits included) per launch over this run's
+        # kernel time, in the unit of `achieved`
+        traffic = round(traffic_pf * B / (kern_ms * 1e-3) / 1e9, 1) if traffic_pf else None
         line = {
             "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
@@ -246,7 +250,8 @@ def main():
             "algo_bytes_per_frame": algo,
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": traffic, "kernel_ms_per_launch": round(kern_ms, 4),
+                         "traffic": traffic, "traffic_bytes_per_frame": traffic_pf,
+                         "traffic_profile": traffic_tag, "kernel_ms_per_launch": round(kern_ms, 4),
                          "frames_per_launch": B},
         }
         if world == 1 and not args.no_cpu:

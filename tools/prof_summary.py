@@ -56,4 +56,5 @@ for s in stats:
         out["avg_kernel_ns"] = float(s["AverageNs"])
         out["calls"] = int(s["Calls"])
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(dst, "pmc_latest.json"), "w"), indent=1)   # read by bench.py
 print(json.dumps(out, indent=1))
