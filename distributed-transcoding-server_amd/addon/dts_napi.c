@@ -13,6 +13,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 
 #include "dts.h"
@@ -149,6 +150,23 @@ static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
     if (get_i32(env, o, "quality", 0, &s->quality) || get_i32(env, o, "qualityOut", 0, &s->quality_out) ||
         get_i32(env, o, "maxBatch", 0, &s->max_batch))
         return -1;
+    /* tonemap: {mode, param, desat, peak, npl} -> HDR10 -> SDR (vf_tonemap / zscale) */
+    bool has_tm = false;
+    napi_has_named_property(env, o, "tonemap", &has_tm);
+    if (has_tm) {
+        napi_value tm;
+        napi_valuetype t;
+        if (napi_get_named_property(env, o, "tonemap", &tm) != napi_ok) return -1;
+        napi_typeof(env, tm, &t);
+        if (t == napi_object) {
+            s->hdr_to_sdr = 1;
+            if (get_i32(env, tm, "mode", DTS_TM_HABLE, &s->tonemap.mode) ||
+                get_f64(env, tm, "param", NAN, &s->tonemap.param) ||
+                get_f64(env, tm, "desat", 0.0, &s->tonemap.desat) ||
+                get_f64(env, tm, "peak", 0.0, &s->tonemap.peak) || get_f64(env, tm, "npl", 100.0, &s->tonemap.npl))
+                return -1;
+        }
+    }
     return 0;
 }
 

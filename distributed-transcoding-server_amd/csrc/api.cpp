@@ -47,7 +47,8 @@ constexpr int kSwsBitexact = 0x80000;
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
 bool fmt_in_ok(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12 || f == DTS_FMT_P010LE; }
-bool fmt_out_ok(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12; }
+bool fmt_out_ok(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12 || f == DTS_FMT_P010LE; }
+bool fmt_8bit(int f) { return f == DTS_FMT_YUV420P || f == DTS_FMT_NV12; }   // quality / SDR outputs
 bool method_ok(int m)
 {
     switch (m) {
@@ -153,12 +154,100 @@ struct dts_graph {
     const dts_frame *p_dst = nullptr;
     dts_qstat *p_q = nullptr;
     int p_chunk_first[2] = {-1, -1}, p_chunk_n[2] = {0, 0};
+    // HDR10 -> SDR: per output a p010 intermediate of `batch` frames, double-buffered
+    // (an event per buffer orders reuse across streams)
+    bool hdr = false;
+    DevLayout lay_mid[DTS_MAX_OUTPUTS];
+    uint8_t *hdr_mid[2][DTS_MAX_OUTPUTS] = {};
+    hipEvent_t hdr_ev[2] = {nullptr, nullptr};
+    unsigned hdr_next = 0;
+    TonemapParams tm{};
 };
 
 // ---------------------------------------------------------------------------
 // graph construction
 // ---------------------------------------------------------------------------
 namespace {
+
+// RGB -> XYZ of a set of xy primaries with D65 white (columns scaled so white has Y = 1)
+void rgb_to_xyz(const double xy[3][2], double m[3][3])
+{
+    double P[3][3], Pi[3][3];
+    for (int i = 0; i < 3; ++i) {
+        P[0][i] = xy[i][0] / xy[i][1];
+        P[1][i] = 1.0;
+        P[2][i] = (1.0 - xy[i][0] - xy[i][1]) / xy[i][1];
+    }
+    auto inv = [](const double a[3][3], double o[3][3]) {
+        const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) -
+                           a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+                           a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {   // cofactor transpose
+                const int r0 = (j + 1) % 3, r1 = (j + 2) % 3, c0 = (i + 1) % 3, c1 = (i + 2) % 3;
+                o[i][j] = (a[r0][c0] * a[r1][c1] - a[r0][c1] * a[r1][c0]) / det;
+            }
+    };
+    inv(P, Pi);
+    const double W[3] = {0.3127 / 0.3290, 1.0, (1.0 - 0.3127 - 0.3290) / 0.3290};
+    double S[3];
+    for (int i = 0; i < 3; ++i) S[i] = Pi[i][0] * W[0] + Pi[i][1] * W[1] + Pi[i][2] * W[2];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) m[i][j] = P[i][j] * S[j];
+}
+
+// zscale=p=bt709 on bt2020 linear light: XYZ->709 x 2020->XYZ
+void bt2020_to_bt709(float out[9])
+{
+    static const double p2020[3][2] = {{0.708, 0.292}, {0.170, 0.797}, {0.131, 0.046}};
+    static const double p709[3][2] = {{0.640, 0.330}, {0.300, 0.600}, {0.150, 0.060}};
+    double a[3][3], b[3][3];
+    rgb_to_xyz(p2020, a);
+    rgb_to_xyz(p709, b);
+    const double det = b[0][0] * (b[1][1] * b[2][2] - b[1][2] * b[2][1]) -
+                       b[0][1] * (b[1][0] * b[2][2] - b[1][2] * b[2][0]) +
+                       b[0][2] * (b[1][0] * b[2][1] - b[1][1] * b[2][0]);
+    double bi[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const int r0 = (j + 1) % 3, r1 = (j + 2) % 3, c0 = (i + 1) % 3, c1 = (i + 2) % 3;
+            bi[i][j] = (b[r0][c0] * b[r1][c1] - b[r0][c1] * b[r1][c0]) / det;
+        }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double v = 0;
+            for (int k = 0; k < 3; ++k) v += bi[i][k] * a[k][j];
+            out[3 * i + j] = (float)v;
+        }
+}
+
+// vf_tonemap.c init() param defaults, peak fallback (ff_determine_signal_peak for
+// linear input without side data: 10) and zscale npl
+TonemapParams tonemap_params(const dts_tonemap_spec &t)
+{
+    TonemapParams p{};
+    p.mode = t.mode;
+    double param = t.param;
+    switch (t.mode) {
+    case DTS_TM_GAMMA: if (std::isnan(param)) param = 1.8; break;
+    case DTS_TM_REINHARD: if (!std::isnan(param)) param = (1.0 - param) / param; break;
+    case DTS_TM_MOBIUS: if (std::isnan(param)) param = 0.3; break;
+    default: break;
+    }
+    if (std::isnan(param)) param = 1.0;
+    const double peak = t.peak > 0 ? t.peak : 10.0, npl = t.npl > 0 ? t.npl : 100.0;
+    auto hable = [](double x) {
+        const double a = 0.15, b = 0.50, c = 0.10, d = 0.20, e = 0.02, f = 0.30;
+        return (x * (x * a + b * c) + d * e) / (x * (x * a + b) + d * f) - e / f;
+    };
+    p.param = (float)param;
+    p.desat = (float)t.desat;
+    p.peak = (float)peak;
+    p.hpeak = (float)hable((float)peak);
+    p.scale = (float)(10000.0 / npl);
+    bt2020_to_bt709(p.m);
+    return p;
+}
 
 struct KindTables {
     SwsFilter fh;                         // the libswscale H filter (v4 plans from it)
@@ -269,6 +358,13 @@ int validate_spec(const dts_graph_spec &s)
     }
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
+    if (s.quality && !fmt_8bit(s.out[s.quality_out].fmt)) return DTS_E_UNSUPPORTED;   // vf_psnr/vf_ssim: 8-bit
+    if (s.hdr_to_sdr) {
+        if (s.src_fmt != DTS_FMT_P010LE) return DTS_E_INVAL;                        // HDR10 sources are p010
+        if (s.tonemap.mode < DTS_TM_NONE || s.tonemap.mode > DTS_TM_MOBIUS) return DTS_E_INVAL;
+        for (int k = 0; k < s.nout; ++k)
+            if (!fmt_8bit(s.out[k].fmt) || (s.out[k].w & 1) || (s.out[k].h & 1)) return DTS_E_UNSUPPORTED;
+    }
     return DTS_OK;
 }
 
@@ -389,7 +485,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.1 (gfx950; abi 1)"; }
+const char *dts_version(void) { return "dts-mi355x 0.2 (gfx950; abi 2)"; }
 
 const char *dts_strerror(int err)
 {
@@ -574,7 +670,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         g = new dts_graph();
         g->ctx = ctx;
         g->spec = s;
-        g->batch = s.max_batch > 0 ? s.max_batch : 32;
+        g->batch = s.max_batch > 0 ? std::min(s.max_batch, 65535) : 32;
         g->src_kind = gp.src_kind;
         g->ndmax = gp.ndmax;
         g->ring_pairs = gp.ring_pairs;
@@ -596,6 +692,23 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         }
         g->lay_src.init(s.src_w, s.src_h, s.src_fmt);
         for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt);
+        if (s.hdr_to_sdr) {
+            g->hdr = true;
+            g->tm = tonemap_params(s.tonemap);
+            for (int sl = 0; sl < 2 && !e; ++sl) {
+                for (int k = 0; k < s.nout && !e; ++k) {
+                    g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
+                    if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->batch * g->lay_mid[k].fstride) != hipSuccess)
+                        e = DTS_E_NOMEM;
+                }
+                if (!e && hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
+            }
+            if (e) {
+                ctx->last_hip = (int)hipGetLastError();
+                dts_graph_destroy(g);
+                return e;
+            }
+        }
         if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt);
         *out = g;
         return DTS_OK;
@@ -641,6 +754,14 @@ void dts_graph_destroy(dts_graph *g)
         if (g->pin_out[sl]) hipHostFree(g->pin_out[sl]);
         if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
         if (g->done[sl]) hipEventDestroy(g->done[sl]);
+    }
+    for (int sl = 0; sl < 2; ++sl) {
+        if (g->hdr_ev[sl]) {
+            hipEventSynchronize(g->hdr_ev[sl]);
+            hipEventDestroy(g->hdr_ev[sl]);
+        }
+        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
+            if (g->hdr_mid[sl][k]) hipFree(g->hdr_mid[sl][k]);
     }
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
@@ -730,29 +851,19 @@ static int quality_enqueue(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
     return DTS_OK;
 }
 
-int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
-                         const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
+// The ladder launches (v4 kinds, then v3 kinds) for nframes frames of src into dst[k]
+// (format dst_fmt[k]); persistent grids over nframes x njobs items, items per launch < 2^30.
+static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, const int *dst_fmt, int nframes,
+                          hipStream_t st)
 {
-    if (!g || !src || !dst || nframes < 0) return DTS_E_INVAL;
-    if (nframes == 0) return DTS_OK;
     const dts_graph_spec &s = g->spec;
-    if (!planes_ok(*src, s.src_w, s.src_h, s.src_fmt, 16)) return DTS_E_INVAL;
-    for (int k = 0; k < s.nout; ++k)
-        if (!planes_ok(dst[k], s.out[k].w, s.out[k].h, s.out[k].fmt, 4)) return DTS_E_INVAL;
-    if (s.src_fmt == DTS_FMT_YUV420P && src->pitch[1] != src->pitch[2]) return DTS_E_INVAL;
-    const bool want_q = s.quality && qref && qraw_dev;
-    if (want_q && !planes_ok(*qref, s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, 4))
-        return DTS_E_INVAL;
     dts_ctx *ctx = g->ctx;
-    hipSetDevice(ctx->device);
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
-
     LadderParams p{};
-    p.src = to_dev(*src, s.src_fmt);
+    p.src = src;
     for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) {
         const int kk = k < s.nout ? k : 0;
-        p.dst[k] = to_dev(dst[kk], s.out[kk].fmt);
-        p.dst_fmt[k] = s.out[kk].fmt;
+        p.dst[k] = dst[kk];
+        p.dst_fmt[k] = dst_fmt[kk];
     }
     p.srcW = s.src_w;
     p.srcH = s.src_h;
@@ -765,7 +876,6 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    // persistent grids over nframes x njobs items (v4 kinds, then v3 kinds); items per launch < 2^30
     const int njobs_max = std::max(1, std::max(p.njobs, g->njobs4));
     const int max_frames = std::max(1, (1 << 30) / njobs_max);
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
@@ -773,9 +883,7 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
         LadderParams pp = p;
         pp.nframes = n;
         pp.nitems = n * p.njobs;
-        pp.src.data[0] += (uint64_t)(f0 * src->frame_stride);
-        pp.src.data[1] += (uint64_t)(f0 * src->frame_stride);
-        pp.src.data[2] += (uint64_t)(f0 * src->frame_stride);
+        for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
         if (g->njobs4) {
@@ -804,6 +912,70 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
             HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, std::min(pp.nitems, g->grid_cap), st));
         }
     }
+    return DTS_OK;
+}
+
+// HDR10 -> SDR: per chunk of `batch` frames, the bit-exact ladder into the p010
+// intermediates, then k_tonemap from each intermediate into the caller's output.
+static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, int nframes, hipStream_t st)
+{
+    const dts_graph_spec &s = g->spec;
+    dts_ctx *ctx = g->ctx;
+    for (int f0 = 0; f0 < nframes; f0 += g->batch) {
+        const int n = std::min(g->batch, nframes - f0);
+        const int sl = (int)(g->hdr_next++ & 1u);
+        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_ev[sl], 0));   // the buffer's previous user is done
+        DevPlanes sc = src, mid[DTS_MAX_OUTPUTS];
+        int mid_fmt[DTS_MAX_OUTPUTS];
+        for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)(f0 * src.fstride);
+        for (int k = 0; k < s.nout; ++k) {
+            mid[k] = g->lay_mid[k].planes(g->hdr_mid[sl][k]);
+            mid_fmt[k] = DTS_FMT_P010LE;
+        }
+        int e = enqueue_ladder(g, sc, mid, mid_fmt, n, st);
+        if (e) return e;
+        for (int k = 0; k < s.nout; ++k) {
+            TonemapParams tp = g->tm;
+            tp.src = mid[k];
+            tp.dst = dst[k];
+            for (int pl = 0; pl < 3; ++pl) tp.dst.data[pl] += (uint64_t)(f0 * dst[k].fstride);
+            tp.dst_fmt = s.out[k].fmt;
+            tp.w = s.out[k].w;
+            tp.h = s.out[k].h;
+            tp.nframes = n;
+            HIPCHK(ctx, launch_tonemap(tp, st));
+        }
+        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], st));
+    }
+    return DTS_OK;
+}
+
+int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
+                         const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
+{
+    if (!g || !src || !dst || nframes < 0) return DTS_E_INVAL;
+    if (nframes == 0) return DTS_OK;
+    const dts_graph_spec &s = g->spec;
+    if (!planes_ok(*src, s.src_w, s.src_h, s.src_fmt, 16)) return DTS_E_INVAL;
+    for (int k = 0; k < s.nout; ++k)
+        if (!planes_ok(dst[k], s.out[k].w, s.out[k].h, s.out[k].fmt, 4)) return DTS_E_INVAL;
+    if (s.src_fmt == DTS_FMT_YUV420P && src->pitch[1] != src->pitch[2]) return DTS_E_INVAL;
+    const bool want_q = s.quality && qref && qraw_dev;
+    if (want_q && !planes_ok(*qref, s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, 4))
+        return DTS_E_INVAL;
+    dts_ctx *ctx = g->ctx;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+
+    const DevPlanes dsrc = to_dev(*src, s.src_fmt);
+    DevPlanes ddst[DTS_MAX_OUTPUTS];
+    int dfmt[DTS_MAX_OUTPUTS];
+    for (int k = 0; k < s.nout; ++k) {
+        ddst[k] = to_dev(dst[k], s.out[k].fmt);
+        dfmt[k] = s.out[k].fmt;
+    }
+    const int e = g->hdr ? enqueue_hdr(g, dsrc, ddst, nframes, st) : enqueue_ladder(g, dsrc, ddst, dfmt, nframes, st);
+    if (e) return e;
     if (want_q) {
         const dts_output_spec &o = s.out[s.quality_out];
         return quality_enqueue(ctx, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
@@ -815,7 +987,7 @@ int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
                            int nframes, dts_qraw *qraw_dev, void *stream)
 {
     if (!ctx || !a || !b || !qraw_dev || nframes < 0 || w < 1 || h < 1) return DTS_E_INVAL;
-    if (!fmt_out_ok(fmt)) return DTS_E_UNSUPPORTED;
+    if (!fmt_8bit(fmt)) return DTS_E_UNSUPPORTED;
     if (!planes_ok(*a, w, h, fmt, 4) || !planes_ok(*b, w, h, fmt, 4)) return DTS_E_INVAL;
     if (nframes == 0) return DTS_OK;
     hipSetDevice(ctx->device);

@@ -151,6 +151,19 @@ struct QualityParams {
 };
 
 // ---------------------------------------------------------------------------
+// HDR10 -> SDR (hdr.hip)
+// ---------------------------------------------------------------------------
+struct TonemapParams {
+    DevPlanes src;                  // p010 at the output size (ladder intermediate)
+    DevPlanes dst;                  // 8-bit yuv420p / nv12
+    int32_t dst_fmt, w, h, nframes; // w, h even; nframes <= 65535
+    int32_t mode;                   // DTS_TM_*
+    float param, desat, peak, hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
+    float m[9];                     // bt2020 -> bt709 linear primaries, row-major
+};
+hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Synthetic source (testsrc2-like), identical on host and device
 // ---------------------------------------------------------------------------
 __host__ __device__ inline uint32_t synth_hash(uint32_t x)

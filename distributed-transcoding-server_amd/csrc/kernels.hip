@@ -60,6 +60,13 @@ __device__ __forceinline__ uint32_t clip8(int v)
     return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
+// output.c p010 output_pixel: av_clip_uintp2(val >> 17, 10) << 6
+__device__ __forceinline__ uint16_t clip10s(int v)
+{
+    v >>= 17;
+    return (uint16_t)((v < 0 ? 0 : (v > 1023 ? 1023 : v)) << 6);
+}
+
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -358,6 +365,7 @@ __device__ __forceinline__ void ladder_item(const LadderParams &P, int frame, in
     if (rung == 3) { dst = P.dst[3]; dfmt = P.dst_fmt[3]; }
     const int64_t dbase = (int64_t)frame * dst.fstride;
     const bool hidepth = SRC == kSrcP010;
+    const bool d16 = dfmt == DTS_FMT_P010LE;
     const int nv = K.nv;
     const int nvl = lane < nv ? lane : nv - 1;
 
@@ -369,8 +377,15 @@ __device__ __forceinline__ void ladder_item(const LadderParams &P, int frame, in
         if (kind == 0) {
             const int c0 = 4 * lane;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] = (hidepth ? c_dither[y & 7][(c0 + i) & 7] : 64) << 12;
+            for (int i = 0; i < 4; ++i) acc[i] = d16 ? 1 << 16 : (hidepth ? c_dither[y & 7][(c0 + i) & 7] : 64) << 12;
             vtaps_any<0>(ring, RP, q0, lane, nv, cq, acc);
+            if (d16) {      // output.c yuv2p010lX_c
+                const uint64_t row = dst.data[0] + dbase + (int64_t)y * dst.pitch[0] + 2 * J.x0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (c0 + i < J.ncols) *GPTR(g_u16, row + 2 * (c0 + i)) = clip10s(acc[i]);
+                return;
+            }
             const uint32_t o = clip8(acc[0]) | (clip8(acc[1]) << 8) | (clip8(acc[2]) << 16) | (clip8(acc[3]) << 24);
             const uint64_t row = dst.data[0] + dbase + (int64_t)y * dst.pitch[0] + J.x0;
             if (c0 + 3 < J.ncols) {
@@ -390,7 +405,20 @@ __device__ __forceinline__ void ladder_item(const LadderParams &P, int frame, in
             } else {
                 acc[0] = acc[1] = acc[2] = acc[3] = 64 << 12;
             }
+            if (d16) acc[0] = acc[1] = acc[2] = acc[3] = 1 << 16;
             vtaps_any<1>(ring, RP, q0, lane, nv, cq, acc);
+            if (d16) {      // output.c yuv2p010cX_c: U16,V16 pairs
+                const uint64_t row = dst.data[1] + dbase + (int64_t)y * dst.pitch[1] + 4 * J.x0;
+                if (c0 < J.ncols) {
+                    *GPTR(g_u16, row + 4 * c0) = clip10s(acc[0]);
+                    *GPTR(g_u16, row + 4 * c0 + 2) = clip10s(acc[2]);
+                }
+                if (c0 + 1 < J.ncols) {
+                    *GPTR(g_u16, row + 4 * c0 + 4) = clip10s(acc[1]);
+                    *GPTR(g_u16, row + 4 * c0 + 6) = clip10s(acc[3]);
+                }
+                return;
+            }
             const uint32_t U0 = clip8(acc[0]), U1 = clip8(acc[1]), V0 = clip8(acc[2]), V1 = clip8(acc[3]);
             if (dfmt == DTS_FMT_NV12) {
                 const uint64_t row = dst.data[1] + dbase + (int64_t)y * dst.pitch[1] + 2 * J.x0;

@@ -23,7 +23,8 @@
 //    pitch (conflict-free writes down a column, reads across a row);
 //  * V: lane = output column, two output rows per wave and iteration,
 //    v_dot2_i32_i16 over ring dwords with the rows' tap pairs (staged in LDS
-//    one step ahead), then dither/round, >> 19, clip and a byte store.
+//    one step ahead), then dither/round, >> 19, clip and a byte store (p010
+//    output: + 1 << 16, >> 17, 10-bit clip, << 6 and a 16-bit store).
 #include "dts_internal.h"
 
 #ifndef DTS_L4_ABLATE
@@ -41,6 +42,7 @@ typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
 // constant address space: wave-uniform reads become s_load
 typedef __attribute__((address_space(4))) const uint32_t k_u32;
 typedef __attribute__((address_space(4))) const int32_t k_i32;
@@ -256,6 +258,14 @@ __device__ __forceinline__ void vstore(uint64_t p, int acc)
     *GP(g_u8, p) = (uint8_t)v;
 }
 
+// output.c yuv2p010lX_c / yuv2p010cX_c: av_clip_uintp2(val >> 17, 10) << 6, LE16
+__device__ __forceinline__ void vstore16(uint64_t p, int acc)
+{
+    int v = acc >> 17;
+    v = v < 0 ? 0 : (v > 1023 ? 1023 : v);
+    *GP(g_u16, p) = (uint16_t)(v << 6);
+}
+
 // Per-item state shared by the H and V halves of a walk.
 struct Item {
     const uint32_t *hco;                 // this wave's H taps (LDS)
@@ -271,6 +281,7 @@ struct Item {
     const int32_t *vslot;
     const int32_t *vlim;
     uint32_t sel, dlo, dhi;
+    bool d16;                            // p010 output (yuv2p010*: 1 << 16 rounding, no dither)
     int R, srcH, nsteps, nvp, lofs, nload, qend, col0, wave, lane, t;
     bool vact;
 };
@@ -289,11 +300,18 @@ __device__ __forceinline__ void vpass(const Item &I, int b)
     for (int y = vlo + I.wave; y < vhi; y += 8) {
         const int y2 = min(y + 4, vhi - 1);
         const int i0 = y - vlo, i1 = y2 - vlo;
-        const int a0 = vtaps(I.rl, I.R, uni(vsl[i0]), ng, vco + i0 * I.nvp, vinit<SRC>(y, I.dlo, I.dhi));
-        const int a1 = vtaps(I.rl, I.R, uni(vsl[i1]), ng, vco + i1 * I.nvp, vinit<SRC>(y2, I.dlo, I.dhi));
+        const int a0 = vtaps(I.rl, I.R, uni(vsl[i0]), ng, vco + i0 * I.nvp,
+                             I.d16 ? 1 << 16 : vinit<SRC>(y, I.dlo, I.dhi));
+        const int a1 = vtaps(I.rl, I.R, uni(vsl[i1]), ng, vco + i1 * I.nvp,
+                             I.d16 ? 1 << 16 : vinit<SRC>(y2, I.dlo, I.dhi));
         if (I.vact) {
-            vstore(I.obase + (int64_t)y * I.opitch, a0);
-            if (y + 4 < vhi) vstore(I.obase + (int64_t)y2 * I.opitch, a1);
+            if (I.d16) {
+                vstore16(I.obase + (int64_t)y * I.opitch, a0);
+                if (y + 4 < vhi) vstore16(I.obase + (int64_t)y2 * I.opitch, a1);
+            } else {
+                vstore(I.obase + (int64_t)y * I.opitch, a0);
+                if (y + 4 < vhi) vstore(I.obase + (int64_t)y2 * I.opitch, a1);
+            }
         }
     }
 }
@@ -419,9 +437,13 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
     const DevPlanes dst = P.dst[J.rung];
     const int dfmt = P.dst_fmt[J.rung];
     const uint64_t dfb = (uint64_t)frame * dst.fstride;
+    I.d16 = dfmt == DTS_FMT_P010LE;
     if (kind == 0) {
-        I.obase = dst.data[0] + dfb + J.x0 + I.lane;
+        I.obase = dst.data[0] + dfb + (uint64_t)(J.x0 + I.lane) * (I.d16 ? 2 : 1);
         I.opitch = dst.pitch[0];
+    } else if (I.d16) {                                            // p010: U16,V16 pairs
+        I.obase = dst.data[1] + dfb + 4 * (J.x0 + I.lane) + 2 * cpl;
+        I.opitch = dst.pitch[1];
     } else if (dfmt == DTS_FMT_NV12) {
         I.obase = dst.data[1] + dfb + 2 * (J.x0 + I.lane) + cpl;
         I.opitch = dst.pitch[1];

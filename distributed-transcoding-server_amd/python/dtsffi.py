@@ -26,6 +26,10 @@ METHODS = {"bilinear": SCALE_BILINEAR, "bicubic": SCALE_BICUBIC, "x": SCALE_X, "
            "lanczos": SCALE_LANCZOS}
 PARAM_DEFAULT = 123456.0
 Q_NONE, Q_PSNR, Q_SSIM, Q_BOTH = 0, 1, 2, 3
+# vf_tonemap.c enum TonemapAlgorithm
+TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS = range(7)
+TM_MODES = {"none": TM_NONE, "linear": TM_LINEAR, "gamma": TM_GAMMA, "clip": TM_CLIP, "reinhard": TM_REINHARD,
+            "hable": TM_HABLE, "mobius": TM_MOBIUS}
 MAX_OUTPUTS = 4
 
 E_INVAL, E_NOMEM, E_RANGE, E_UNSUPPORTED, E_BUSY, E_NODEV, E_HIP = -22, -12, -34, -95, -16, -19, -1000
@@ -36,10 +40,16 @@ class OutputSpec(ctypes.Structure):
                 ("method", ctypes.c_int32), ("param", ctypes.c_double * 2)]
 
 
+class TonemapSpec(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("pad_", ctypes.c_int32), ("param", ctypes.c_double),
+                ("desat", ctypes.c_double), ("peak", ctypes.c_double), ("npl", ctypes.c_double)]
+
+
 class GraphSpec(ctypes.Structure):
     _fields_ = [("src_w", ctypes.c_int32), ("src_h", ctypes.c_int32), ("src_fmt", ctypes.c_int32),
                 ("nout", ctypes.c_int32), ("out", OutputSpec * MAX_OUTPUTS),
-                ("quality", ctypes.c_int32), ("quality_out", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
+                ("quality", ctypes.c_int32), ("quality_out", ctypes.c_int32), ("max_batch", ctypes.c_int32),
+                ("hdr_to_sdr", ctypes.c_int32), ("tonemap", TonemapSpec)]
 
 
 class Frame(ctypes.Structure):
@@ -214,8 +224,9 @@ def graph_plan(spec):
     return info
 
 
-def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0):
-    """outputs: list of (w, h, fmt, method[, (p0, p1)])."""
+def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0, tonemap=None):
+    """outputs: list of (w, h, fmt, method[, (p0, p1)]).  tonemap: None, or a dict
+    {mode, param, desat, peak, npl} turning on HDR10 -> SDR (dts_tonemap_spec)."""
     s = GraphSpec()
     s.src_w, s.src_h, s.src_fmt = src_w, src_h, src_fmt
     s.nout = len(outputs)
@@ -224,6 +235,13 @@ def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max
         par = o[4] if len(o) > 4 else (PARAM_DEFAULT, PARAM_DEFAULT)
         s.out[i].param[0], s.out[i].param[1] = par
     s.quality, s.quality_out, s.max_batch = quality, quality_out, max_batch
+    if tonemap is not None:
+        s.hdr_to_sdr = 1
+        s.tonemap.mode = tonemap.get("mode", TM_HABLE)
+        s.tonemap.param = tonemap.get("param", float("nan"))
+        s.tonemap.desat = tonemap.get("desat", 0.0)
+        s.tonemap.peak = tonemap.get("peak", 0.0)
+        s.tonemap.npl = tonemap.get("npl", 100.0)
     return s
 
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define DTS_ABI_VERSION 1
+#define DTS_ABI_VERSION 2
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -66,6 +66,15 @@ extern "C" {
 #define DTS_SCALE_LANCZOS  0x200
 #define DTS_PARAM_DEFAULT  123456.0 /* SWS_PARAM_DEFAULT */
 
+/* HDR10 -> SDR tone mapping curves: vf_tonemap.c enum TonemapAlgorithm */
+#define DTS_TM_NONE     0
+#define DTS_TM_LINEAR   1
+#define DTS_TM_GAMMA    2
+#define DTS_TM_CLIP     3
+#define DTS_TM_REINHARD 4
+#define DTS_TM_HABLE    5
+#define DTS_TM_MOBIUS   6
+
 /* quality checks (vf_psnr / vf_ssim) */
 #define DTS_Q_NONE 0
 #define DTS_Q_PSNR 1
@@ -75,9 +84,20 @@ extern "C" {
 typedef struct dts_ctx dts_ctx;
 typedef struct dts_graph dts_graph;
 
+typedef struct dts_tonemap_spec {
+    int32_t mode;       /* DTS_TM_* (vf_tonemap tonemap=) */
+    int32_t pad_;
+    double param;       /* vf_tonemap param; NaN = the curve's default (init()) */
+    double desat;       /* vf_tonemap desat; <= 0 = off */
+    double peak;        /* vf_tonemap peak (units of npl); <= 0 = its fallback for
+                           linear input without HDR side data: 10 */
+    double npl;         /* zscale npl, cd/m^2 mapped to 1.0; <= 0 = 100 */
+} dts_tonemap_spec;
+
 typedef struct dts_output_spec {
     int32_t w, h;       /* output size (even for 4:2:0 not required) */
-    int32_t fmt;        /* DTS_FMT_YUV420P or DTS_FMT_NV12 */
+    int32_t fmt;        /* DTS_FMT_YUV420P, DTS_FMT_NV12 or DTS_FMT_P010LE
+                           (output.c yuv2p010lX_c / yuv2p010cX_c) */
     int32_t method;     /* DTS_SCALE_*; always run as method|ACCURATE_RND|BITEXACT */
     double param[2];    /* sws param[0..1]; DTS_PARAM_DEFAULT for defaults */
 } dts_output_spec;
@@ -89,6 +109,14 @@ typedef struct dts_graph_spec {
     int32_t quality;                    /* DTS_Q_* */
     int32_t quality_out;                /* output index compared with qref */
     int32_t max_batch;                  /* frames per device launch; 0 = 32 */
+    /* HDR10 -> SDR (BASELINE config 3): the source is p010 PQ bt2020nc
+     * limited range; every output (8-bit yuv420p/nv12, even w/h) is scaled
+     * bit-exactly to a p010 intermediate and then converted as by
+     *   zscale=t=linear:npl=NPL,format=gbrpf32le,zscale=p=bt709,
+     *   tonemap=MODE:param=P:desat=D:peak=K,zscale=t=bt709:m=bt709:r=tv
+     * (float path, +-1 LSB vs the double restatement). */
+    int32_t hdr_to_sdr;                 /* 0 = off */
+    dts_tonemap_spec tonemap;
 } dts_graph_spec;
 
 /* host frame: plane p at data[p] with row pitch pitch[p] bytes.

@@ -53,8 +53,8 @@ int orc_init_filter(int16_t *coeff, int32_t *pos, int cap_taps,
 /* utils.c get_local_pos() */
 int orc_get_local_pos(int chr_subsample, int pos);
 
-/* One frame through the scaler: src/dst formats in {YUV420P, NV12, P010LE
- * (src only)}; planes addressed by data[3]/pitch[3] in bytes (for NV12 and
+/* One frame through the scaler: src/dst formats in {YUV420P, NV12, P010LE}
+ * (p010 output: output.c yuv2p010lX_c / yuv2p010cX_c); planes addressed by data[3]/pitch[3] in bytes (for NV12 and
  * P010 plane 1 is the interleaved UV plane, plane 2 unused).
  * Returns 0 or <0 on unsupported parameters. */
 int orc_scale_frame(int srcW, int srcH, int srcFmt,
@@ -86,6 +86,17 @@ void orc_quality_frame420(int w, int h, const uint8_t *const a[3],
  * `cap` indices, returns the number of output frames. */
 int orc_fps_map(int64_t nb_in, int in_num, int in_den, int out_num, int out_den,
                 int64_t *out_idx, int cap);
+
+/* HDR10 (p010, PQ, bt2020nc, limited) -> SDR bt709 8-bit 4:2:0 at the same
+ * size (vf_tonemap_ref.c): zscale linearise + primaries + vf_tonemap MODE
+ * (0 none, 1 linear, 2 gamma, 3 clip, 4 reinhard, 5 hable, 6 mobius) + zscale
+ * bt709 out.  param NaN = vf_tonemap default; peak <= 0 -> 10; npl <= 0 ->
+ * 100.  w and h even.  Returns 0 or <0. */
+int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_t src_pitch[3],
+                         int dstFmt, uint8_t *const dst[3], const int64_t dst_pitch[3],
+                         int mode, double param, double desat, double peak, double npl);
+double orc_tonemap_param(int mode, double param);
+void orc_bt2020_to_bt709(double m[3][3]);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,12 @@ def lib():
         L.orc_quality_frame420.argtypes = [i32, i32, ctypes.POINTER(vp), ctypes.POINTER(i64),
                                            ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.POINTER(OrcQStat)]
         L.orc_fps_map.argtypes = [i64, i32, i32, i32, i32, vp, i32]
+        d = ctypes.c_double
+        L.orc_hdr_to_sdr_frame.argtypes = [i32, i32, ctypes.POINTER(vp), ctypes.POINTER(i64), i32,
+                                           ctypes.POINTER(vp), ctypes.POINTER(i64), i32, d, d, d, d]
+        L.orc_tonemap_param.argtypes = [i32, d]
+        L.orc_tonemap_param.restype = d
+        L.orc_bt2020_to_bt709.argtypes = [ctypes.POINTER(d * 3)]
         _lib = L
     return _lib
 
@@ -73,6 +79,8 @@ def _alloc(w, h, fmt):
     cw, ch = (w + 1) // 2, (h + 1) // 2
     if fmt == 0:
         return [np.zeros((h, w), np.uint8), np.zeros((ch, cw), np.uint8), np.zeros((ch, cw), np.uint8)]
+    if fmt == 2:
+        return [np.zeros((h, 2 * w), np.uint8), np.zeros((ch, 4 * cw), np.uint8), None]
     return [np.zeros((h, w), np.uint8), np.zeros((ch, 2 * cw), np.uint8), None]
 
 
@@ -117,3 +125,23 @@ def fps_map(nb_in, in_rate, out_rate, cap=1 << 20):
     out = np.zeros(cap, np.int64)
     n = lib().orc_fps_map(nb_in, in_rate[0], in_rate[1], out_rate[0], out_rate[1], out.ctypes.data, cap)
     return out[:n]
+
+
+TM_MODES = {"none": 0, "linear": 1, "gamma": 2, "clip": 3, "reinhard": 4, "hable": 5, "mobius": 6}
+
+
+def hdr_to_sdr(src_planes, w, h, dst_fmt, mode=5, param=float("nan"), desat=0.0, peak=0.0, npl=0.0):
+    """HDR10 p010 -> SDR bt709 8-bit (zscale + vf_tonemap restated, double precision)."""
+    dst = _alloc(w, h, dst_fmt)
+    sd, sp = _ptrs(src_planes)
+    dd, dp = _ptrs(dst)
+    r = lib().orc_hdr_to_sdr_frame(w, h, sd, sp, dst_fmt, dd, dp, mode, param, desat, peak, npl)
+    if r != 0:
+        raise RuntimeError(f"orc_hdr_to_sdr_frame failed ({r})")
+    return dst
+
+
+def bt2020_to_bt709():
+    m = ((ctypes.c_double * 3) * 3)()
+    lib().orc_bt2020_to_bt709(m)
+    return np.array([[m[i][j] for j in range(3)] for i in range(3)])

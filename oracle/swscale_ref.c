@@ -425,6 +425,47 @@ static void yuv2nv12cX(const uint8_t *chrDither, const int16_t *chrFilter,
     }
 }
 
+/* output.c av_clip_uintp2(val >> 17, 10) << 6 as AV_WL16 (output_pixel of
+ * the p010 writers, shift = 17) */
+static inline void put_p010(uint8_t *d, int val)
+{
+    int v = val >> 17;
+    if (v & ~1023) v = (~v >> 31) & 1023;
+    v <<= 6;
+    d[0] = (uint8_t)v;
+    d[1] = (uint8_t)(v >> 8);
+}
+
+/* output.c yuv2p010lX_c (LE): val = 1 << 16 + sum, no dither (yuv2p010l1_c's
+ * (src + 16) >> 5 is the same value for the single 4096 tap) */
+static void yuv2p010lX(const int16_t *filter, int filterSize, const int16_t **src,
+                       uint8_t *dest, int dstW)
+{
+    int i, j;
+    for (i = 0; i < dstW; i++) {
+        int val = 1 << 16;
+        for (j = 0; j < filterSize; j++)
+            val += src[j][i] * filter[j];
+        put_p010(dest + 2 * i, val);
+    }
+}
+
+/* output.c yuv2p010cX_c (LE, U first) */
+static void yuv2p010cX(const int16_t *chrFilter, int chrFilterSize, const int16_t **chrUSrc,
+                       const int16_t **chrVSrc, uint8_t *dest, int chrDstW)
+{
+    int i, j;
+    for (i = 0; i < chrDstW; i++) {
+        int u = 1 << 16, v = 1 << 16;
+        for (j = 0; j < chrFilterSize; j++) {
+            u += chrUSrc[j][i] * chrFilter[j];
+            v += chrVSrc[j][i] * chrFilter[j];
+        }
+        put_p010(dest + 4 * i, u);
+        put_p010(dest + 4 * i + 2, v);
+    }
+}
+
 /* Horizontal pass over every source row of one plane -> 15-bit rows.
  * kind: 0 = 8-bit plane, 1 = 8-bit interleaved (take byte `comp` of pairs),
  *       2 = p010 plane (LE16 >> 6), 3 = p010 interleaved (comp). */
@@ -465,7 +506,7 @@ static int16_t *hpass(const uint8_t *base, int64_t pitch, int kind, int comp,
 
 static int fmt_is_nv(int fmt) { return fmt == ORC_FMT_NV12 || fmt == ORC_FMT_P010LE; }
 
-/* swscale.c swscale() main loop for 4:2:0 -> 4:2:0, 8-bit output,
+/* swscale.c swscale() main loop for 4:2:0 -> 4:2:0, 8-bit or p010 output,
  * restricted to the BITEXACT|ACCURATE_RND C path (no range conversion:
  * both sides limited-range YUV). */
 int orc_scale_frame(int srcW, int srcH, int srcFmt,
@@ -485,7 +526,7 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
     int y, j;
 
     if (srcW < 4 || srcH < 4 || dstW < 2 || dstH < 2) return -22;
-    if (dstFmt != ORC_FMT_YUV420P && dstFmt != ORC_FMT_NV12) return -22;
+    if (dstFmt != ORC_FMT_YUV420P && dstFmt != ORC_FMT_NV12 && dstFmt != ORC_FMT_P010LE) return -22;
     if (srcFmt != ORC_FMT_YUV420P && srcFmt != ORC_FMT_NV12 && srcFmt != ORC_FMT_P010LE) return -22;
 
     if (make_filter(&hl, srcW, dstW, 4, 1 << 14, flags, param, lpos, lpos) < 0 ||
@@ -511,6 +552,11 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
             if (r > srcH - 1) r = srcH - 1; /* zero-coefficient taps only */
             lines[j] = ly + (size_t)r * dstW;
         }
+        if (dstFmt == ORC_FMT_P010LE) {
+            yuv2p010lX(vl.coeff + (size_t)y * vl.size, vl.size, lines,
+                       dst[0] + (int64_t)y * dst_pitch[0], dstW);
+            continue;
+        }
         yuv2planeX_8(vl.coeff + (size_t)y * vl.size, vl.size, lines,
                      dst[0] + (int64_t)y * dst_pitch[0], dstW, lumDither, 0);
     }
@@ -522,7 +568,10 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
             ulines[j] = lu + (size_t)r * chrDstW;
             vlines[j] = lv + (size_t)r * chrDstW;
         }
-        if (dstFmt == ORC_FMT_NV12) {
+        if (dstFmt == ORC_FMT_P010LE) {
+            yuv2p010cX(vc.coeff + (size_t)y * vc.size, vc.size, ulines, vlines,
+                       dst[1] + (int64_t)y * dst_pitch[1], chrDstW);
+        } else if (dstFmt == ORC_FMT_NV12) {
             yuv2nv12cX(chrDither, vc.coeff + (size_t)y * vc.size, vc.size, ulines, vlines,
                        dst[1] + (int64_t)y * dst_pitch[1], chrDstW);
         } else {
