@@ -34,10 +34,28 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-transcoding-server_amd", "pyt
 import dtsffi as D  # noqa: E402
 
 METRIC = "frames/s and % HBM roofline, 4K→ABR ladder scale+convert, 1/2/4/8 MI355X"
+FMTS = {D.FMT_YUV420P: "yuv420p", D.FMT_NV12: "nv12", D.FMT_P010LE: "p010le"}
 HBM_PEAK = 8.0e12       # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table)
 SRC_W, SRC_H = 3840, 2160
 LADDER = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_NV12, D.SCALE_BICUBIC),
           (854, 480, D.FMT_NV12, D.SCALE_BICUBIC)]
+
+# BASELINE.json configs measurable on one GPU.  cfg2 is the metric's workload (the
+# default bench line); cfg3 / cfg4 are extra lines (--workload) with their own
+# algorithmic bytes.
+WORKLOADS = {
+    "cfg2": {"src": (SRC_W, SRC_H, D.FMT_YUV420P), "outs": LADDER, "tonemap": None, "quality": False,
+             "desc": "cfg2: 4K60 8-bit yuv420p -> 1080p/720p/854x480 nv12 ABR ladder, bicubic "
+                     "(SWS_BITEXACT|ACCURATE_RND semantics), one fused launch per batch"},
+    "cfg3": {"src": (SRC_W, SRC_H, D.FMT_P010LE), "outs": [(1920, 1080, D.FMT_YUV420P, D.SCALE_BICUBIC)],
+             "tonemap": {"mode": D.TM_HABLE, "desat": 0.0, "peak": 0.0, "npl": 100.0}, "quality": False,
+             "desc": "cfg3: 4K60 10-bit p010 HDR10 (PQ, bt2020nc) -> SDR bt709 8-bit 1080p yuv420p: bit-exact "
+                     "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB)"},
+    "cfg4": {"src": (7680, 4320, D.FMT_YUV420P), "outs": [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)],
+             "tonemap": None, "quality": True,
+             "desc": "cfg4: 8K30 yuv420p -> 4K lanczos + per-frame vf_psnr/vf_ssim of the output vs a 4K "
+                     "reference"},
+}
 
 
 def dev_batch(t, w, h, fmt, pitch_align=256):
@@ -65,17 +83,39 @@ def frame_bytes(w, h, fmt, pitch_align=256):
     return (off + 4095) // 4096 * 4096
 
 
-def cpu_baseline(budget_s, threads):
-    """Oracle (C restatement of libswscale, single frame per thread) on host cores."""
+def oracle_outputs(wl, src, qref=None):
+    """The CPU oracle's outputs (and quality record) for one source frame of workload wl."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
+    sw, sh, sfmt = wl["src"]
+    outs = []
+    for (w, h, fmt, m) in wl["outs"]:
+        if wl["tonemap"]:
+            t = wl["tonemap"]
+            mid = orc.scale_frame(src, sw, sh, sfmt, w, h, D.FMT_P010LE, m)
+            outs.append(orc.hdr_to_sdr(mid, w, h, fmt, t["mode"], float("nan"), t["desat"], t["peak"], t["npl"]))
+        else:
+            outs.append(orc.scale_frame(src, sw, sh, sfmt, w, h, fmt, m))
+    q = None
+    if wl["quality"] and qref is not None:
+        w, h = wl["outs"][0][:2]
+        q = orc.quality_frame(w, h, outs[0], qref)
+    return outs, q
+
+
+def cpu_baseline(wl_name, budget_s, threads):
+    """Oracle (C restatement of libswscale / vf_*, single frame per thread) on host cores."""
     from concurrent.futures import ThreadPoolExecutor
-    frames = [D.synth_host(SRC_W, SRC_H, D.FMT_YUV420P, 0, 0x5EED, i) for i in range(threads)]
+    wl = WORKLOADS[wl_name]
+    sw, sh, sfmt = wl["src"]
+    frames = [D.synth_host(sw, sh, sfmt, 0, 0x5EED, i) for i in range(threads)]
+    qref = None
+    if wl["quality"]:
+        w, h, fmt, _ = wl["outs"][0]
+        qref = D.synth_host(w, h, fmt, 0, 0x0EF, 0)
 
     def one(i):
-        src = frames[i % len(frames)]
-        for (w, h, fmt, m) in LADDER:
-            orc.scale_frame(src, SRC_W, SRC_H, 0, w, h, fmt, m)
+        oracle_outputs(wl, frames[i % len(frames)], qref)
         return 1
     done = 0
     t0 = time.perf_counter()
@@ -84,8 +124,8 @@ def cpu_baseline(budget_s, threads):
             done += sum(ex.map(one, range(done, done + threads)))
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{done} synthetic 4K yuv420p frames through the 3-rung bicubic nv12 ladder by the CPU "
-                      f"oracle (plain-C libswscale C-path restatement, ctypes, 1 frame per thread) in {dt:.1f} s; "
+            "sample": f"{done} synthetic {sw}x{sh} source frames through the {wl_name} graph by the CPU "
+                      f"oracle (plain-C libswscale / vf_* restatement, ctypes, 1 frame per thread) in {dt:.1f} s; "
                       "ffmpeg is not installed on the box"}
 
 
@@ -99,24 +139,40 @@ def hip_runtimes():
     return sorted(libs)
 
 
-def verify_first_frame(src_index, outs):
-    """Bit-exact check of frame 0 of the last batch against the CPU oracle."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def unpack_dev_frame(raw, w, h, fmt):
+    """Plane list of frame row `raw` laid out by dev_batch."""
+    planes, off = [], 0
+    for shp in D.plane_shapes(w, h, fmt):
+        if shp is None:
+            planes.append(None)
+            continue
+        pitch = (shp[1] + 255) // 256 * 256
+        planes.append(raw[off:off + pitch * shp[0]].reshape(shp[0], pitch)[:, :shp[1]])
+        off += pitch * shp[0]
+    return planes
+
+
+def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None):
+    """Frame 0 of the last batch against the CPU oracle: bit-exact for the
+    integer paths, +-1 LSB for the HDR float path, 1e-4 for SSIM."""
     import numpy as np
-    import orc
-    host = D.synth_host(SRC_W, SRC_H, D.FMT_YUV420P, 0, 0x5EED, src_index)
-    for k, (w, h, fmt, m) in enumerate(LADDER):
-        want = orc.scale_frame(host, SRC_W, SRC_H, 0, w, h, fmt, m)
-        raw = outs[k][0].cpu().numpy()
-        off = 0
-        for p, shp in enumerate(D.plane_shapes(w, h, fmt)):
-            if shp is None:
+    sw, sh, sfmt = wl["src"]
+    host = D.synth_host(sw, sh, sfmt, 0, 0x5EED, src_index)
+    want, wq = oracle_outputs(wl, host, qref_host)
+    for k, (w, h, fmt, m) in enumerate(wl["outs"]):
+        got = unpack_dev_frame(outs[k][0].cpu().numpy(), w, h, fmt)
+        for a, b in zip(got, want[k]):
+            if a is None:
                 continue
-            pitch = (shp[1] + 255) // 256 * 256
-            plane = raw[off:off + pitch * shp[0]].reshape(shp[0], pitch)[:, :shp[1]]
-            off += pitch * shp[0]
-            if not np.array_equal(plane, want[p]):
+            d = np.abs(a.astype(np.int16) - b.astype(np.int16))
+            if d.max() > (1 if wl["tonemap"] else 0):
                 return False
+    if wq is not None and qraw is not None:
+        w, h = wl["outs"][0][:2]
+        r = D.QRaw.from_buffer_copy(qraw[0].cpu().numpy().tobytes())
+        gq = D.qstat_finalize(w, h, [r])[0]
+        if gq["sse"] != wq["sse"] or abs(gq["ssim_all"] - wq["ssim_all"]) > 1e-4:
+            return False
     return True
 
 
@@ -144,7 +200,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS),
+                    help="cfg2 = the BASELINE metric's workload (default line); cfg3 / cfg4 = extra lines")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    sw, sh, sfmt = wl["src"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -163,23 +223,32 @@ def main():
     runtimes = hip_runtimes()
     if len(runtimes) != 1:
         print(f"WARNING: {len(runtimes)} HIP runtimes mapped: {runtimes}", file=sys.stderr)
-    g = D.Graph(ctx, D.make_spec(SRC_W, SRC_H, D.FMT_YUV420P, LADDER))
-    info = g.info
     B, R = args.batch, max(args.ring, 2 * args.batch)
     R = (R // B) * B
+    g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, wl["outs"], quality=D.Q_BOTH if wl["quality"] else D.Q_NONE,
+                                 max_batch=B, tonemap=wl["tonemap"]))
+    info = g.info
 
     # device-resident source ring: this rank's segments (frame index offset by rank)
-    sfb = frame_bytes(SRC_W, SRC_H, D.FMT_YUV420P)
+    sfb = frame_bytes(sw, sh, sfmt)
     src = torch.empty((R, sfb), dtype=torch.uint8, device=dev)
-    sd, _ = dev_batch(src, SRC_W, SRC_H, D.FMT_YUV420P)
+    sd, _ = dev_batch(src, sw, sh, sfmt)
     first = rank * 1_000_000
-    ctx.synth_device(SRC_W, SRC_H, D.FMT_YUV420P, 0, 0x5EED, first, sd, R, sptr)
+    ctx.synth_device(sw, sh, sfmt, 0, 0x5EED, first, sd, R, sptr)
     outs, ods = [], []
-    for (w, h, fmt, _m) in LADDER:
+    for (w, h, fmt, _m) in wl["outs"]:
         t = torch.empty((B, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
         d, _ = dev_batch(t, w, h, fmt)
         outs.append(t)
         ods.append(d)
+    qref = qrd = qraw = None
+    if wl["quality"]:                      # the 4K reference the output is scored against (one frame, reused)
+        w, h, fmt, _m = wl["outs"][0]
+        qref = torch.empty((B, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
+        qrd, _ = dev_batch(qref, w, h, fmt)
+        qrd.frame_stride = 0
+        ctx.synth_device(w, h, fmt, 0, 0x0EF, 0, qrd, 1, sptr)
+        qraw = torch.zeros((B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev)
 
     def batch_src(step):
         i0 = (step * B) % R
@@ -190,8 +259,12 @@ def main():
         d.frame_stride = sd.frame_stride
         return d
 
+    def step(i):
+        g.run_device(batch_src(i), B, ods, qref=qrd, qraw_ptr=qraw.data_ptr() if qraw is not None else 0,
+                     stream=sptr)
+
     for s in range(args.warmup):
-        g.run_device(batch_src(s), B, ods, stream=sptr)
+        step(s)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -201,7 +274,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         ev[s][0].record(stream)
-        g.run_device(batch_src(args.warmup + s), B, ods, stream=sptr)
+        step(args.warmup + s)
         ev[s][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -226,26 +299,31 @@ def main():
     verified = None
     if rank == 0 and not args.no_verify:
         last = args.warmup + args.steps - 1
-        verified = verify_first_frame(first + (last * B) % R, outs)
+        qhost = None
+        if wl["quality"]:
+            w, h, fmt, _m = wl["outs"][0]
+            qhost = D.synth_host(w, h, fmt, 0, 0x0EF, 0)
+        verified = verify_first_frame(wl, first + (last * B) % R, outs, qhost, qraw)
     if rank == 0:
         fps = frames_total / wall_max
         algo = info.algo_bytes_per_frame
         achieved = algo * B / (kern_ms * 1e-3)
-        traffic_pf, traffic_tag = load_traffic()
+        traffic_pf, traffic_tag = load_traffic() if args.workload == "cfg2" else (None, None)
         # PMC bytes (FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits included) per launch over this run's
         # kernel time, in the unit of `achieved`
         traffic = round(traffic_pf * B / (kern_ms * 1e-3) / 1e9, 1) if traffic_pf else None
         line = {
-            "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": world,
+            "metric": METRIC if args.workload == "cfg2" else f"frames/s and % HBM roofline, {args.workload}",
+            "value": round(fps, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": f"synthetic testsrc2-like 4K yuv420p (seed 0x5EED), device-resident ring of {R} frames per GPU",
-            "config": {"workload": "cfg2: 4K60 8-bit yuv420p -> 1080p/720p/854x480 nv12 ABR ladder, bicubic "
-                                   "(SWS_BITEXACT|ACCURATE_RND semantics), one fused launch per batch",
-                       "src": f"{SRC_W}x{SRC_H} yuv420p", "outputs": ["1920x1080 nv12", "1280x720 nv12",
-                                                                      "854x480 nv12"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8" if not wl["tonemap"] else "u16 scale + f32 tonemap",
+            "data": f"synthetic testsrc2-like {sw}x{sh} {FMTS[sfmt]} (seed 0x5EED), device-resident ring of {R} "
+                    "frames per GPU",
+            "config": {"workload": wl["desc"], "src": f"{sw}x{sh} {FMTS[sfmt]}",
+                       "outputs": [f"{w}x{h} {FMTS[fmt]}" for (w, h, fmt, _m) in wl["outs"]],
                        "batch_frames": B, "parallelism": f"segments x{world} (one process per GPU)"},
-            "mpixel_per_s": round(fps * SRC_W * SRC_H / 1e6, 1),
+            "mpixel_per_s": round(fps * sw * sh / 1e6, 1),
             "verified_vs_oracle": verified, "hip_runtime": runtimes,
             "algo_bytes_per_frame": algo,
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
@@ -256,7 +334,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             threads = min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)
+            line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, threads)
         print(json.dumps(line), flush=True)
     g.close()
     ctx.close()
