@@ -1,0 +1,104 @@
+"use strict";
+// ladder.js -- Jobs rows -> one libdts graph spec per source (SURVEY.md §8b/§8f).
+//
+// In the reference a rendition is one `job_list` row (database.js:61-94:
+// width, height, framerate, bitrate, codec, codecSettings, chunks) that points
+// at its source (`sourceID`, database.js:66-72).  A CPU worker would run one
+// ffmpeg per row and segment; the GPU worker groups the rows that share a
+// source into ONE graph with an output per row -- the `split=N` ladder -- so
+// the source segment is read from HBM once for all renditions.
+//
+// Node 12 (this image): no `??` / `?.`.
+
+const FMT = { yuv420p: 0, nv12: 1, p010le: 2, p010: 2 };
+// libswscale SWS_* flag values (swscale.h), as include/dts.h DTS_SCALE_*
+const METHOD = { bilinear: 0x2, bicubic: 0x4, x: 0x8, point: 0x10, neighbor: 0x10, area: 0x20, gauss: 0x80,
+                 sinc: 0x100, lanczos: 0x200 };
+// vf_tonemap.c enum TonemapAlgorithm (include/dts.h DTS_TM_*)
+const TONEMAP = { none: 0, linear: 1, gamma: 2, clip: 3, reinhard: 4, hable: 5, mobius: 6 };
+const MAX_OUTPUTS = 4;
+
+// Jobs.codecSettings is free text in the reference (database.js:78).  The GPU
+// worker reads an optional JSON object from it with the filtergraph knobs a CPU
+// worker would put on its ffmpeg command line:
+//   {"scale": "bicubic", "format": "nv12", "param": [b, c], "tonemap": {"mode": "hable", ...}}
+function parseSettings(text) {
+    if (!text) return {};
+    try {
+        const o = JSON.parse(text);
+        return o && typeof o === "object" ? o : {};
+    } catch (e) {
+        return {};                        // plain encoder options: nothing for the filtergraph
+    }
+}
+
+function outputOf(job) {
+    const s = parseSettings(job.codecSettings);
+    const method = METHOD[String(s.scale || "bicubic").toLowerCase()];
+    if (method === undefined) throw new Error("job " + job.id + ": unknown scale method " + s.scale);
+    const fmt = FMT[String(s.format || "nv12").toLowerCase()];
+    if (fmt === undefined) throw new Error("job " + job.id + ": unknown output format " + s.format);
+    const o = { w: job.width | 0, h: job.height | 0, fmt: fmt, method: method };
+    if (Array.isArray(s.param)) o.param = s.param.slice(0, 2);
+    return o;
+}
+
+function tonemapOf(job) {
+    const s = parseSettings(job.codecSettings);
+    if (!s.tonemap) return null;
+    const t = typeof s.tonemap === "string" ? { mode: s.tonemap } : s.tonemap;
+    const mode = TONEMAP[String(t.mode || "hable").toLowerCase()];
+    if (mode === undefined) throw new Error("job " + job.id + ": unknown tonemap " + t.mode);
+    const r = { mode: mode };
+    ["param", "desat", "peak", "npl"].forEach(function (k) { if (typeof t[k] === "number") r[k] = t[k]; });
+    return r;
+}
+
+// Group rendition rows by source.  src: {w, h, fmt, fps: [num, den]} per sourceID.
+// Returns [{sourceID, jobs: [row...], spec}] with at most MAX_OUTPUTS rows per graph
+// (a larger ladder is split into several graphs over the same source).
+function planLadders(jobs, sources) {
+    const bySrc = new Map();                   // one ladder per (source, output frame rate)
+    jobs.forEach(function (j) {
+        const key = j.sourceID + "@" + (j.framerate || 0);
+        if (!bySrc.has(key)) bySrc.set(key, []);
+        bySrc.get(key).push(j);
+    });
+    const plans = [];
+    bySrc.forEach(function (rows) {
+        const sid = rows[0].sourceID;
+        const src = sources[sid];
+        if (!src) throw new Error("source " + sid + " has no stream info");
+        rows.sort(function (a, b) { return b.width * b.height - a.width * a.height || a.id - b.id; });
+        for (let i = 0; i < rows.length; i += MAX_OUTPUTS) {
+            const part = rows.slice(i, i + MAX_OUTPUTS);
+            const tm = tonemapOf(part[0]);
+            part.forEach(function (r) {
+                if (JSON.stringify(tonemapOf(r)) !== JSON.stringify(tm))
+                    throw new Error("jobs " + part[0].id + "/" + r.id + ": one graph needs one tonemap setting");
+            });
+            const spec = { src: { w: src.w, h: src.h, fmt: src.fmt }, outputs: part.map(outputOf), quality: 0,
+                           maxBatch: 32 };
+            if (tm) spec.tonemap = tm;
+            plans.push({ sourceID: sid, framerate: part[0].framerate || 0, jobs: part, spec: spec });
+        }
+    });
+    return plans;
+}
+
+// Jobs.framerate (database.js:75) vs the source rate: the vf_fps (round=near)
+// input frame of every output frame of a segment of `n` source frames.
+function rateOf(fps) {
+    return Number.isInteger(fps) ? [fps, 1] : [Math.round(fps * 1001), 1001];      // 29.97 -> 30000/1001
+}
+
+function fpsFrames(addon, n, srcFps, outFps) {
+    if (!outFps || !srcFps) return null;
+    const r = rateOf(outFps);
+    if (r[0] * srcFps[1] === srcFps[0] * r[1]) return null;                       // same rate: identity
+    return addon.fpsMap(n, srcFps[0], srcFps[1], r[0], r[1]);
+}
+
+module.exports = { FMT: FMT, METHOD: METHOD, TONEMAP: TONEMAP, MAX_OUTPUTS: MAX_OUTPUTS, parseSettings: parseSettings,
+                   outputOf: outputOf, tonemapOf: tonemapOf, planLadders: planLadders, rateOf: rateOf,
+                   fpsFrames: fpsFrames };

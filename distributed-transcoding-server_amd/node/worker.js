@@ -1,0 +1,57 @@
+"use strict";
+// worker.js -- the GPU transcoding worker entry: Jobs/JobChunks rows in,
+// renditions + updated JobChunks rows out (the drop-in for a CPU worker that
+// spawns ffmpeg-static per segment, index.js:9).
+//
+//   node worker.js <job.json> [--dump DIR]
+//
+// job.json: {"workerId": 1, "segmentFrames": 600, "gpus": [0, ...] (optional),
+//            "sources": {"<sourceID>": {"w": 3840, "h": 2160, "fmt": 0, "fps": [60, 1]}},
+//            "jobs": [Jobs rows], "chunks": [JobChunks rows]}
+// Prints one JSON object: {"chunks": [updated rows], "summary": {...}}.
+// --dump DIR writes every output frame as DIR/<jobId>_<chunkOffset>_<frame>.raw
+// (packed planes) for offline checks.  Decode/encode stay in host libavcodec
+// and are not part of this process; the source here is libdts's synthetic one.
+const path = require("path");
+const fs = require("fs");
+
+function threadPool(n) {
+    // before any async work starts: one libuv worker per GPU slot (+ 2 spare)
+    if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = String(Math.max(4, n + 2));
+}
+
+function loadAddon() {
+    const p = process.env.DTS_ADDON || path.join(__dirname, "..", "addon", "dts_napi.node");
+    return require(p);
+}
+
+async function main(argv) {
+    const cfg = JSON.parse(fs.readFileSync(argv[0], "utf8"));
+    const di = argv.indexOf("--dump");
+    const dump = di >= 0 ? argv[di + 1] : null;
+    threadPool(cfg.gpus ? cfg.gpus.length : 8);
+    const addon = loadAddon();
+    const { GpuSegmentScheduler } = require("./scheduler");
+    const sink = dump ? function (plan, rows, per) {
+        per.forEach(function (frames, k) {
+            frames.forEach(function (f, i) {
+                const off = rows[k] ? rows[k].chunkOffset : "x";
+                const name = path.join(dump, plan.jobs[k].id + "_" + off + "_" + i + ".raw");
+                fs.writeFileSync(name, Buffer.concat(f.data.filter(function (b) { return b; })));
+            });
+        });
+    } : null;
+    const sched = new GpuSegmentScheduler({ addon: addon, gpus: cfg.gpus, workerId: cfg.workerId,
+                                            segmentFrames: cfg.segmentFrames, sink: sink });
+    const summary = await sched.runJobs(cfg.jobs, cfg.chunks, cfg.sources);
+    process.stdout.write(JSON.stringify({ chunks: cfg.chunks, summary: summary }) + "\n");
+}
+
+if (require.main === module) {
+    main(process.argv.slice(2)).catch(function (e) {
+        process.stderr.write("worker: " + (e && e.stack || e) + "\n");
+        process.exitCode = 1;
+    });
+}
+
+module.exports = { main: main };

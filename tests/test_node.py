@@ -1,0 +1,81 @@
+"""The Node.js GPU worker (distributed-transcoding-server_amd/node): ladder
+planning from Jobs rows, the GPU-slot-aware segment scheduler and the
+JobChunks state machine.
+
+CPU: tests/node/test_scheduler.js against a stand-in addon.
+GPU: worker.js through the real N-API addon (dts_napi.node -> libdts.so) on a
+small 3-rendition job; every dumped output frame must equal the CPU oracle
+bit-exactly, and the JobChunks rows must come back "done" with their sha1.
+"""
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import dtsffi as D
+import orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+
+def test_scheduler_cpu():
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "test_scheduler.js")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "ok" in r.stdout
+
+
+def test_addon_loads_cpu():
+    """The addon loads and reports the library version without a device."""
+    addon = os.path.join(ROOT, "distributed-transcoding-server_amd", "addon", "dts_napi.node")
+    r = subprocess.run([NODE, "-e", f"const a=require({json.dumps(addon)}); console.log(a.version());"
+                                    f"console.log(JSON.stringify(a.fpsMap(10, 60, 1, 30, 1)))"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split("\n")
+    assert lines[0].startswith("dts-mi355x")
+    assert json.loads(lines[1]) == [0, 2, 4, 6, 8]
+
+
+@pytest.mark.gpu
+def test_worker_gpu_bitexact(tmp_path):
+    sw, sh, seg = 384, 216, 3
+    jobs = [{"id": 21, "sourceID": 5, "width": 192, "height": 108, "framerate": 60},
+            {"id": 22, "sourceID": 5, "width": 128, "height": 72, "framerate": 60,
+             "codecSettings": json.dumps({"scale": "lanczos", "format": "yuv420p"})},
+            {"id": 23, "sourceID": 5, "width": 86, "height": 48, "framerate": 60}]
+    chunks = []
+    for j in jobs:
+        for off in range(2):
+            chunks.append({"id": len(chunks) + 1, "mainJob": j["id"], "chunkOffset": off, "assignedTo": None,
+                           "status": None, "result": None})
+    cfg = {"workerId": 3, "segmentFrames": seg, "gpus": [0],
+           "sources": {"5": {"w": sw, "h": sh, "fmt": 0, "fps": [60, 1]}}, "jobs": jobs, "chunks": chunks}
+    (tmp_path / "job.json").write_text(json.dumps(cfg))
+    dump = tmp_path / "out"
+    dump.mkdir()
+    r = subprocess.run([NODE, os.path.join(ROOT, "distributed-transcoding-server_amd", "node", "worker.js"),
+                        str(tmp_path / "job.json"), "--dump", str(dump)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    outs = {21: (192, 108, D.FMT_NV12, D.SCALE_BICUBIC), 22: (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS),
+            23: (86, 48, D.FMT_NV12, D.SCALE_BICUBIC)}
+    for c in res["chunks"]:
+        assert c["status"] == "done" and c["assignedTo"] == 3
+        rec = json.loads(c["result"])
+        w, h, fmt, m = outs[c["mainJob"]]
+        h1 = hashlib.sha1()
+        for i in range(seg):
+            src = D.synth_host(sw, sh, D.FMT_YUV420P, 0, 0x5EED, c["chunkOffset"] * seg + i)
+            want = orc.scale_frame(src, sw, sh, D.FMT_YUV420P, w, h, fmt, m)
+            packed = b"".join(np.ascontiguousarray(p).tobytes() for p in want if p is not None)
+            got = (dump / f"{c['mainJob']}_{c['chunkOffset']}_{i}.raw").read_bytes()
+            assert got == packed, f"job {c['mainJob']} chunk {c['chunkOffset']} frame {i}"
+            h1.update(packed)
+        assert rec["sha1"] == h1.hexdigest() and rec["frames"] == seg and rec["gpu"] == 0
