@@ -995,6 +995,36 @@ int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
     return quality_enqueue(ctx, w, h, fmt, *a, *b, nframes, qraw_dev, st);
 }
 
+int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames *seq, int nseq,
+                         int first, int count, const dts_dev_frames *dst, void *stream)
+{
+    if (!ctx || !seq || !dst || w < 16 || h < 4 || mode < 0 || mode > 3 || nseq < 1 || first < 0 || count < 0 ||
+        first + count > nseq)
+        return DTS_E_INVAL;
+    if (!planes_ok(*seq, w, h, DTS_FMT_YUV420P, 1) || !planes_ok(*dst, w, h, DTS_FMT_YUV420P, 1))
+        return DTS_E_INVAL;
+    if (count == 0) return DTS_OK;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+    const int fields = (mode & 1) ? 2 : 1;
+    YadifParams p{};
+    p.seq = to_dev(*seq, DTS_FMT_YUV420P);
+    p.w = w;
+    p.h = h;
+    p.nseq = nseq;
+    p.mode = mode;
+    p.tff = tff ? 1 : 0;
+    const int chunk = 32768;                              // outputs per launch (grid z)
+    for (int j0 = 0; j0 < count; j0 += chunk) {
+        const int n = std::min(chunk, count - j0);
+        p.first = first + j0;
+        p.dst = to_dev(*dst, DTS_FMT_YUV420P);
+        for (int pl = 0; pl < 3; ++pl) p.dst.data[pl] += (uint64_t)((int64_t)j0 * fields * dst->frame_stride);
+        HIPCHK(ctx, launch_yadif(p, n * fields, st));
+    }
+    return DTS_OK;
+}
+
 int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out)
 {
     if (!raw || !out || n < 0 || w < 1 || h < 1) return DTS_E_INVAL;

@@ -164,6 +164,17 @@ struct TonemapParams {
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);
 
 // ---------------------------------------------------------------------------
+// vf_yadif (deint.hip)
+// ---------------------------------------------------------------------------
+struct YadifParams {
+    DevPlanes seq;                  // nseq yuv420p frames (fstride apart)
+    DevPlanes dst;                  // output frames of this launch
+    int32_t w, h, nseq, first;      // outputs come from frames first, first + 1, ...
+    int32_t mode, tff;              // yadif mode 0..3, field order
+};
+hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Synthetic source (testsrc2-like), identical on host and device
 // ---------------------------------------------------------------------------
 __host__ __device__ inline uint32_t synth_hash(uint32_t x)

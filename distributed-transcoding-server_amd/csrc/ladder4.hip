@@ -27,6 +27,14 @@
 //    output: + 1 << 16, >> 17, 10-bit clip, << 6 and a 16-bit store).
 #include "dts_internal.h"
 
+#ifndef DTS_L4_HSMEM
+#define DTS_L4_HSMEM 1      // H taps: 1 = scalar loads (s_load) from the global table, 0 = LDS broadcast reads (r01v5)
+#endif
+
+#ifndef DTS_L4_VSMEM
+#define DTS_L4_VSMEM 0      // 1: V taps / ring slots read with scalar loads from the global tables (no LDS staging)
+#endif
+
 #ifndef DTS_L4_ABLATE
 #define DTS_L4_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads
 #endif
@@ -152,7 +160,11 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
         pb[q] = pair_at<CVT>(rb, q, sel, z);
         if (q % PPL == PPL - 1) load_chunk(ra, rb, nw, q / PPL, z);
     }
+#if DTS_L4_HSMEM
+    k_u32 *cg = GP(k_u32, cl);
+#else
     const uint4 *cv = reinterpret_cast<const uint4 *>(cl);
+#endif
     // a constant trip count (no early exit) keeps the loop fully unrolled, so
     // every pa/pb/ra/rb index is a compile-time register; qend is tested once
     // per 8 positions, the output mask once per position
@@ -167,6 +179,11 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
                 if (pn % PPL == PPL - 1) load_chunk(ra, rb, nw, pn / PPL, z);
                 if ((uint32_t)(mask >> q) & 1u) {
                     uint32_t c[NP];
+#if DTS_L4_HSMEM
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) c[i] = cg[i];
+                    cg += NP;
+#else
 #pragma unroll
                     for (int i = 0; i < NP / 4; ++i) {
                         const uint4 v = cv[i];
@@ -176,6 +193,7 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
                         c[4 * i + 3] = v.w;
                     }
                     cv += NP / 4;
+#endif
                     int a = 0, b = 0;
 #pragma unroll
                     for (int t = 0; t < N; ++t) {
@@ -213,9 +231,23 @@ constexpr int kCP = kRing4Cols + 1;   // ring column pitch (dwords)
 // (row pairs) from slot s0 on (wrapping at R), with the row's tap pairs in LDS
 // at cq (broadcast ds_read_b128; rows are zero-padded to groups of 4, so the
 // ring dwords past the window only meet zero taps).  s0 is wave-uniform.
+#if DTS_L4_VSMEM
+struct KQuad {                                  // 4 wave-uniform tap pairs through s_load
+    k_u32 *p;
+    __device__ __forceinline__ uint4 operator[](int g) const
+    {
+        return make_uint4(p[4 * g], p[4 * g + 1], p[4 * g + 2], p[4 * g + 3]);
+    }
+};
+#endif
+
 __device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, int ng, const uint32_t *cq, int acc)
 {
+#if DTS_L4_VSMEM
+    const KQuad c4{GP(k_u32, cq)};
+#else
     const uint4 *c4 = reinterpret_cast<const uint4 *>(cq);
+#endif
     if (s0 + 4 * ng <= R) {
         const uint32_t *p = rl + s0 * kCP;
         for (int g = 0; g < ng; ++g, p += 4 * kCP) {
@@ -294,8 +326,13 @@ __device__ __forceinline__ void vpass(const Item &I, int b)
 {
     k_i32 *vlim = GP(k_i32, I.vlim);
     const int vlo = b > 0 ? vlim[b - 1] : 0, vhi = vlim[b];
+#if DTS_L4_VSMEM
+    k_i32 *vsl = GP(k_i32, I.vslot) + vlo;
+    const uint32_t *vco = I.vcoef + (int64_t)vlo * I.nvp;
+#else
     const int *vsl = I.vsl_base + (b & 1) * kV4SlotMax;
     const uint32_t *vco = I.vco_base + (b & 1) * kV4CoefDw;
+#endif
     const int ng = I.nvp >> 2;
     for (int y = vlo + I.wave; y < vhi; y += 8) {
         const int y2 = min(y + 4, vhi - 1);
@@ -356,7 +393,7 @@ __device__ __forceinline__ void walk(const Item &I, uint32_t *ring)
     }
     int slot0 = 0;
     for (int b = 0; b <= I.nsteps; ++b) {
-        if (b < I.nsteps) vstage(I, b);
+        if (!DTS_L4_VSMEM && b < I.nsteps) vstage(I, b);
         if (!(DTS_L4_ABLATE & 2) && b > 0) vpass<SRC>(I, b - 1);
         __syncthreads();
         if (b < I.nsteps) {
@@ -421,14 +458,19 @@ __device__ __forceinline__ void item4(const Ladder4Params &P, int frame, const J
     }
     // LDS: [ring][H taps: 4 waves][V taps: 2 step buffers][V slots: 2 step buffers]
     uint32_t *const hco = ring + kRing4Dw + I.wave * kH4CoefDw;
-    I.hco = hco;
     I.vco_base = ring + kRing4Dw + 4 * kH4CoefDw;
     I.vsl_base = reinterpret_cast<int *>(I.vco_base + 2 * kV4CoefDw);
+#if DTS_L4_HSMEM
+    I.hco = K.hcoef + hg.coef;                                     // read by s_load in hpass
+    (void)hco;
+#else
+    I.hco = hco;
     {   // this wave's output taps for the whole walk: global -> LDS once per item
         const int ndw = __builtin_popcountll(hg.mask) * ((K.N + 3) & ~3);
         const uint4 *g4 = reinterpret_cast<const uint4 *>(K.hcoef + hg.coef);
         for (int i = I.lane; i < ndw / 4; i += 64) reinterpret_cast<uint4 *>(hco)[i] = g4[i];
     }
+#endif
 
     // V-side constants of this lane
     I.vact = I.lane < J.ncols;

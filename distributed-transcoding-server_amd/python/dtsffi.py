@@ -90,7 +90,7 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_ctx_last_hip_error", "dts_graph_create", "dts_graph_destroy", "dts_graph_info_get",
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
-           "dts_sws_filter", "dts_fps_map", "dts_graph_plan"]
+           "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device"]
 
 _lib = None
 
@@ -131,6 +131,8 @@ def lib():
     L.dts_sws_filter.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_double), i32, vp, vp, i32]
     L.dts_fps_map.argtypes = [i64, i32, i32, i32, i32, vp, i64]
     L.dts_fps_map.restype = i64
+    L.dts_yadif_run_device.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(DevFrames), i32, i32, i32,
+                                       ctypes.POINTER(DevFrames), vp]
     _lib = L
     return L
 
@@ -275,6 +277,10 @@ class Context:
         check(lib().dts_quality_run_device(self.h, w, h, fmt, ctypes.byref(a), ctypes.byref(b), nframes,
                                            ctypes.c_void_p(qraw_ptr), ctypes.c_void_p(stream or 0)),
               "quality_run_device")
+
+    def yadif_device(self, w, h, mode, tff, seq, nseq, first, count, dst, stream=None):
+        check(lib().dts_yadif_run_device(self.h, w, h, mode, tff, ctypes.byref(seq), nseq, first, count,
+                                         ctypes.byref(dst), ctypes.c_void_p(stream or 0)), "yadif_run_device")
 
     def synth_device(self, w, h, fmt, pattern, seed, first, dst, nframes, stream=None):
         check(lib().dts_synth_device(self.h, w, h, fmt, pattern, seed, first, ctypes.byref(dst), nframes,

@@ -19,6 +19,7 @@
  *                          optional `psnr`/`ssim` filters against a reference
  *   dts_quality_*      <- vf_psnr.c do_psnr / vf_ssim.c do_ssim
  *   dts_fps_map        <- vf_fps.c frame selection (round=near)
+ *   dts_yadif_run_device <- `-vf yadif` (vf_yadif.c)
  *   dts_synth_*        <- `-f lavfi testsrc2` (synthetic source; testsrc2 itself
  *                          needs ffmpeg, so this is a deterministic stand-in)
  *
@@ -201,6 +202,17 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes,
 int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt,
                            const dts_dev_frames *a, const dts_dev_frames *b,
                            int nframes, dts_qraw *qraw_dev, void *stream);
+/* vf_yadif (FFmpeg 4.4, 8-bit yuv420p) on a device-resident sequence of nseq
+ * frames: outputs are made for frames first .. first+count-1, each with
+ * prev = frame i-1 and next = frame i+1 clamped to the sequence (yadif's
+ * clone of the first / last frame).  mode 0 send_frame, 1 send_field (2 outputs
+ * per frame: first then second field), 2 / 3 the same without the spatial
+ * interlacing check; tff 1 = top field first (yadif parity auto on progressive-
+ * flagged input), 0 = bottom first.  dst holds count (x2 for field modes)
+ * frames.  Replaces `-vf yadif=mode:parity` (vf_yadif.c filter_slice). */
+int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames *seq, int nseq,
+                         int first, int count, const dts_dev_frames *dst, void *stream);
+
 /* vf_psnr get_psnr / vf_ssim ssim_db finishing of raw records (host). */
 int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out);
 

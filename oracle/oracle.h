@@ -96,6 +96,13 @@ int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_
                          int dstFmt, uint8_t *const dst[3], const int64_t dst_pitch[3],
                          int mode, double param, double desat, double peak, double npl);
 double orc_tonemap_param(int mode, double param);
+
+/* vf_yadif (vf_yadif_ref.c) on one 8-bit yuv420p frame: prev/cur/next planes
+ * share pitch[]; mode 0..3 (send_frame, send_field, *_nospatial); tff = field
+ * order; is_second = second field of send_field modes.  Returns 0 or <0. */
+int orc_yadif_frame(int w, int h, const uint8_t *const prev[3], const uint8_t *const cur[3],
+                    const uint8_t *const next[3], const int64_t pitch[3], uint8_t *const dst[3],
+                    const int64_t dpitch[3], int mode, int tff, int is_second);
 void orc_bt2020_to_bt709(double m[3][3]);
 
 #ifdef __cplusplus

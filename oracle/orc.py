@@ -48,6 +48,8 @@ def lib():
         L.orc_tonemap_param.argtypes = [i32, d]
         L.orc_tonemap_param.restype = d
         L.orc_bt2020_to_bt709.argtypes = [ctypes.POINTER(d * 3)]
+        L.orc_yadif_frame.argtypes = [i32, i32, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                      ctypes.POINTER(i64), ctypes.POINTER(vp), ctypes.POINTER(i64), i32, i32, i32]
         _lib = L
     return _lib
 
@@ -145,3 +147,17 @@ def bt2020_to_bt709():
     m = ((ctypes.c_double * 3) * 3)()
     lib().orc_bt2020_to_bt709(m)
     return np.array([[m[i][j] for j in range(3)] for i in range(3)])
+
+
+def yadif_frame(prev, cur, nxt, w, h, mode=0, tff=1, is_second=0):
+    """vf_yadif on one yuv420p frame (planes of prev/cur/next must share pitches)."""
+    pd, pp = _ptrs(prev)
+    cd, cp = _ptrs(cur)
+    nd, np_ = _ptrs(nxt)
+    assert list(pp) == list(cp) == list(np_), "prev/cur/next must share plane pitches"
+    dst = _alloc(w, h, 0)
+    dd, dp = _ptrs(dst)
+    r = lib().orc_yadif_frame(w, h, pd, cd, nd, cp, dd, dp, mode, tff, is_second)
+    if r != 0:
+        raise RuntimeError(f"orc_yadif_frame failed ({r})")
+    return dst

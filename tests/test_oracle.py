@@ -110,3 +110,20 @@ def test_fps_map_properties():
     m = orc.fps_map(1001, (24000, 1001), (30, 1))
     assert len(m) == (1001 * 1001 * 30 + 12000) // 24000 and m[0] == 0 and np.all(np.diff(m) >= 0)
     assert m[-1] == 1000
+
+
+def test_yadif_oracle_properties():
+    """vf_yadif known answers: the kept field is copied; a static picture (prev =
+    cur = next) whose odd rows equal their even neighbours is reproduced; a
+    vertically constant plane stays constant."""
+    import dtsffi as D
+    w, h = 48, 20
+    f = D.synth_host(w, h, D.FMT_YUV420P, 0, 3, 0)
+    o = orc.yadif_frame(f, f, f, w, h, 0, 1, 0)
+    assert np.array_equal(o[0][0::2], f[0][0::2])           # tff, first field: even rows kept
+    o2 = orc.yadif_frame(f, f, f, w, h, 1, 1, 1)
+    assert np.array_equal(o2[0][1::2], f[0][1::2])          # second field: odd rows kept
+    c = [np.tile(np.arange(p.shape[1], dtype=np.uint8)[None, :] * 3, (p.shape[0], 1)) for p in f]
+    for mode in range(4):
+        oc = orc.yadif_frame(c, c, c, w, h, mode, 1, 0)
+        assert all(np.array_equal(a, b) for a, b in zip(oc, c))
