@@ -190,6 +190,29 @@ def load_traffic():
         return None, None
 
 
+def segment_base(rank):
+    """First synthetic frame index of this rank's segments: ranks own disjoint
+    segments of the source (weak scaling, no data exchange)."""
+    return rank * 1_000_000
+
+
+def gather_records(frames, checksum, wall, world, dev):
+    """The only collectives of the path: all-gather of the per-rank segment
+    records (frames, output checksum) and the max-reduce of the wall time.
+    Works on any backend (RCCL on the GPU box, gloo in the CPU tests).
+    Returns (total frames, max wall seconds, [(frames, checksum) per rank])."""
+    rec = torch.tensor([float(frames), float(checksum)], dtype=torch.float64, device=dev)
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        gathered = [torch.zeros_like(rec) for _ in range(world)]
+        dist.all_gather(gathered, rec)
+    else:
+        gathered = [rec]
+    records = [(int(r[0].item()), int(r[1].item())) for r in gathered]
+    return sum(r[0] for r in records), float(wall_t.item()), records
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,7 +256,7 @@ def main():
     sfb = frame_bytes(sw, sh, sfmt)
     src = torch.empty((R, sfb), dtype=torch.uint8, device=dev)
     sd, _ = dev_batch(src, sw, sh, sfmt)
-    first = rank * 1_000_000
+    first = segment_base(rank)
     ctx.synth_device(sw, sh, sfmt, 0, 0x5EED, first, sd, R, sptr)
     outs, ods = [], []
     for (w, h, fmt, _m) in wl["outs"]:
@@ -284,17 +307,8 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
     # segment records: frames + an output checksum per rank, gathered over RCCL
-    rec = torch.tensor([float(args.steps * B), float(sum(int(o.sum().item()) for o in outs) % (1 << 40))],
-                       dtype=torch.float64, device=dev)
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        gathered = [torch.zeros_like(rec) for _ in range(world)]
-        dist.all_gather(gathered, rec)
-        frames_total = sum(int(r[0].item()) for r in gathered)
-    else:
-        frames_total = int(rec[0].item())
-    wall_max = float(wall_t.item())
+    checksum = sum(int(o.sum().item()) for o in outs) % (1 << 40)
+    frames_total, wall_max, _records = gather_records(args.steps * B, checksum, wall, world, dev)
 
     verified = None
     if rank == 0 and not args.no_verify:

@@ -36,7 +36,7 @@
 #endif
 
 #ifndef DTS_L4_ABLATE
-#define DTS_L4_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads
+#define DTS_L4_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads, 8 skip V stores
 #endif
 
 namespace dts {
@@ -341,7 +341,9 @@ __device__ __forceinline__ void vpass(const Item &I, int b)
                              I.d16 ? 1 << 16 : vinit<SRC>(y, I.dlo, I.dhi));
         const int a1 = vtaps(I.rl, I.R, uni(vsl[i1]), ng, vco + i1 * I.nvp,
                              I.d16 ? 1 << 16 : vinit<SRC>(y2, I.dlo, I.dhi));
-        if (I.vact) {
+        if (DTS_L4_ABLATE & 8) {                                   // diagnostic: keep V, drop its stores
+            asm volatile("" ::"v"(a0), "v"(a1));
+        } else if (I.vact) {
             if (I.d16) {
                 vstore16(I.obase + (int64_t)y * I.opitch, a0);
                 if (y + 4 < vhi) vstore16(I.obase + (int64_t)y2 * I.opitch, a1);
