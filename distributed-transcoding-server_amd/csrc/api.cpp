@@ -162,6 +162,7 @@ struct dts_graph {
     hipEvent_t hdr_ev[2] = {nullptr, nullptr};
     unsigned hdr_next = 0;
     TonemapParams tm{};
+    float *dev_tm_lut = nullptr;          // the transfer-curve tables of tm (TonemapParams::lut)
 };
 
 // ---------------------------------------------------------------------------
@@ -247,6 +248,24 @@ TonemapParams tonemap_params(const dts_tonemap_spec &t)
     p.scale = (float)(10000.0 / npl);
     bt2020_to_bt709(p.m);
     return p;
+}
+
+// [0..N]: SMPTE ST 2084 EOTF x 10000 / npl (zscale t=linear:npl), [N+1..2N+1]: BT.709
+// OETF (zimg rec_709_oetf), sampled in double at i / N on [0, 1]
+std::vector<float> tonemap_luts(const dts_tonemap_spec &t)
+{
+    const double m1 = 2610.0 / 16384.0, m2 = 2523.0 / 4096.0 * 128.0;
+    const double c1 = 3424.0 / 4096.0, c2 = 2413.0 / 4096.0 * 32.0, c3 = 2392.0 / 4096.0 * 32.0;
+    const double alpha = 1.09929682680944, beta = 0.018053968510807;
+    const double scale = 10000.0 / (t.npl > 0 ? t.npl : 100.0);
+    std::vector<float> v(2 * (kTmLutN + 1));
+    for (int i = 0; i <= kTmLutN; ++i) {
+        const double x = (double)i / kTmLutN;
+        const double p = std::pow(x, 1.0 / m2);
+        v[i] = (float)(std::pow(std::max(p - c1, 0.0) / (c2 - c3 * p), 1.0 / m1) * scale);
+        v[kTmLutN + 1 + i] = (float)(x < beta ? 4.5 * x : alpha * std::pow(x, 0.45) - (alpha - 1.0));
+    }
+    return v;
 }
 
 struct KindTables {
@@ -703,6 +722,14 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
                 }
                 if (!e && hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
             }
+            if (!e) {
+                const std::vector<float> luts = tonemap_luts(s.tonemap);
+                const size_t nb = luts.size() * sizeof(float);
+                if (hipMalloc(&g->dev_tm_lut, nb) != hipSuccess ||
+                    hipMemcpy(g->dev_tm_lut, luts.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
+                    e = DTS_E_HIP;
+                g->tm.lut = g->dev_tm_lut;
+            }
             if (e) {
                 ctx->last_hip = (int)hipGetLastError();
                 dts_graph_destroy(g);
@@ -763,6 +790,7 @@ void dts_graph_destroy(dts_graph *g)
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             if (g->hdr_mid[sl][k]) hipFree(g->hdr_mid[sl][k]);
     }
+    if (g->dev_tm_lut) hipFree(g->dev_tm_lut);
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_queue) hipFree(g->dev_queue);

@@ -153,6 +153,8 @@ struct QualityParams {
 // ---------------------------------------------------------------------------
 // HDR10 -> SDR (hdr.hip)
 // ---------------------------------------------------------------------------
+constexpr int kTmLutN = 1024;      // intervals of the PQ EOTF / BT.709 OETF tables
+constexpr int kTmRows = 16;        // 2x2-block rows per k_tonemap workgroup
 struct TonemapParams {
     DevPlanes src;                  // p010 at the output size (ladder intermediate)
     DevPlanes dst;                  // 8-bit yuv420p / nv12
@@ -160,6 +162,7 @@ struct TonemapParams {
     int32_t mode;                   // DTS_TM_*
     float param, desat, peak, hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
+    const float *lut;               // device [2][kTmLutN + 1]: PQ EOTF x 10000 / npl, then BT.709 OETF
 };
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);
 
