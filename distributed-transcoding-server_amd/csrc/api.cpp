@@ -1042,6 +1042,7 @@ int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dt
     p.nseq = nseq;
     p.mode = mode;
     p.tff = tff ? 1 : 0;
+    p.aligned = planes_ok(*seq, w, h, DTS_FMT_YUV420P, 4) && planes_ok(*dst, w, h, DTS_FMT_YUV420P, 4);
     const int chunk = 32768;                              // outputs per launch (grid z)
     for (int j0 = 0; j0 < count; j0 += chunk) {
         const int n = std::min(chunk, count - j0);

@@ -174,6 +174,7 @@ struct YadifParams {
     DevPlanes dst;                  // output frames of this launch
     int32_t w, h, nseq, first;      // outputs come from frames first, first + 1, ...
     int32_t mode, tff;              // yadif mode 0..3, field order
+    int32_t aligned;                // every plane base / pitch of seq and dst is a multiple of 4
 };
 hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s);
 
