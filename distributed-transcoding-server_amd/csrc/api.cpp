@@ -33,6 +33,14 @@ namespace {
 
 constexpr int kSwsAccurateRnd = 0x40000;
 constexpr int kQueueSlots = 64;
+constexpr int kQueueWidth = 8;            // counters per slot: one per XCD for k_ladder4
+
+// k_ladder4 work queues: one per XCD unless DTS_XCD=0 (A/B runs)
+int ladder4_queues()
+{
+    const char *f = std::getenv("DTS_XCD");
+    return (f && f[0] == '0') ? 1 : kQueueWidth;
+}
 constexpr int kSwsBitexact = 0x80000;
 
 #define HIPCHK(ctx, expr)                                  \
@@ -701,7 +709,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         hipSetDevice(ctx->device);
         e = upload_v3(g, gp.kts);
         if (!e && gp.v4_mask) e = upload_v4(g, gp);
-        if (!e && hipMalloc(&g->dev_queue, kQueueSlots * sizeof(unsigned int)) != hipSuccess) {
+        if (!e && hipMalloc(&g->dev_queue, kQueueSlots * kQueueWidth * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
             e = DTS_E_HIP;
         }
@@ -930,12 +938,16 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.nitems = n * g->njobs4;
             q.jobs = g->dev_jobs4;
             q.rk = g->dev_rk4;
-            q.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
-            HIPCHK(ctx, hipMemsetAsync(q.queue, 0, sizeof(unsigned int), st));
-            HIPCHK(ctx, launch_ladder4(q, g->lds4, std::min(q.nitems, g->grid4), st));
+            q.nq = n >= 64 ? ladder4_queues() : 1;               // small batches keep one queue (all XCDs busy)
+            q.queue = g->dev_queue + kQueueWidth * (g->queue_next++ % kQueueSlots);
+            HIPCHK(ctx, hipMemsetAsync(q.queue, 0, kQueueWidth * sizeof(unsigned int), st));
+            // every queue needs workgroups: a multiple of nq, at least nq
+            int grid = std::min(q.nitems, g->grid4);
+            grid = std::max(q.nq, (grid + q.nq - 1) / q.nq * q.nq);
+            HIPCHK(ctx, launch_ladder4(q, g->lds4, grid, st));
         }
         if (p.njobs) {
-            pp.queue = g->dev_queue + (g->queue_next++ % kQueueSlots);
+            pp.queue = g->dev_queue + kQueueWidth * (g->queue_next++ % kQueueSlots);
             HIPCHK(ctx, hipMemsetAsync(pp.queue, 0, sizeof(unsigned int), st));
             HIPCHK(ctx, launch_ladder(pp, g->ndmax, g->lds_bytes, std::min(pp.nitems, g->grid_cap), st));
         }

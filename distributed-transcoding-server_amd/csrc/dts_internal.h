@@ -123,10 +123,11 @@ struct Ladder4Params {
     DevPlanes src;
     DevPlanes dst[kMaxRungs];
     int32_t dst_fmt[kMaxRungs];
-    int32_t srcH, chrH, ring, src_kind, njobs, nitems, nframes, pad_;
+    int32_t srcH, chrH, ring, src_kind, njobs, nitems, nframes;
+    int32_t nq;                     // work queues (1, or 8 = one per XCD; frame f in queue f % nq)
     const Job4 *jobs;
     const RungKind4 *rk;
-    unsigned int *queue;
+    unsigned int *queue;            // nq counters
 };
 
 hipError_t launch_ladder4(const Ladder4Params &p, int lds_bytes, int grid, hipStream_t s);

@@ -534,12 +534,18 @@ __global__ void __launch_bounds__(kThreads, DTS_L4_WAVES) k_ladder4(const Ladder
     extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
     volatile int *slot = reinterpret_cast<volatile int *>(ring);   // ring dword 0: idle between items
     for (;;) {
-        if (threadIdx.x == 0) *slot = (int)atomicAdd(P.queue, 1u);
+        // nq > 1: one queue per XCD (workgroups are dispatched round-robin over the
+        // XCDs), holding the frames f = x (mod nq), so every strip of a frame -- and
+        // the source rows its renditions and halos re-read -- stays in one XCD's L2
+        const int x = P.nq > 1 ? (int)(blockIdx.x % (unsigned)P.nq) : 0;
+        if (threadIdx.x == 0) *slot = (int)atomicAdd(P.queue + x, 1u);
         __syncthreads();
         const int item = uni(*slot);
         __syncthreads();
-        if (item >= P.nitems) return;
-        const int frame = item / P.njobs, jid = item - frame * P.njobs;
+        const int nf = (P.nframes - x + P.nq - 1) / P.nq;          // frames of this queue
+        if (item >= nf * P.njobs) return;
+        const int fq = item / P.njobs, jid = item - fq * P.njobs;
+        const int frame = x + P.nq * fq;
         const Job4 J = kload(P.jobs + jid);
         if (kLumaCvt == kChromaCvt || J.kind == 0)
             item4<SRC, kLumaCvt>(P, frame, J, ring);

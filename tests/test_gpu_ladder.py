@@ -120,13 +120,13 @@ def test_many_frames_batches(ctx):
         assert planes_equal(got[f][0], want), first_diff(got[f][0], want)
 
 
-def test_device_path_matches_host_path(ctx):
-    """dts_graph_run_device on torch-allocated HBM == the host path."""
+@pytest.mark.parametrize("n,w,h", [(5, 640, 360), (77, 192, 108)])
+def test_device_path_matches_host_path(ctx, n, w, h):
+    """dts_graph_run_device on torch-allocated HBM == the oracle.  77 frames
+    (>= 64) exercise the per-XCD work queues (frame f in queue f % 8)."""
     import torch
-    w, h = 640, 360
-    outs = [(320, 180, D.FMT_NV12, BIC), (216, 120, D.FMT_NV12, BIC)]
+    outs = [(w // 2, h // 2, D.FMT_NV12, BIC), ((w // 3 + 3) // 4 * 4, h // 3, D.FMT_NV12, BIC)]
     g = D.Graph(ctx, D.make_spec(w, h, D.FMT_YUV420P, outs))
-    n = 5
     src = torch.empty((n, h * w + 2 * ((w + 1) // 2) * ((h + 1) // 2) + 64), dtype=torch.uint8, device="cuda")
     fstride = src.stride(0)
     assert fstride % 16 == 0
@@ -136,7 +136,7 @@ def test_device_path_matches_host_path(ctx):
     sf.data[0], sf.data[1], sf.data[2] = base, base + h * w, base + h * w + cw * ch
     sf.pitch[0], sf.pitch[1], sf.pitch[2] = w, cw, cw
     sf.frame_stride = fstride
-    # cw = 320 and plane offsets are multiples of 16 for this geometry
+    # plane offsets and pitches are multiples of 16 for these geometries
     ctx.synth_device(w, h, D.FMT_YUV420P, 0, 42, 0, sf, n, torch.cuda.current_stream().cuda_stream)
     dsts, bufs = [], []
     for (ow, oh, of, _m) in outs:
