@@ -253,13 +253,15 @@ TonemapParams tonemap_params(const dts_tonemap_spec &t)
     p.desat = (float)t.desat;
     p.peak = (float)peak;
     p.hpeak = (float)hable((float)peak);
+    p.inv_hpeak = 1.0f / p.hpeak;
     p.scale = (float)(10000.0 / npl);
     bt2020_to_bt709(p.m);
     return p;
 }
 
 // [0..N]: SMPTE ST 2084 EOTF x 10000 / npl (zscale t=linear:npl), [N+1..2N+1]: BT.709
-// OETF (zimg rec_709_oetf), sampled in double at i / N on [0, 1]
+// OETF (zimg rec_709_oetf), sampled in double at i / N on [0, 1]; each entry is
+// (value, slope to the next entry), the last one (value, 0)
 std::vector<float> tonemap_luts(const dts_tonemap_spec &t)
 {
     const double m1 = 2610.0 / 16384.0, m2 = 2523.0 / 4096.0 * 128.0;
@@ -273,7 +275,14 @@ std::vector<float> tonemap_luts(const dts_tonemap_spec &t)
         v[i] = (float)(std::pow(std::max(p - c1, 0.0) / (c2 - c3 * p), 1.0 / m1) * scale);
         v[kTmLutN + 1 + i] = (float)(x < beta ? 4.5 * x : alpha * std::pow(x, 0.45) - (alpha - 1.0));
     }
-    return v;
+    std::vector<float> o(4 * (kTmLutN + 1));
+    for (int c = 0; c < 2; ++c)
+        for (int i = 0; i <= kTmLutN; ++i) {
+            const float *t = v.data() + c * (kTmLutN + 1);
+            o[2 * (c * (kTmLutN + 1) + i)] = t[i];
+            o[2 * (c * (kTmLutN + 1) + i) + 1] = i < kTmLutN ? t[i + 1] - t[i] : 0.0f;
+        }
+    return o;
 }
 
 struct KindTables {
@@ -736,7 +745,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
                 if (hipMalloc(&g->dev_tm_lut, nb) != hipSuccess ||
                     hipMemcpy(g->dev_tm_lut, luts.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
                     e = DTS_E_HIP;
-                g->tm.lut = g->dev_tm_lut;
+                g->tm.lut = reinterpret_cast<const float2 *>(g->dev_tm_lut);
             }
             if (e) {
                 ctx->last_hip = (int)hipGetLastError();

@@ -161,9 +161,9 @@ struct TonemapParams {
     DevPlanes dst;                  // 8-bit yuv420p / nv12
     int32_t dst_fmt, w, h, nframes; // w, h even; nframes <= 65535
     int32_t mode;                   // DTS_TM_*
-    float param, desat, peak, hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
+    float param, desat, peak, hpeak, inv_hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
-    const float *lut;               // device [2][kTmLutN + 1]: PQ EOTF x 10000 / npl, then BT.709 OETF
+    const float2 *lut;              // device [2][kTmLutN + 1] (value, slope): PQ EOTF x 10000 / npl, BT.709 OETF
 };
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);
 

@@ -31,19 +31,22 @@ __device__ __forceinline__ float pw(float x, float y)
 
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 
-// table t[0..kTmLutN] of a curve on [0, 1], linearly interpolated
-__device__ __forceinline__ float lut(const float *t, float v)
+// table t[0..kTmLutN] of (value, slope to the next entry) of a curve on [0, 1],
+// linearly interpolated: clamp (v_med3), scale, truncate, one 8-byte LDS read, fma
+__device__ __forceinline__ float lut(const float2 *t, float v)
 {
-    const float x = clamp01(v) * (float)kTmLutN;
-    const int i = min((int)x, kTmLutN - 1);
-    const float f = x - (float)i;
-    return t[i] + f * (t[i + 1] - t[i]);
+    const float x = __builtin_amdgcn_fmed3f(v, 0.f, 1.f) * (float)kTmLutN;
+    const int i = (int)x;
+    const float2 e = t[i];
+    return __builtin_fmaf(x - (float)i, e.y, e.x);
 }
+
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 __device__ __forceinline__ float hable(float in)
 {
     const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
-    return (in * (in * a + b * c) + d * e) / (in * (in * a + b) + d * f) - e / f;
+    return (in * (in * a + b * c) + d * e) * rcp(in * (in * a + b) + d * f) - e / f;
 }
 
 __device__ __forceinline__ float mobius(float in, float j, float peak)
@@ -61,10 +64,10 @@ __device__ __forceinline__ int q8(float v)
 }
 
 // One pixel: 10-bit Y, chroma (Cb', Cr' already centred) -> bt709 Y' / Cb' / Cr'
-__device__ __forceinline__ void pixel(const TonemapParams &P, const float *tl, int y10, float cb, float cr, float &Y,
+__device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, int y10, float cb, float cr, float &Y,
                                       float &Cb, float &Cr)
 {
-    const float *pq = tl, *oetf = tl + kTmLutN + 1;           // pq already scaled by 10000 / npl
+    const float2 *pq = tl, *oetf = tl + kTmLutN + 1;          // pq already scaled by 10000 / npl
     constexpr float kr2 = 0.2627f, kb2 = 0.0593f, kg2 = 1.f - kr2 - kb2;
     constexpr float kr7 = 0.2126f, kb7 = 0.0722f, kg7 = 1.f - kr7 - kb7;
     const float yy = (float)(y10 - 64) * (1.f / 876.f);
@@ -91,11 +94,11 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float *tl, i
         break;
     case DTS_TM_CLIP: sig = fminf(fmaxf(sig * P.param, 0.f), 1.f); break;
     case DTS_TM_REINHARD: sig = sig / (sig + P.param) * (P.peak + P.param) / P.peak; break;
-    case DTS_TM_HABLE: sig = hable(sig) / P.hpeak; break;
+    case DTS_TM_HABLE: sig = hable(sig) * P.inv_hpeak; break;
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
-    const float k = sig / sig0;
+    const float k = sig * rcp(sig0);
     r = lut(oetf, r * k);
     g = lut(oetf, g * k);
     b = lut(oetf, b * k);
@@ -108,7 +111,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float *tl, i
 
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
-    __shared__ float tl[2 * (kTmLutN + 1)];
+    __shared__ float2 tl[2 * (kTmLutN + 1)];
     for (int i = threadIdx.x; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
     __syncthreads();
     const int bx = blockIdx.x * 64 + (threadIdx.x & 63);
