@@ -498,14 +498,15 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     // Strips in source-column order: every rendition and plane of a column range
     // together, so the items a queue hands out back to back walk the same source rows
     // and re-read them from L2 (r01: +3 % over heaviest-first at 256 frames per launch).
-    // DTS_ORDER=h restores heaviest-first (H tap pairs x columns x source rows), which
-    // shortens the tail of launches with few frames.
+    // A single rendition keeps heaviest-first (H tap pairs x columns x source rows),
+    // which shortens the launch tail (cfg4: 26.1k vs 25.0k fps); DTS_ORDER=h / c force one.
     auto cost4 = [&](const Job4 &j) {
         return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH;
     };
     std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(), [&](const Job4 &a, const Job4 &b) { return cost4(a) > cost4(b); });
     const char *order = std::getenv("DTS_ORDER");
-    if (!(order && order[0] == 'h')) {
+    const bool by_column = order ? order[0] == 'c' : s.nout > 1;   // one rendition: no source re-reads to share
+    if (by_column) {
         auto srcx = [&](const Job4 &j) { return (double)(j.x0 + 0.5 * j.ncols) / gp.kts[j.rk].dstW; };
         std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(),
                          [&](const Job4 &a, const Job4 &b) { return srcx(a) < srcx(b); });
