@@ -666,6 +666,7 @@ static int upload_v4(dts_graph *g, const GraphPlan &gp)
         const Plan4 &pl = gp.p4[i];
         offs[i].groups = push_blob(blob, pl.groups);
         offs[i].hcoef = push_blob(blob, pl.hcoef);
+        blob.resize(blob.size() + 16 * sizeof(uint32_t), 0);  // k_ladder4 prefetches one output's taps past the last
         offs[i].vslot = push_blob(blob, pl.vslot);
         offs[i].vcoef = push_blob(blob, pl.vcoef);
         offs[i].vlim = push_blob(blob, pl.vlim);

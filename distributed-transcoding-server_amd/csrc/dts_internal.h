@@ -155,7 +155,10 @@ struct QualityParams {
 // HDR10 -> SDR (hdr.hip)
 // ---------------------------------------------------------------------------
 constexpr int kTmLutN = 1024;      // intervals of the PQ EOTF / BT.709 OETF tables
-constexpr int kTmRows = 16;        // 2x2-block rows per k_tonemap workgroup
+#ifndef DTS_TM_ROWS
+#define DTS_TM_ROWS 64
+#endif
+constexpr int kTmRows = DTS_TM_ROWS; // 2x2-block rows per k_tonemap workgroup
 struct TonemapParams {
     DevPlanes src;                  // p010 at the output size (ladder intermediate)
     DevPlanes dst;                  // 8-bit yuv420p / nv12

@@ -29,8 +29,6 @@ __device__ __forceinline__ float pw(float x, float y)
     return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 }
 
-__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
-
 // table t[0..kTmLutN] of (value, slope to the next entry) of a curve on [0, 1],
 // linearly interpolated: clamp (v_med3), scale, truncate, one 8-byte LDS read, fma
 __device__ __forceinline__ float lut(const float2 *t, float v)

@@ -31,6 +31,14 @@
 #define DTS_L4_HSMEM 1      // H taps: 1 = scalar loads (s_load) from the global table, 0 = LDS broadcast reads (r01v5)
 #endif
 
+#ifndef DTS_L4_HPF
+#define DTS_L4_HPF 0        // 1: prefetch the next output's H taps (r01v10: -2 % cfg2, the extra SGPRs spill)
+#endif
+
+#ifndef DTS_L4_V2
+#define DTS_L4_V2 1         // V: both rows of an iteration share one tap-group loop (LDS reads issued together)
+#endif
+
 #ifndef DTS_L4_VSMEM
 #define DTS_L4_VSMEM 0      // 1: V taps / ring slots read with scalar loads from the global tables (no LDS staging)
 #endif
@@ -162,6 +170,11 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
     }
 #if DTS_L4_HSMEM
     k_u32 *cg = GP(k_u32, cl);
+#if DTS_L4_HPF
+    uint32_t cn[NP];                                 // the next output's taps (the table is padded by 16 dwords)
+#pragma unroll
+    for (int i = 0; i < NP; ++i) cn[i] = cg[i];
+#endif
 #else
     const uint4 *cv = reinterpret_cast<const uint4 *>(cl);
 #endif
@@ -179,7 +192,14 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
                 if (pn % PPL == PPL - 1) load_chunk(ra, rb, nw, pn / PPL, z);
                 if ((uint32_t)(mask >> q) & 1u) {
                     uint32_t c[NP];
-#if DTS_L4_HSMEM
+#if DTS_L4_HSMEM && DTS_L4_HPF
+                    cg += NP;
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        c[i] = cn[i];
+                        cn[i] = cg[i];
+                    }
+#elif DTS_L4_HSMEM
 #pragma unroll
                     for (int i = 0; i < NP; ++i) c[i] = cg[i];
                     cg += NP;
@@ -272,6 +292,36 @@ __device__ __forceinline__ int vtaps(const uint32_t *rl, int R, int s0, int ng, 
     return acc;
 }
 
+// Two output rows of one lane at once (slots s0, s1, tap rows cq0, cq1): the
+// LDS reads of both rows' groups issue together, so one LDS round trip serves
+// both accumulators.  Each accumulator sums in vtaps' order (bit-identical).
+__device__ __forceinline__ void vtaps2(const uint32_t *rl, int R, int s0, int s1, int ng, const uint32_t *cq0,
+                                       const uint32_t *cq1, int &acc0, int &acc1)
+{
+#if DTS_L4_V2 && !DTS_L4_VSMEM
+    if (s0 + 4 * ng <= R && s1 + 4 * ng <= R) {
+        const uint32_t *p = rl + s0 * kCP, *q = rl + s1 * kCP;
+        const uint4 *c0 = reinterpret_cast<const uint4 *>(cq0), *c1 = reinterpret_cast<const uint4 *>(cq1);
+        for (int g = 0; g < ng; ++g, p += 4 * kCP, q += 4 * kCP) {
+            const uint4 a = c0[g], b = c1[g];
+            const uint32_t p0 = p[0], p1 = p[kCP], p2 = p[2 * kCP], p3 = p[3 * kCP];
+            const uint32_t q0 = q[0], q1 = q[kCP], q2 = q[2 * kCP], q3 = q[3 * kCP];
+            acc0 = dot2(p0, a.x, acc0);
+            acc1 = dot2(q0, b.x, acc1);
+            acc0 = dot2(p1, a.y, acc0);
+            acc1 = dot2(q1, b.y, acc1);
+            acc0 = dot2(p2, a.z, acc0);
+            acc1 = dot2(q2, b.z, acc1);
+            acc0 = dot2(p3, a.w, acc0);
+            acc1 = dot2(q3, b.w, acc1);
+        }
+        return;
+    }
+#endif
+    acc0 = vtaps(rl, R, s0, ng, cq0, acc0);
+    acc1 = vtaps(rl, R, s1, ng, cq1, acc1);
+}
+
 // yuv2planeX_8 / yuv2nv12cX accumulator start for output row y: the dither
 // (flat 64 for 8-bit sources, this lane's ff_dither_8x8_128 column, packed in
 // dlo/dhi, for >8-bit sources) << 12
@@ -337,10 +387,10 @@ __device__ __forceinline__ void vpass(const Item &I, int b)
     for (int y = vlo + I.wave; y < vhi; y += 8) {
         const int y2 = min(y + 4, vhi - 1);
         const int i0 = y - vlo, i1 = y2 - vlo;
-        const int a0 = vtaps(I.rl, I.R, uni(vsl[i0]), ng, vco + i0 * I.nvp,
-                             I.d16 ? 1 << 16 : vinit<SRC>(y, I.dlo, I.dhi));
-        const int a1 = vtaps(I.rl, I.R, uni(vsl[i1]), ng, vco + i1 * I.nvp,
-                             I.d16 ? 1 << 16 : vinit<SRC>(y2, I.dlo, I.dhi));
+        const int s0 = uni(vsl[i0]), s1 = uni(vsl[i1]);
+        int a0 = I.d16 ? 1 << 16 : vinit<SRC>(y, I.dlo, I.dhi);
+        int a1 = I.d16 ? 1 << 16 : vinit<SRC>(y2, I.dlo, I.dhi);
+        vtaps2(I.rl, I.R, s0, s1, ng, vco + i0 * I.nvp, vco + i1 * I.nvp, a0, a1);
         if (DTS_L4_ABLATE & 8) {                                   // diagnostic: keep V, drop its stores
             asm volatile("" ::"v"(a0), "v"(a1));
         } else if (I.vact) {
