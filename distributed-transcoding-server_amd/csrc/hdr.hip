@@ -30,13 +30,12 @@ __device__ __forceinline__ float pw(float x, float y)
 }
 
 // table t[0..kTmLutN] of (value, slope to the next entry) of a curve on [0, 1],
-// linearly interpolated: clamp (v_med3), scale, truncate, one 8-byte LDS read, fma
+// linearly interpolated: clamp (v_med3), scale, truncate / fract, one 8-byte LDS read, fma
 __device__ __forceinline__ float lut(const float2 *t, float v)
 {
     const float x = __builtin_amdgcn_fmed3f(v, 0.f, 1.f) * (float)kTmLutN;
-    const int i = (int)x;
-    const float2 e = t[i];
-    return __builtin_fmaf(x - (float)i, e.y, e.x);
+    const float2 e = t[(int)x];
+    return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
 }
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -57,8 +56,8 @@ __device__ __forceinline__ float mobius(float in, float j, float peak)
 
 __device__ __forceinline__ int q8(float v)
 {
-    const float r = floorf(v + 0.5f);
-    return (int)fminf(fmaxf(r, 0.f), 255.f);
+    // floor(v + 0.5) clipped to [0, 255]: after the clip the value is >= 0, so truncation is the floor
+    return (int)__builtin_amdgcn_fmed3f(v + 0.5f, 0.f, 255.f);
 }
 
 // One pixel: 10-bit Y, chroma (Cb', Cr' already centred) -> bt709 Y' / Cb' / Cr'
