@@ -190,7 +190,7 @@ __device__ __forceinline__ void hpass(uint32_t (&ra)[32], uint32_t (&rb)[32], ui
                 pa[pn] = pair_at<CVT>(ra, pn, sel, z);
                 pb[pn] = pair_at<CVT>(rb, pn, sel, z);
                 if (pn % PPL == PPL - 1) load_chunk(ra, rb, nw, pn / PPL, z);
-                if ((uint32_t)(mask >> q) & 1u) {
+                if ((((q < 32) ? (uint32_t)mask : (uint32_t)(mask >> 32)) >> (q & 31)) & 1u) {
                     uint32_t c[NP];
 #if DTS_L4_HSMEM && DTS_L4_HPF
                     cg += NP;
