@@ -69,11 +69,28 @@ static void finalize_ctx(napi_env env, void *data, void *hint)
     dts_ctx_destroy((dts_ctx *)data);
 }
 
+/* A graph external: the libdts graph plus the spec it was made from (run()
+ * validates every caller frame against it).  libdts reference-counts the
+ * context, so the graph stays valid whichever finalizer runs first. */
+typedef struct {
+    dts_graph *g;
+    dts_graph_spec spec;
+} graph_box;
+
 static void finalize_graph(napi_env env, void *data, void *hint)
 {
     (void)env;
     (void)hint;
-    dts_graph_destroy((dts_graph *)data);
+    graph_box *b = (graph_box *)data;
+    dts_graph_destroy(b->g);
+    free(b);
+}
+
+static graph_box *get_graph(napi_env env, napi_value v)
+{
+    graph_box *b = NULL;
+    if (napi_get_value_external(env, v, (void **)&b) != napi_ok || !b || !b->g) return NULL;
+    return b;
 }
 
 /* ---- version(), deviceCount() ------------------------------------------ */
@@ -181,11 +198,20 @@ static napi_value js_create_graph(napi_env env, napi_callback_info info)
         return throw_dts(env, DTS_E_INVAL, "createGraph: ctx");
     dts_graph_spec s;
     if (parse_spec(env, argv[1], &s)) return throw_dts(env, DTS_E_INVAL, "createGraph: spec");
-    dts_graph *g = NULL;
-    int e = dts_graph_create(ctx, &s, &g);
-    if (e) return throw_dts(env, e, "dts_graph_create");
+    graph_box *b = (graph_box *)calloc(1, sizeof(graph_box));
+    if (!b) return throw_dts(env, DTS_E_NOMEM, "createGraph");
+    int e = dts_graph_create(ctx, &s, &b->g);
+    if (e) {
+        free(b);
+        return throw_dts(env, e, "dts_graph_create");
+    }
+    b->spec = s;
     napi_value ext;
-    NAPI_OK(env, napi_create_external(env, g, finalize_graph, NULL, &ext));
+    if (napi_create_external(env, b, finalize_graph, NULL, &ext) != napi_ok) {
+        dts_graph_destroy(b->g);
+        free(b);
+        return throw_dts(env, DTS_E_NOMEM, "createGraph: external");
+    }
     return ext;
 }
 
@@ -202,11 +228,10 @@ static napi_value js_graph_info(napi_env env, napi_callback_info info)
     size_t argc = 1;
     napi_value argv[1];
     NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    dts_graph *g = NULL;
-    if (argc < 1 || napi_get_value_external(env, argv[0], (void **)&g) != napi_ok || !g)
-        return throw_dts(env, DTS_E_INVAL, "graphInfo(graph)");
+    graph_box *b = argc >= 1 ? get_graph(env, argv[0]) : NULL;
+    if (!b) return throw_dts(env, DTS_E_INVAL, "graphInfo(graph)");
     dts_graph_info gi;
-    int e = dts_graph_info_get(g, &gi);
+    int e = dts_graph_info_get(b->g, &gi);
     if (e) return throw_dts(env, e, "dts_graph_info_get");
     napi_value o;
     NAPI_OK(env, napi_create_object(env, &o));
@@ -226,11 +251,13 @@ static napi_value js_graph_info(napi_env env, napi_callback_info info)
 }
 
 /* ---- frames ------------------------------------------------------------- */
-/* {data: [Buffer, Buffer, Buffer|null], pitch: [n, n, n]} */
-static int parse_frame(napi_env env, napi_value o, dts_frame *f)
+/* {data: [Buffer, Buffer, Buffer|null], pitch: [n, n, n]}; len[p] = byte
+ * length of plane p's Buffer (0 when it is not a Buffer) */
+static int parse_frame(napi_env env, napi_value o, dts_frame *f, size_t len[3])
 {
     napi_value data, pitch;
     memset(f, 0, sizeof *f);
+    len[0] = len[1] = len[2] = 0;
     if (napi_get_named_property(env, o, "data", &data) != napi_ok ||
         napi_get_named_property(env, o, "pitch", &pitch) != napi_ok)
         return -1;
@@ -240,8 +267,7 @@ static int parse_frame(napi_env env, napi_value o, dts_frame *f)
         if (napi_get_element(env, data, p, &b) != napi_ok) return -1;
         napi_is_buffer(env, b, &isbuf);
         if (isbuf) {
-            size_t len = 0;
-            if (napi_get_buffer_info(env, b, &f->data[p], &len) != napi_ok) return -1;
+            if (napi_get_buffer_info(env, b, &f->data[p], &len[p]) != napi_ok) return -1;
         } else {
             f->data[p] = NULL;
         }
@@ -255,15 +281,36 @@ static int parse_frame(napi_env env, napi_value o, dts_frame *f)
     return 0;
 }
 
-static int parse_frames(napi_env env, napi_value arr, dts_frame **out, uint32_t *n)
+/* Every plane the format declares is a Buffer whose pitch covers a row and
+ * whose length covers pitch * (rows - 1) + row bytes (libdts reads and
+ * writes exactly that much through the caller's pointers). */
+static int frame_fits(const dts_frame *f, const size_t len[3], int w, int h, int fmt)
 {
+    int64_t rowb[3], rows[3];
+    if (dts_frame_layout(w, h, fmt, rowb, rows, NULL)) return 0;
+    for (int p = 0; p < 3; ++p) {
+        if (!rowb[p]) continue;
+        if (!f->data[p] || f->pitch[p] < rowb[p]) return 0;
+        if ((uint64_t)len[p] < (uint64_t)(f->pitch[p] * (rows[p] - 1) + rowb[p])) return 0;
+    }
+    return 1;
+}
+
+/* frames i of arr must each fit geometry (w[i % nw], h[i % nw], fmt[i % nw]) */
+static int parse_frames(napi_env env, napi_value arr, dts_frame **out, uint32_t *n, const int32_t *w,
+                        const int32_t *h, const int32_t *fmt, int nw)
+{
+    *out = NULL;
     if (napi_get_array_length(env, arr, n) != napi_ok) return -1;
     *out = (dts_frame *)calloc(*n ? *n : 1, sizeof(dts_frame));
     if (!*out) return -1;
     for (uint32_t i = 0; i < *n; ++i) {
         napi_value fo;
-        napi_get_element(env, arr, i, &fo);
-        if (parse_frame(env, fo, &(*out)[i])) return -1;
+        size_t len[3];
+        if (napi_get_element(env, arr, i, &fo) != napi_ok) return -1;
+        if (parse_frame(env, fo, &(*out)[i], len)) return -1;
+        const int k = (int)(i % (uint32_t)nw);
+        if (!frame_fits(&(*out)[i], len, w[k], h[k], fmt[k])) return -1;
     }
     return 0;
 }
@@ -278,6 +325,15 @@ typedef struct {
     dts_qstat *q;
     int n, status;
 } run_job;
+
+static void free_job(run_job *j)
+{
+    free(j->src);
+    free(j->dst);
+    free(j->qref);
+    free(j->q);
+    free(j);
+}
 
 static void run_execute(napi_env env, void *data)
 {
@@ -335,11 +391,7 @@ static void run_complete(napi_env env, napi_status st, void *data)
     for (int k = 0; k < 4; ++k)
         if (j->keep[k]) napi_delete_reference(env, j->keep[k]);
     napi_delete_async_work(env, j->work);
-    free(j->src);
-    free(j->dst);
-    free(j->qref);
-    free(j->q);
-    free(j);
+    free_job(j);
 }
 
 static napi_value js_run(napi_env env, napi_callback_info info)
@@ -348,31 +400,45 @@ static napi_value js_run(napi_env env, napi_callback_info info)
     napi_value argv[4];
     NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     if (argc < 3) return throw_dts(env, DTS_E_INVAL, "run(graph, src, dst[, qref])");
+    graph_box *b = get_graph(env, argv[0]);
+    if (!b) return throw_dts(env, DTS_E_INVAL, "run: graph");
+    const dts_graph_spec *s = &b->spec;
     run_job *j = (run_job *)calloc(1, sizeof(run_job));
     if (!j) return throw_dts(env, DTS_E_NOMEM, "run");
-    if (napi_get_value_external(env, argv[0], (void **)&j->g) != napi_ok || !j->g) {
-        free(j);
-        return throw_dts(env, DTS_E_INVAL, "run: graph");
+    j->g = b->g;
+    int32_t ow[DTS_MAX_OUTPUTS], oh[DTS_MAX_OUTPUTS], of[DTS_MAX_OUTPUTS];
+    for (int k = 0; k < s->nout; ++k) {
+        ow[k] = s->out[k].w;
+        oh[k] = s->out[k].h;
+        of[k] = s->out[k].fmt;
     }
     uint32_t ns = 0, nd = 0, nq = 0;
-    if (parse_frames(env, argv[1], &j->src, &ns) || parse_frames(env, argv[2], &j->dst, &nd)) {
-        free(j->src);
-        free(j->dst);
-        free(j);
-        return throw_dts(env, DTS_E_INVAL, "run: frames");
+    if (parse_frames(env, argv[1], &j->src, &ns, &s->src_w, &s->src_h, &s->src_fmt, 1) ||
+        parse_frames(env, argv[2], &j->dst, &nd, ow, oh, of, s->nout)) {
+        free_job(j);
+        return throw_dts(env, DTS_E_INVAL, "run: frames (a plane is missing, or its Buffer / pitch is too small)");
+    }
+    if ((uint64_t)nd != (uint64_t)ns * (uint64_t)s->nout) {
+        free_job(j);
+        return throw_dts(env, DTS_E_INVAL, "run: dst must hold src.length * outputs frames (frame-major)");
     }
     j->n = (int)ns;
     napi_valuetype qt = napi_undefined;
     if (argc >= 4) napi_typeof(env, argv[3], &qt);
     if (qt == napi_object) {
-        if (parse_frames(env, argv[3], &j->qref, &nq) || nq != ns) {
-            free(j->src);
-            free(j->dst);
-            free(j->qref);
-            free(j);
+        const int qo = s->quality_out;
+        if (!s->quality || parse_frames(env, argv[3], &j->qref, &nq, &ow[qo], &oh[qo], &of[qo], 1) || nq != ns) {
+            free_job(j);
             return throw_dts(env, DTS_E_INVAL, "run: qref frames");
         }
         j->q = (dts_qstat *)calloc(ns ? ns : 1, sizeof(dts_qstat));
+        if (!j->q) {
+            free_job(j);
+            return throw_dts(env, DTS_E_NOMEM, "run");
+        }
+    } else if (s->quality) {
+        free_job(j);
+        return throw_dts(env, DTS_E_INVAL, "run: the graph has quality on and needs qref frames");
     }
     for (int k = 0; k < 4 && (size_t)k < argc; ++k) {
         napi_valuetype t;
@@ -384,7 +450,6 @@ static napi_value js_run(napi_env env, napi_callback_info info)
     napi_create_string_utf8(env, "dts_run", NAPI_AUTO_LENGTH, &name);
     NAPI_OK(env, napi_create_async_work(env, NULL, name, run_execute, run_complete, j, &j->work));
     NAPI_OK(env, napi_queue_async_work(env, j->work));
-    (void)nd;
     return promise;
 }
 
@@ -405,7 +470,9 @@ static napi_value js_synth_frame(napi_env env, napi_callback_info info)
     napi_get_value_uint32(env, argv[4], &seed);
     napi_get_value_int64(env, argv[5], &idx);
     dts_frame f;
-    if (parse_frame(env, argv[6], &f)) return throw_dts(env, DTS_E_INVAL, "synthFrame: frame");
+    size_t len[3];
+    if (parse_frame(env, argv[6], &f, len) || !frame_fits(&f, len, w, h, fmt))
+        return throw_dts(env, DTS_E_INVAL, "synthFrame: frame");
     int e = dts_synth_host(w, h, fmt, pat, seed, idx, &f);
     if (e) return throw_dts(env, e, "dts_synth_host");
     napi_value u;

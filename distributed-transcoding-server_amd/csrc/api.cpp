@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,13 +21,24 @@
 
 using namespace dts;
 
+// Quality partials (per-tile SSE / SSIM sums) of one k_quality -> k_qreduce
+// pair.  `ev` marks the last launch that used the buffer: the next user waits
+// on it, whatever stream it runs on, so two in-flight batches never share
+// partials (the host path's two streams used to race on one).
+struct QScratch {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+};
+
 struct dts_ctx {
     int device = 0;
     int last_hip = 0;
     hipStream_t stream[2] = {nullptr, nullptr};
-    // quality scratch (partials), grown on demand
-    void *qscratch = nullptr;
-    size_t qscratch_bytes = 0;
+    QScratch qs;                               // dts_quality_run_device
+    // graphs hold a reference: the context outlives every graph made on it,
+    // whichever of dts_ctx_destroy / dts_graph_destroy runs first
+    std::atomic<int> refs{1};
 };
 
 namespace {
@@ -148,6 +160,9 @@ struct dts_graph {
     RungKind4 *dev_rk4 = nullptr;
     int njobs4 = 0, lds4 = 0, grid4 = 0;
 
+    QScratch qs;                          // dts_graph_run_device's quality partials
+    QScratch hqs[2];                      // the host path's, one per slot / stream
+    bool host_ready = false;              // every host-path buffer of both slots allocated
     // host-path batch resources (2 slots)
     int batch = 32;
     DevLayout lay_src, lay_out[DTS_MAX_OUTPUTS], lay_q;
@@ -577,14 +592,29 @@ int dts_ctx_create(int device, dts_ctx **out)
     return DTS_OK;
 }
 
-void dts_ctx_destroy(dts_ctx *c)
+static void qscratch_free(QScratch &q)
 {
-    if (!c) return;
+    if (q.ev) {
+        hipEventSynchronize(q.ev);
+        hipEventDestroy(q.ev);
+    }
+    if (q.p) hipFree(q.p);
+    q = QScratch{};
+}
+
+static void ctx_release(dts_ctx *c)
+{
+    if (c->refs.fetch_sub(1) != 1) return;
     hipSetDevice(c->device);
+    qscratch_free(c->qs);
     for (auto &s : c->stream)
         if (s) hipStreamDestroy(s);
-    if (c->qscratch) hipFree(c->qscratch);
     delete c;
+}
+
+void dts_ctx_destroy(dts_ctx *c)
+{
+    if (c) ctx_release(c);
 }
 
 int dts_ctx_last_hip_error(const dts_ctx *c) { return c ? c->last_hip : 0; }
@@ -717,6 +747,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         const dts_graph_spec &s = *spec;
         g = new dts_graph();
         g->ctx = ctx;
+        ctx->refs.fetch_add(1);
         g->spec = s;
         g->batch = s.max_batch > 0 ? std::min(s.max_batch, 65535) : 32;
         g->src_kind = gp.src_kind;
@@ -793,24 +824,13 @@ int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info)
     }
 }
 
+static void free_host_path(dts_graph *g);
+
 void dts_graph_destroy(dts_graph *g)
 {
     if (!g) return;
     hipSetDevice(g->ctx->device);
-    for (int sl = 0; sl < 2; ++sl) {
-        if (g->done[sl]) hipEventSynchronize(g->done[sl]);
-    }
-    for (int sl = 0; sl < 2; ++sl) {
-        if (g->dev_src[sl]) hipFree(g->dev_src[sl]);
-        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
-            if (g->dev_out[sl][k]) hipFree(g->dev_out[sl][k]);
-        if (g->dev_q[sl]) hipFree(g->dev_q[sl]);
-        if (g->dev_qraw[sl]) hipFree(g->dev_qraw[sl]);
-        if (g->pin_in[sl]) hipHostFree(g->pin_in[sl]);
-        if (g->pin_out[sl]) hipHostFree(g->pin_out[sl]);
-        if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
-        if (g->done[sl]) hipEventDestroy(g->done[sl]);
-    }
+    free_host_path(g);
     for (int sl = 0; sl < 2; ++sl) {
         if (g->hdr_ev[sl]) {
             hipEventSynchronize(g->hdr_ev[sl]);
@@ -823,7 +843,11 @@ void dts_graph_destroy(dts_graph *g)
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_queue) hipFree(g->dev_queue);
+    qscratch_free(g->qs);
+    for (auto &q : g->hqs) qscratch_free(q);
+    dts_ctx *ctx = g->ctx;
     delete g;
+    ctx_release(ctx);
 }
 
 int dts_graph_info_get(const dts_graph *g, dts_graph_info *info)
@@ -863,22 +887,23 @@ static DevPlanes to_dev(const dts_dev_frames &f, int fmt)
     return d;
 }
 
-static int ensure_qscratch(dts_ctx *ctx, size_t bytes)
+static int ensure_qscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
 {
-    if (ctx->qscratch_bytes >= bytes) return DTS_OK;
-    if (ctx->qscratch) {
-        hipDeviceSynchronize();
-        hipFree(ctx->qscratch);
-        ctx->qscratch = nullptr;
-        ctx->qscratch_bytes = 0;
+    if (!q.ev) HIPCHK(ctx, hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+    if (q.bytes >= bytes) return DTS_OK;
+    if (q.p) {
+        HIPCHK(ctx, hipEventSynchronize(q.ev));         // its last user is done
+        hipFree(q.p);
+        q.p = nullptr;
+        q.bytes = 0;
     }
-    HIPCHK(ctx, hipMalloc(&ctx->qscratch, bytes));
-    ctx->qscratch_bytes = bytes;
+    HIPCHK(ctx, hipMalloc(&q.p, bytes));
+    q.bytes = bytes;
     return DTS_OK;
 }
 
-static int quality_enqueue(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_frames &a, const dts_dev_frames &b,
-                           int n, dts_qraw *qraw, hipStream_t st)
+static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, const dts_dev_frames &a,
+                           const dts_dev_frames &b, int n, dts_qraw *qraw, hipStream_t st)
 {
     QualityParams q{};
     q.a = to_dev(a, fmt);
@@ -898,13 +923,15 @@ static int quality_enqueue(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
     q.interleaved = fmt == DTS_FMT_NV12;
     q.nframes = n;
     const size_t need = (size_t)n * total * (sizeof(double) + sizeof(unsigned long long));
-    int e = ensure_qscratch(ctx, need);
+    int e = ensure_qscratch(ctx, qs, need);
     if (e) return e;
-    q.partial_ssim = static_cast<double *>(ctx->qscratch);
-    q.partial_sse = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(ctx->qscratch) +
+    q.partial_ssim = static_cast<double *>(qs.p);
+    q.partial_sse = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(qs.p) +
                                                           (size_t)n * total * sizeof(double));
     q.out = qraw;
+    HIPCHK(ctx, hipStreamWaitEvent(st, qs.ev, 0));         // the previous user of these partials
     HIPCHK(ctx, launch_quality(q, total, st));
+    HIPCHK(ctx, hipEventRecord(qs.ev, st));
     return DTS_OK;
 }
 
@@ -1011,8 +1038,8 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
     return DTS_OK;
 }
 
-int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
-                         const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
+static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
+                      const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
 {
     if (!g || !src || !dst || nframes < 0) return DTS_E_INVAL;
     if (nframes == 0) return DTS_OK;
@@ -1039,9 +1066,16 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, c
     if (e) return e;
     if (want_q) {
         const dts_output_spec &o = s.out[s.quality_out];
-        return quality_enqueue(ctx, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
+        return quality_enqueue(ctx, qs, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
     }
     return DTS_OK;
+}
+
+int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
+                         const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
+{
+    if (!g) return DTS_E_INVAL;
+    return run_device(g, g->qs, src, nframes, dst, qref, qraw_dev, stream);
 }
 
 int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_frames *a, const dts_dev_frames *b,
@@ -1053,7 +1087,7 @@ int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
     if (nframes == 0) return DTS_OK;
     hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
-    return quality_enqueue(ctx, w, h, fmt, *a, *b, nframes, qraw_dev, st);
+    return quality_enqueue(ctx, ctx->qs, w, h, fmt, *a, *b, nframes, qraw_dev, st);
 }
 
 int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames *seq, int nseq,
@@ -1117,9 +1151,47 @@ int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out)
 // ---------------------------------------------------------------------------
 // host-memory path: pinned double-buffered staging over two HIP streams
 // ---------------------------------------------------------------------------
+static void free_host_path(dts_graph *g)
+{
+    for (int sl = 0; sl < 2; ++sl) {
+        if (g->done[sl]) hipEventSynchronize(g->done[sl]);
+        if (g->dev_src[sl]) hipFree(g->dev_src[sl]);
+        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
+            if (g->dev_out[sl][k]) hipFree(g->dev_out[sl][k]);
+        if (g->dev_q[sl]) hipFree(g->dev_q[sl]);
+        if (g->dev_qraw[sl]) hipFree(g->dev_qraw[sl]);
+        if (g->pin_in[sl]) hipHostFree(g->pin_in[sl]);
+        if (g->pin_out[sl]) hipHostFree(g->pin_out[sl]);
+        if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
+        if (g->done[sl]) hipEventDestroy(g->done[sl]);
+        g->dev_src[sl] = g->dev_q[sl] = nullptr;
+        for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) g->dev_out[sl][k] = nullptr;
+        g->dev_qraw[sl] = g->pin_qraw[sl] = nullptr;
+        g->pin_in[sl] = g->pin_out[sl] = nullptr;
+        g->done[sl] = nullptr;
+        g->p_chunk_first[sl] = -1;
+    }
+    g->host_ready = false;
+}
+
+static int alloc_host_path(dts_graph *g);
+
+// Every buffer of both slots, or none (a failed allocation frees what was made,
+// so a retried submit starts from scratch).
 static int ensure_host_path(dts_graph *g)
 {
-    if (g->pin_in[0]) return DTS_OK;
+    if (g->host_ready) return DTS_OK;
+    const int e = alloc_host_path(g);
+    if (e) {
+        free_host_path(g);
+        return e;
+    }
+    g->host_ready = true;
+    return DTS_OK;
+}
+
+static int alloc_host_path(dts_graph *g)
+{
     dts_ctx *ctx = g->ctx;
     const dts_graph_spec &s = g->spec;
     const int B = g->batch;
@@ -1254,8 +1326,8 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             dts_dev_frames ddst[DTS_MAX_OUTPUTS];
             for (int k = 0; k < s.nout; ++k) ddst[k] = dev_frames(g->dev_out[sl][k], g->lay_out[k]);
             dts_dev_frames dq = s.quality ? dev_frames(g->dev_q[sl], g->lay_q) : dts_dev_frames{};
-            e = dts_graph_run_device(g, &dsrc, n, ddst, s.quality ? &dq : nullptr, s.quality ? g->dev_qraw[sl] : nullptr,
-                                     st);
+            e = run_device(g, g->hqs[sl], &dsrc, n, ddst, s.quality ? &dq : nullptr,
+                           s.quality ? g->dev_qraw[sl] : nullptr, st);
             if (e) return e;
             uint8_t *op = g->pin_out[sl];
             for (int k = 0; k < s.nout; ++k) {

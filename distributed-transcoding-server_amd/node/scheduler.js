@@ -160,6 +160,13 @@ class GpuSegmentScheduler extends EventEmitter {
         });
         const total = queue.length;
         let finished = 0;
+        function safeUpdate(r, fields) {
+            try {
+                self._update(r, fields);
+            } catch (e) {
+                self.emit("updateError", e, r, fields);
+            }
+        }
         return new Promise(function (resolve) {
             if (!total) return resolve(self._summary(0));
             function pull(slot) {
@@ -171,30 +178,44 @@ class GpuSegmentScheduler extends EventEmitter {
                 const task = queue.splice(i, 1)[0];
                 slot.busy = true;
                 task.rows.forEach(function (r) {
-                    if (r) self._update(r, { assignedTo: self.workerId, status: "assigned" });
+                    if (r) safeUpdate(r, { assignedTo: self.workerId, status: "assigned" });
                 });
-                task.rows.forEach(function (r) { if (r) self._update(r, { status: "processing" }); });
+                task.rows.forEach(function (r) { if (r) safeUpdate(r, { status: "processing" }); });
+                // a throw from onUpdate / an 'update' listener must neither leave the slot busy
+                // nor lose the task from the count (ADVICE r01): every handler is guarded, and
+                // the release runs whatever happened before it
+                let counted = false;
                 self._runSegment(slot, task).then(function (res) {
-                    task.rows.forEach(function (r, k) {
-                        if (r) self._update(r, { status: "done", result: JSON.stringify(res[k]) });
-                    });
+                    counted = true;
+                    finished++;
                     slot.done++;
                     slot.ms += res.length ? res[0].ms : 0;
-                    finished++;
+                    task.rows.forEach(function (r, k) {
+                        if (r) safeUpdate(r, { status: "done", result: JSON.stringify(res[k]) });
+                    });
                 }, function (err) {
                     task.tries++;
                     task.lastGpu = slot.dev;
                     slot.failed++;
                     if (task.tries > self.maxRetries) {
-                        task.rows.forEach(function (r) {
-                            if (r) self._update(r, { status: "failed", result: JSON.stringify({ error: String(err && err.message || err), gpu: slot.dev, tries: task.tries }) });
-                        });
+                        counted = true;
                         finished++;
+                        task.rows.forEach(function (r) {
+                            if (r) safeUpdate(r, { status: "failed", result: JSON.stringify({ error: String(err && err.message || err), gpu: slot.dev, tries: task.tries }) });
+                        });
                     } else {
-                        task.rows.forEach(function (r) { if (r) self._update(r, { status: null, assignedTo: null }); });
+                        task.rows.forEach(function (r) { if (r) safeUpdate(r, { status: null, assignedTo: null }); });
                         queue.push(task);
-                        self.emit("retry", task, err);
+                        try {
+                            self.emit("retry", task, err);
+                        } catch (e) {
+                            self.emit("updateError", e, null, null);
+                        }
                     }
+                }).catch(function (e) {
+                    // a bug in the handlers above: count the task as failed rather than hang
+                    if (!counted && queue.indexOf(task) < 0) finished++;
+                    self.emit("updateError", e, null, null);
                 }).then(function () {
                     slot.busy = false;
                     if (finished === total) return resolve(self._summary(total));

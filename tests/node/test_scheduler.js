@@ -142,6 +142,21 @@ function testLadderPlanning() {
     assert.deepStrictEqual(ladder.rateOf(29.97), [30000, 1001]);
 }
 
+async function testThrowingUpdateDoesNotHang() {
+    // a failing JobChunks.update (onUpdate throws) must not leave a slot busy or hang runJobs
+    const addon = fakeAddon({ devices: 2 });
+    const js = jobSet(5);
+    let errors = 0;
+    const s = new GpuSegmentScheduler({ addon: addon, workerId: 1, segmentFrames: 2,
+        onUpdate: function (row, f) { if (f.status === "done" && row.id % 2) throw new Error("db down"); } });
+    s.on("updateError", function () { errors++; });
+    const sum = await s.runJobs(js.jobs, js.chunks, js.sources);
+    assert.strictEqual(sum.segments, 5);
+    assert.strictEqual(addon.stats.runs, 5);
+    assert.ok(errors > 0);
+    js.chunks.forEach(function (c) { assert.strictEqual(c.status, "done"); });
+}
+
 function testNoDevicesIsLoud() {
     assert.throws(function () { new GpuSegmentScheduler({ addon: fakeAddon({ devices: 0 }) }); }, /no CPU fallback/);
 }
@@ -153,5 +168,6 @@ function testNoDevicesIsLoud() {
     await testRetryOnAnotherGpu();
     await testGiveUpAfterRetries();
     await testFpsMapAndResume();
+    await testThrowingUpdateDoesNotHang();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });

@@ -1,0 +1,87 @@
+"""GPU parity at the BASELINE configs' real geometry, and the host path with
+quality on over many batches (both pinned slots / streams in flight).
+
+Integer outputs and SSE bit-exact against the oracle; SSIM within the
+north-star 1e-4 (absolute).  All calls go through the C-ABI (libdts.so).
+"""
+import numpy as np
+import pytest
+
+import dtsffi as D
+import orc
+from _util import first_diff, planes_equal
+
+pytestmark = pytest.mark.gpu
+SSIM_TOL = 1e-4
+
+
+def check_q(got, want):
+    assert got["sse"] == want["sse"]
+    for c in range(3):
+        assert got["ssim"][c] == pytest.approx(want["ssim"][c], abs=SSIM_TOL)
+    assert got["ssim_all"] == pytest.approx(want["ssim_all"], abs=SSIM_TOL)
+    assert got["psnr_avg"] == pytest.approx(want["psnr_avg"], rel=1e-12)
+
+
+def test_host_path_quality_many_batches(ctx):
+    """nframes > 3 x max_batch with PSNR/SSIM on: consecutive chunks run on the
+    two host-path streams at once, each with its own quality partials (ADVICE
+    r01: they used to share one scratch buffer).  Every frame is checked."""
+    sw, sh, w, h = 512, 288, 256, 144
+    n, batch = 14, 4
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 5, f) for f in range(n)]
+    # a different reference per frame, so swapped partials cannot go unnoticed
+    refs = [D.synth_host(w, h, D.FMT_YUV420P, 1, 100 + f, 0) for f in range(n)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, [(w, h, D.FMT_YUV420P, D.SCALE_LANCZOS)],
+                                 quality=D.Q_BOTH, quality_out=0, max_batch=batch))
+    for _rep in range(2):                     # the second submit reuses both slots' buffers
+        outs, qs = g.run_host(frames, qref=refs)
+        for f in range(n):
+            want_img = orc.scale_frame(frames[f], sw, sh, 0, w, h, 0, D.SCALE_LANCZOS)
+            assert planes_equal(outs[f][0], want_img), first_diff(outs[f][0], want_img)
+            check_q(qs[f], orc.quality_frame(w, h, want_img, refs[f]))
+    g.close()
+
+
+def test_cfg4_8k_to_4k_lanczos_quality(ctx):
+    """BASELINE config 4 at full size: 8K yuv420p -> 4K lanczos + per-frame
+    vf_psnr / vf_ssim of the output against a 4K reference rendition."""
+    sw, sh, w, h = 7680, 4320, 3840, 2160
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 0x5EED, 0)]
+    refs = [D.synth_host(w, h, D.FMT_YUV420P, 0, 0x0EF, 0)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, [(w, h, D.FMT_YUV420P, D.SCALE_LANCZOS)],
+                                 quality=D.Q_BOTH, quality_out=0))
+    outs, qs = g.run_host(frames, qref=refs)
+    want_img = orc.scale_frame(frames[0], sw, sh, 0, w, h, 0, D.SCALE_LANCZOS)
+    assert planes_equal(outs[0][0], want_img), first_diff(outs[0][0], want_img)
+    check_q(qs[0], orc.quality_frame(w, h, want_img, refs[0]))
+    g.close()
+
+
+def test_cfg1_1080p_to_720p_bicubic(ctx):
+    """BASELINE config 1's filter (the CPU-worker plumbing case): 1080p yuv420p
+    -> 720p bicubic yuv420p (libx264 is host-side and absent; only the pixel
+    path is checked)."""
+    sw, sh = 1920, 1080
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 0x5EED, f) for f in range(2)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]))
+    outs, _ = g.run_host(frames)
+    for f in range(2):
+        want = orc.scale_frame(frames[f], sw, sh, 0, 1280, 720, 0, D.SCALE_BICUBIC)
+        assert planes_equal(outs[f][0], want), first_diff(outs[f][0], want)
+    g.close()
+
+
+def test_cfg2_ladder_4k_host_path_two_frames(ctx):
+    """BASELINE config 2 through the host path (pinned H2D, one fused launch, D2H)."""
+    sw, sh = 3840, 2160
+    outs = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_NV12, D.SCALE_BICUBIC),
+            (854, 480, D.FMT_NV12, D.SCALE_BICUBIC)]
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 0x5EED, f) for f in (3, 4)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, outs))
+    got, _ = g.run_host(frames)
+    for f in range(2):
+        for k, (w, h, fmt, m) in enumerate(outs):
+            want = orc.scale_frame(frames[f], sw, sh, 0, w, h, fmt, m)
+            assert planes_equal(got[f][k], want), f"frame {f} out {k}: {first_diff(got[f][k], want)}"
+    g.close()

@@ -29,6 +29,8 @@ for s in "$@"; do
     benchq) step benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu ;;
     benchv3) DTS_LADDER=3 step benchv3 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
     benchw4) DTS_LIB=$PWD/distributed-transcoding-server_amd/lib/libdts_w4.so step benchw4 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
+    probe)  step probe 60 ./tools/probe_mfma_i8 ;;
+    new)    step tests_new 600 python -u -m pytest tests/test_gpu_configs.py tests/test_node.py -m gpu -v --timeout 300 --timeout-method thread ;;
     v4small) step v4small 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "v4 and (small or 4k_one)" ;;
     *) echo "unknown step $s" ;;
   esac
