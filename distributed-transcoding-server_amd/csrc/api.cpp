@@ -159,6 +159,12 @@ struct dts_graph {
     Job4 *dev_jobs4 = nullptr;
     RungKind4 *dev_rk4 = nullptr;
     int njobs4 = 0, lds4 = 0, grid4 = 0;
+    // v5 ladder (ladder5.hip): every plane kind of every rendition, when the graph fits it
+    bool v5 = false;
+    void *dev_tables5 = nullptr;
+    Job5 *dev_jobs5 = nullptr;
+    Kind5 *dev_kinds5 = nullptr;
+    int njobs5 = 0, lds5 = 0, grid5 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -394,6 +400,10 @@ struct GraphPlan {
     std::vector<Plan4> p4;
     std::vector<Job> jobs;                // v3 strips (the kinds not on v4)
     std::vector<Job4> jobs4;              // v4 strips
+    bool v5 = false;                      // the whole graph runs on k_ladder5
+    Plan5Kind p5[2];                      // luma, chroma
+    std::vector<Job5> jobs5;
+    int lds5 = 0;
     dts_graph_info info{};
 };
 
@@ -426,6 +436,41 @@ bool v4_enabled()
     return !(f && f[0] == '3');
 }
 
+// DTS_LADDER=4 / 3 keep the graph off the v5 kernel (A/B runs, tests)
+bool v5_enabled()
+{
+    const char *f = std::getenv("DTS_LADDER");
+    return !(f && (f[0] == '3' || f[0] == '4'));
+}
+
+// k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs
+bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
+{
+    if (!v5_enabled() || s.hdr_to_sdr) return false;
+    if (s.src_fmt != DTS_FMT_YUV420P && s.src_fmt != DTS_FMT_NV12) return false;
+    for (int kind = 0; kind < 2; ++kind) {
+        Plan5In in;
+        in.chroma = kind == 1;
+        in.nv12_chroma = kind == 1 && s.src_fmt == DTS_FMT_NV12;
+        in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
+        in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
+        for (int k = 0; k < s.nout; ++k) {
+            const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
+            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
+        }
+        if (!plan5_kind(in, gp.p5[kind])) return false;
+    }
+    for (int kind = 0; kind < 2; ++kind)
+        for (int st = 0; st < (int)gp.p5[kind].strips.size(); ++st) gp.jobs5.push_back(Job5{kind, st});
+    // strips in source-column order (luma x of the strip start): a queue hands out
+    // neighbouring strips back to back, so their shared halo columns hit L2
+    auto srcx = [&](const Job5 &j) { return (j.kind ? 2 : 1) * gp.p5[j.kind].strips[j.strip].L; };
+    std::stable_sort(gp.jobs5.begin(), gp.jobs5.end(), [&](const Job5 &a, const Job5 &b) { return srcx(a) < srcx(b); });
+    gp.lds5 = 4 * std::max(gp.p5[0].lds_dw, gp.p5[1].lds_dw);
+    gp.v5 = true;
+    return true;
+}
+
 bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
 {
     const bool p010 = s.src_fmt == DTS_FMT_P010LE, nv12 = s.src_fmt == DTS_FMT_NV12;
@@ -448,13 +493,23 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     const bool use4 = v4_enabled();
     gp.kts.resize((size_t)s.nout * 2);
     gp.p4.resize(gp.kts.size());
+    for (size_t i = 0; i < gp.kts.size(); ++i) {
+        e = build_kind(s, (int)(i >> 1), (int)(i & 1), gp.kts[i]);
+        if (e) return e;
+    }
+    const bool v5 = plan5_graph(s, gp);
     int ndmax_need = 1;
     for (int k = 0; k < s.nout; ++k)
         for (int kind = 0; kind < 2; ++kind) {
             const size_t i = (size_t)k * 2 + kind;
             KindTables &kt = gp.kts[i];
-            e = build_kind(s, k, kind, kt);
-            if (e) return e;
+            if (v5) {
+                gp.info.h_taps[k][kind] = kt.h.span;
+                gp.info.v_taps[k][kind] = kt.v.span;
+                gp.info.sws_h_size[k][kind] = kt.sws_h;
+                gp.info.sws_v_size[k][kind] = kt.sws_v;
+                continue;
+            }
             if (use4 && plan4_for(s, kt, kind, gp.p4[i]))
                 gp.v4_mask |= 1u << i;
             else
@@ -467,7 +522,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
         }
     gp.ndmax = ladder_ndmax_for(ndmax_need);
     if (!gp.ndmax) return DTS_E_RANGE;
-    const bool on3 = gp.v4_mask != (1u << gp.kts.size()) - 1;
+    const bool on3 = !v5 && gp.v4_mask != (1u << gp.kts.size()) - 1;
     if (on3) {
         // v3 ring: smallest power of two holding every V window of the kinds v3 runs
         int rp = 8;
@@ -494,7 +549,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
         gp.lds_bytes = 2 * gp.stage_bytes + gp.ring_pairs * kLumaCols * 4;
         if (gp.lds_bytes > 160 * 1024) return DTS_E_RANGE;
     }
-    for (size_t i = 0; i < gp.kts.size(); ++i) {
+    for (size_t i = 0; i < gp.kts.size() && !v5; ++i) {
         if (!((gp.v4_mask >> i) & 1)) continue;
         const Plan4 &pl = gp.p4[i];
         for (int st = 0; st < pl.nstrips; ++st)
@@ -537,9 +592,14 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     }
     if (s.quality) algo += in.out_frame_bytes[s.quality_out];
     in.algo_bytes_per_frame = algo;
-    in.njobs = (int)(gp.jobs.size() + gp.jobs4.size());
-    in.lds_bytes = std::max(gp.lds_bytes, gp.lds4);
+    in.njobs = (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
+    in.lds_bytes = std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
     in.ladder_v4_mask = (int32_t)gp.v4_mask;
+    in.ladder_v5 = gp.v5 ? 1 : 0;
+    for (int kind = 0; kind < 2; ++kind) {
+        in.v5_strip_width[kind] = gp.v5 ? gp.p5[kind].strip_width : 0;
+        in.v5_strips[kind] = gp.v5 ? (int32_t)gp.p5[kind].strips.size() : 0;
+    }
     return DTS_OK;
 }
 
@@ -547,7 +607,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.2 (gfx950; abi 2)"; }
+const char *dts_version(void) { return "dts-mi355x 0.3 (gfx950; abi 3)"; }
 
 const char *dts_strerror(int err)
 {
@@ -735,6 +795,74 @@ static int upload_v4(dts_graph *g, const GraphPlan &gp)
     return DTS_OK;
 }
 
+// v5 tables -> one device blob (strips, entries, B fragments, V tables, Kind5 x 2, jobs), plus its grid
+static int upload_v5(dts_graph *g, const GraphPlan &gp)
+{
+    dts_ctx *ctx = g->ctx;
+    std::vector<uint8_t> blob;
+    struct Offs {
+        size_t strips = 0, ents = 0, bfrag = 0;
+        std::vector<size_t> vslot, vcoef, vlim;
+    } offs[2];
+    for (int kind = 0; kind < 2; ++kind) {
+        const Plan5Kind &pk = gp.p5[kind];
+        offs[kind].strips = push_blob(blob, pk.strips);
+        offs[kind].ents = push_blob(blob, pk.ents);
+        offs[kind].bfrag = push_blob(blob, pk.bfrag);
+        for (size_t r = 0; r < pk.vslot.size(); ++r) {
+            offs[kind].vslot.push_back(push_blob(blob, pk.vslot[r]));
+            offs[kind].vcoef.push_back(push_blob(blob, pk.vcoef[r]));
+            offs[kind].vlim.push_back(push_blob(blob, pk.vlim[r]));
+        }
+    }
+    const size_t jobs_off = push_blob(blob, gp.jobs5);
+    const size_t k_off = (size_t)align_up((int64_t)blob.size(), 256);
+    blob.resize(k_off + 2 * sizeof(Kind5));
+    HIPCHK(ctx, hipMalloc(&g->dev_tables5, blob.size()));
+    uint8_t *base = static_cast<uint8_t *>(g->dev_tables5);
+    Kind5 kinds[2];
+    std::memset(kinds, 0, sizeof kinds);
+    for (int kind = 0; kind < 2; ++kind) {
+        const Plan5Kind &pk = gp.p5[kind];
+        Kind5 &k = kinds[kind];
+        k.nplanes = pk.nplanes;
+        k.nsteps = pk.nsteps;
+        k.srcH = kind ? (g->spec.src_h + 1) >> 1 : g->spec.src_h;
+        k.P = pk.P;
+        k.stage = pk.stage;
+        k.nrings = pk.nrings;
+        k.nunits = pk.nunits;
+        k.nstrips = (int32_t)pk.strips.size();
+        k.R = pk.R;
+        k.M = pk.M;
+        for (int i = 0; i < kL5MaxRings; ++i) k.ring[i] = pk.ring[i];
+        for (int u = 0; u < pk.nunits; ++u) {
+            k.unit[u] = pk.unit[u];
+            const int r = pk.unit[u].rung;
+            k.unit[u].vslot = reinterpret_cast<const int32_t *>(base + offs[kind].vslot[r]);
+            k.unit[u].vcoef = reinterpret_cast<const uint32_t *>(base + offs[kind].vcoef[r]);
+            k.unit[u].vlim = reinterpret_cast<const int32_t *>(base + offs[kind].vlim[r]);
+        }
+        k.strips = reinterpret_cast<const Strip5 *>(base + offs[kind].strips);
+        k.ents = reinterpret_cast<const Ent5 *>(base + offs[kind].ents);
+        k.bfrag = reinterpret_cast<const uint32_t *>(base + offs[kind].bfrag);
+    }
+    std::memcpy(blob.data() + k_off, kinds, sizeof kinds);
+    HIPCHK(ctx, hipMemcpy(g->dev_tables5, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    g->dev_jobs5 = reinterpret_cast<Job5 *>(base + jobs_off);
+    g->dev_kinds5 = reinterpret_cast<Kind5 *>(base + k_off);
+    g->njobs5 = (int)gp.jobs5.size();
+    g->lds5 = gp.lds5;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+        cus = 256;
+    const int bpc = ladder5_blocks_per_cu(g->src_kind, g->lds5);
+    if (bpc < 1) return DTS_E_RANGE;
+    g->grid5 = bpc * cus;
+    g->v5 = true;
+    return DTS_OK;
+}
+
 int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
 {
     if (!ctx || !spec || !out) return DTS_E_INVAL;
@@ -759,8 +887,9 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         g->v4_mask = gp.v4_mask;
         g->info = gp.info;
         hipSetDevice(ctx->device);
-        e = upload_v3(g, gp.kts);
+        e = gp.v5 ? DTS_OK : upload_v3(g, gp.kts);
         if (!e && gp.v4_mask) e = upload_v4(g, gp);
+        if (!e && gp.v5) e = upload_v5(g, gp);
         if (!e && hipMalloc(&g->dev_queue, kQueueSlots * kQueueWidth * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
             e = DTS_E_HIP;
@@ -842,6 +971,7 @@ void dts_graph_destroy(dts_graph *g)
     if (g->dev_tm_lut) hipFree(g->dev_tm_lut);
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
+    if (g->dev_tables5) hipFree(g->dev_tables5);
     if (g->dev_queue) hipFree(g->dev_queue);
     qscratch_free(g->qs);
     for (auto &q : g->hqs) qscratch_free(q);
@@ -960,7 +1090,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    const int njobs_max = std::max(1, std::max(p.njobs, g->njobs4));
+    const int njobs_max = std::max(1, std::max(std::max(p.njobs, g->njobs4), g->njobs5));
     const int max_frames = std::max(1, (1 << 30) / njobs_max);
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
         const int n = std::min(max_frames, nframes - f0);
@@ -970,6 +1100,26 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
+        if (g->v5) {
+            Ladder5Params q{};
+            q.src = pp.src;
+            for (int k = 0; k < kMaxRungs; ++k) {
+                q.dst[k] = pp.dst[k];
+                q.dst_fmt[k] = pp.dst_fmt[k];
+            }
+            q.njobs = g->njobs5;
+            q.nframes = n;
+            q.nq = n >= 64 ? ladder4_queues() : 1;
+            q.lds_dw = g->lds5 / 4;
+            q.jobs = g->dev_jobs5;
+            q.kinds = g->dev_kinds5;
+            q.queue = g->dev_queue + kQueueWidth * (g->queue_next++ % kQueueSlots);
+            HIPCHK(ctx, hipMemsetAsync(q.queue, 0, kQueueWidth * sizeof(unsigned int), st));
+            int grid = std::min(n * g->njobs5, g->grid5);
+            grid = std::max(q.nq, (grid + q.nq - 1) / q.nq * q.nq);
+            HIPCHK(ctx, launch_ladder5(q, g->src_kind, g->lds5, grid, st));
+            continue;
+        }
         if (g->njobs4) {
             Ladder4Params q{};
             q.src = pp.src;

@@ -134,6 +134,90 @@ hipError_t launch_ladder4(const Ladder4Params &p, int lds_bytes, int grid, hipSt
 int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
 
 // ---------------------------------------------------------------------------
+// v5 ladder (ladder5.hip): H on the matrix cores (v_mfma_i32_16x16x64_i8),
+// V by v_dot2_i32_i16 from a quad-major LDS ring, every rendition of a
+// column strip from one staged copy of the source rows.
+// ---------------------------------------------------------------------------
+constexpr int kL5Rows = 16;         // source rows per step (the MFMA's M)
+constexpr int kL5Ent = 8;           // H entries (K blocks of 64 source columns) per wave
+constexpr int kL5MaxRings = 2 * DTS_MAX_OUTPUTS;
+constexpr int kL5MaxUnits = 2 * DTS_MAX_OUTPUTS;
+constexpr int kL5MaxLoads = 4;      // 16-B staging loads per thread per step
+constexpr int kL5Bias = 128 << 14;  // 128 * sum(taps): the (src ^ 0x80) offset of every H output
+
+struct Ent5 {                       // one K block of one H tile, run by one wave
+    int32_t bfrag;                  // B fragment pair (hi 1 KB, lo 1 KB; 16 B per lane)
+    int16_t soff;                   // byte offset of the K block in the staged row (multiple of 8)
+    int16_t col0;                   // ring column of the tile's first output (multiple of 16)
+    int8_t plane;                   // staged plane (chroma: 0 = U, 1 = V)
+    int8_t ring;                    // ring of the tile's outputs
+    int8_t flags;                   // 1: first K block of the tile, 2: last (epilogue)
+    int8_t pad_;
+};
+
+struct Ring5 {                      // H outputs of one (rendition, plane), quad-major:
+    int32_t lds;                    // dword (quad k, slot s, column m) at lds + k*qstride + 4 s + m
+    int32_t qstride;                // dwords per quad = 4 x slots allocated (slots = 1 mod 8)
+};
+
+struct Unit5 {                      // V work of one (rendition, output mode) of a plane kind
+    int32_t rung;
+    int32_t mode;                   // 0: 4 columns of one plane per lane, 1: nv12 chroma (2 columns x U, V)
+    int32_t plane;                  // mode 0: output plane (0 Y / 1 U / 2 V)
+    int32_t ring0, ring1;           // ring(s) read (mode 1: U, V)
+    int32_t np4;                    // V tap pairs per output row, rounded up to 4
+    int32_t dstW;                   // columns of the output plane
+    int32_t vco;                    // dword offset of this unit's per-step V staging (2 buffers of vco_dw)
+    int32_t vco_dw;                 // dwords per buffer: rows x (4 + np4)
+    int32_t pad_;
+    const int32_t *vslot;           // [dstH] ring slot of the row's first tap pair
+    const uint32_t *vcoef;          // [dstH][np4] int16x2 tap pairs
+    const int32_t *vlim;            // [nsteps] output rows complete after step b
+};
+
+struct Strip5 {                     // one column strip of a plane kind
+    int32_t L;                      // first staged sample column (multiple of 16)
+    int32_t nchunk;                 // 16-B staging loads per step (all rows, all planes)
+    int32_t cpr;                    // 16-B loads per staged row per plane
+    int32_t pad_;
+    int32_t ent0[4], nent[4];       // each wave's H entries
+    int32_t x0[DTS_MAX_OUTPUTS];    // first output column per rendition (multiple of 16)
+    int32_t quads[kL5MaxUnits];     // V lane tasks per output row, per unit
+};
+
+struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every rendition
+    int32_t nplanes, nsteps, srcH;
+    int32_t P;                      // staged row pitch, bytes (16 x odd: conflict-free A reads)
+    int32_t stage;                  // dword offset of the 2 stage buffers
+    int32_t nrings, nunits, nstrips;
+    int32_t R;                      // ring slots (row pairs) of every ring, a multiple of 8: pair p in slot p % R
+    int32_t M;                      // 8-pair blocks starting below M are also written at R + slot
+    int32_t pad_;
+    Ring5 ring[kL5MaxRings];
+    Unit5 unit[kL5MaxUnits];
+    const Strip5 *strips;
+    const Ent5 *ents;
+    const uint32_t *bfrag;
+};
+
+struct Job5 {
+    int32_t kind, strip;
+};
+
+struct Ladder5Params {
+    DevPlanes src;
+    DevPlanes dst[kMaxRungs];
+    int32_t dst_fmt[kMaxRungs];
+    int32_t njobs, nframes, nq, lds_dw;
+    const Job5 *jobs;
+    const Kind5 *kinds;
+    unsigned int *queue;
+};
+
+hipError_t launch_ladder5(const Ladder5Params &p, int src_kind, int lds_bytes, int grid, hipStream_t s);
+int ladder5_blocks_per_cu(int src_kind, int lds_bytes);
+
+// ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
 // ---------------------------------------------------------------------------
 constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x

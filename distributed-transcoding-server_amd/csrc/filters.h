@@ -76,4 +76,34 @@ struct Plan4 {
 bool plan4_kind(const SwsFilter &fh, const VTable &v, int srcH, int dstW, int dstH, int bps, int nlmax, int cap,
                 int maxcols, int64_t row_bytes, int ring, Plan4 &out);
 
+// v5 ladder plan of one plane kind (plan5.cpp, ladder5.hip).
+struct Plan5Rung {
+    const SwsFilter *fh;             // the libswscale H filter
+    const VTable *v;                 // the packed V table
+    int dstW, dstH, fmt;             // plane size and the rendition's output format
+};
+
+struct Plan5In {
+    bool chroma = false;             // U + V planes (else luma)
+    bool nv12_chroma = false;        // chroma staged from an interleaved nv12 plane
+    int srcW = 0, srcH = 0;          // plane size
+    int lds_cap = 80 * 1024;         // bytes per workgroup (2 per CU)
+    std::vector<Plan5Rung> rungs;
+};
+
+struct Plan5Kind {
+    int nplanes = 1, nsteps = 0, P = 0, stage = 0, nrings = 0, nunits = 0, lds_dw = 0, strip_width = 0;
+    int R = 0, M = 0;
+    Ring5 ring[kL5MaxRings]{};
+    Unit5 unit[kL5MaxUnits]{};
+    std::vector<Strip5> strips;
+    std::vector<Ent5> ents;
+    std::vector<uint32_t> bfrag;
+    std::vector<std::vector<int32_t>> vslot, vlim;   // per rendition
+    std::vector<std::vector<uint32_t>> vcoef;
+};
+
+// false: the geometry / format does not fit k_ladder5 (the kind then runs on v4 / v3)
+bool plan5_kind(const Plan5In &in, Plan5Kind &out);
+
 } // namespace dts

@@ -82,7 +82,8 @@ class GraphInfo(ctypes.Structure):
                 ("v_taps", (ctypes.c_int32 * 2) * MAX_OUTPUTS),
                 ("sws_h_size", (ctypes.c_int32 * 2) * MAX_OUTPUTS),
                 ("sws_v_size", (ctypes.c_int32 * 2) * MAX_OUTPUTS), ("ladder_v4_mask", ctypes.c_int32),
-                ("h_pairs4", (ctypes.c_int32 * 2) * MAX_OUTPUTS)]
+                ("h_pairs4", (ctypes.c_int32 * 2) * MAX_OUTPUTS), ("ladder_v5", ctypes.c_int32),
+                ("v5_strip_width", ctypes.c_int32 * 2), ("v5_strips", ctypes.c_int32 * 2)]
 
 
 # Every symbol include/dts.h declares (checked by tests/test_abi.py).

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DTS_ABI_VERSION 2
+#define DTS_ABI_VERSION 3
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -165,6 +165,10 @@ typedef struct dts_graph_info {
     int32_t ladder_v4_mask;             /* bit 2*output+kind: that plane kind runs on the v4
                                            ladder kernel (the rest on v3; DTS_LADDER=3 forces v3) */
     int32_t h_pairs4[DTS_MAX_OUTPUTS][2]; /* v4 H tap pairs per output (luma, chroma), 0 = v3 */
+    int32_t ladder_v5;                  /* 1: the whole graph runs on the v5 ladder kernel (H on the
+                                           matrix cores; DTS_LADDER=4 / 3 force v4 / v3) */
+    int32_t v5_strip_width[2];          /* v5 source columns per strip (luma, chroma) */
+    int32_t v5_strips[2];               /* v5 strips per plane kind */
 } dts_graph_info;
 
 const char *dts_version(void);

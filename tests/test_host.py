@@ -110,9 +110,9 @@ LADDER4K = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_NV12, D
 
 @pytest.mark.parametrize("fmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
 def test_plan_bench_ladder_runs_on_v4(fmt, monkeypatch):
-    """The BASELINE cfg2/cfg3 geometries plan every plane kind onto the v4 kernel;
-    DTS_LADDER=3 moves them all back to v3."""
-    monkeypatch.delenv("DTS_LADDER", raising=False)
+    """The BASELINE cfg2/cfg3 geometries plan every plane kind onto the v4 kernel
+    under DTS_LADDER=4; DTS_LADDER=3 moves them all back to v3."""
+    monkeypatch.setenv("DTS_LADDER", "4")
     info = D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K))
     # p010 chroma of the 480p rung: 4-byte (U16,V16) samples leave the v4 window too few pairs
     assert info.ladder_v4_mask == (0x1f if fmt == D.FMT_P010LE else 0x3f)
@@ -122,9 +122,26 @@ def test_plan_bench_ladder_runs_on_v4(fmt, monkeypatch):
     assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v4_mask == 0
 
 
+@pytest.mark.parametrize("fmt", [D.FMT_YUV420P, D.FMT_NV12])
+def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
+    """8-bit sources with 8-bit outputs (cfg1, cfg2, cfg4 and upscales) plan the whole
+    graph onto the v5 (matrix-core) ladder: every strip's H entries fit the waves and
+    its LDS fits two workgroups per CU.  p010 sources and HDR graphs stay on v4 / v3."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    for sw, sh, outs in [(3840, 2160, LADDER4K), (7680, 4320, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)]),
+                         (1920, 1080, [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]),
+                         (640, 360, [(1280, 720, D.FMT_NV12, D.SCALE_BICUBIC), (320, 180, D.FMT_NV12, D.SCALE_AREA)])]:
+        info = D.graph_plan(D.make_spec(sw, sh, fmt, outs))
+        assert info.ladder_v5 == 1 and info.ladder_v4_mask == 0
+        assert info.lds_bytes <= 80 * 1024 and min(info.v5_strips) >= 1
+    assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, LADDER4K)).ladder_v5 == 0
+    monkeypatch.setenv("DTS_LADDER", "4")
+    assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == 0
+
+
 def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
     """Upscales stay on v3; the downscale output of the same graph still plans to v4."""
-    monkeypatch.delenv("DTS_LADDER", raising=False)
+    monkeypatch.setenv("DTS_LADDER", "4")
     info = D.graph_plan(D.make_spec(640, 360, D.FMT_YUV420P, [(1280, 720, D.FMT_NV12, D.SCALE_BICUBIC),
                                                               (320, 180, D.FMT_NV12, D.SCALE_BICUBIC)]))
     assert info.ladder_v4_mask & 0x3 == 0 and info.ladder_v4_mask & 0xc == 0xc

@@ -31,6 +31,8 @@ for s in "$@"; do
     benchw4) DTS_LIB=$PWD/distributed-transcoding-server_amd/lib/libdts_w4.so step benchw4 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
     probe)  step probe 60 ./tools/probe_mfma_i8 ;;
     new)    step tests_new 600 python -u -m pytest tests/test_gpu_configs.py tests/test_node.py -m gpu -v --timeout 300 --timeout-method thread ;;
+    v5small) step v5small 180 python -u -m pytest tests/test_gpu_ladder.py -x -v --timeout 60 --timeout-method thread -k "v5 and (small or identity)" ;;
+    v5all)  step v5all 600 python -u -m pytest tests/test_gpu_ladder.py tests/test_gpu_configs.py tests/test_golden.py -v --timeout 120 --timeout-method thread -m gpu -k "v5 or configs or golden" ;;
     v4small) step v4small 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "v4 and (small or 4k_one)" ;;
     *) echo "unknown step $s" ;;
   esac
