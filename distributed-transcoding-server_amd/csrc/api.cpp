@@ -21,6 +21,10 @@
 
 using namespace dts;
 
+#ifdef DTS_L5_STAMP
+namespace dts { int ladder5_stamps(unsigned long long *out, bool reset); }
+#endif
+
 // Quality partials (per-tile SSE / SSIM sums) of one k_quality -> k_qreduce
 // pair.  `ev` marks the last launch that used the buffer: the next user waits
 // on it, whatever stream it runs on, so two in-flight batches never share
@@ -466,7 +470,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     // neighbouring strips back to back, so their shared halo columns hit L2
     auto srcx = [&](const Job5 &j) { return (j.kind ? 2 : 1) * gp.p5[j.kind].strips[j.strip].L; };
     std::stable_sort(gp.jobs5.begin(), gp.jobs5.end(), [&](const Job5 &a, const Job5 &b) { return srcx(a) < srcx(b); });
-    gp.lds5 = 4 * std::max(gp.p5[0].lds_dw, gp.p5[1].lds_dw);
+    gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     return true;
 }
@@ -801,19 +805,15 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
     dts_ctx *ctx = g->ctx;
     std::vector<uint8_t> blob;
     struct Offs {
-        size_t strips = 0, ents = 0, bfrag = 0;
-        std::vector<size_t> vslot, vcoef, vlim;
+        size_t strips = 0, ents = 0, bfrag = 0, vsched = 0, vstep = 0;
     } offs[2];
     for (int kind = 0; kind < 2; ++kind) {
         const Plan5Kind &pk = gp.p5[kind];
         offs[kind].strips = push_blob(blob, pk.strips);
         offs[kind].ents = push_blob(blob, pk.ents);
         offs[kind].bfrag = push_blob(blob, pk.bfrag);
-        for (size_t r = 0; r < pk.vslot.size(); ++r) {
-            offs[kind].vslot.push_back(push_blob(blob, pk.vslot[r]));
-            offs[kind].vcoef.push_back(push_blob(blob, pk.vcoef[r]));
-            offs[kind].vlim.push_back(push_blob(blob, pk.vlim[r]));
-        }
+        offs[kind].vsched = push_blob(blob, pk.vsched);
+        offs[kind].vstep = push_blob(blob, pk.vstep);
     }
     const size_t jobs_off = push_blob(blob, gp.jobs5);
     const size_t k_off = (size_t)align_up((int64_t)blob.size(), 256);
@@ -831,18 +831,12 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
         k.P = pk.P;
         k.stage = pk.stage;
         k.nrings = pk.nrings;
-        k.nunits = pk.nunits;
+        k.nrungs = g->spec.nout;
         k.nstrips = (int32_t)pk.strips.size();
-        k.R = pk.R;
-        k.M = pk.M;
         for (int i = 0; i < kL5MaxRings; ++i) k.ring[i] = pk.ring[i];
-        for (int u = 0; u < pk.nunits; ++u) {
-            k.unit[u] = pk.unit[u];
-            const int r = pk.unit[u].rung;
-            k.unit[u].vslot = reinterpret_cast<const int32_t *>(base + offs[kind].vslot[r]);
-            k.unit[u].vcoef = reinterpret_cast<const uint32_t *>(base + offs[kind].vcoef[r]);
-            k.unit[u].vlim = reinterpret_cast<const int32_t *>(base + offs[kind].vlim[r]);
-        }
+        for (int r = 0; r < DTS_MAX_OUTPUTS; ++r) k.out[r] = pk.out[r];
+        k.vsched = reinterpret_cast<const VEnt5 *>(base + offs[kind].vsched);
+        k.vstep = reinterpret_cast<const int4 *>(base + offs[kind].vstep);
         k.strips = reinterpret_cast<const Strip5 *>(base + offs[kind].strips);
         k.ents = reinterpret_cast<const Ent5 *>(base + offs[kind].ents);
         k.bfrag = reinterpret_cast<const uint32_t *>(base + offs[kind].bfrag);
@@ -1103,14 +1097,10 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         if (g->v5) {
             Ladder5Params q{};
             q.src = pp.src;
-            for (int k = 0; k < kMaxRungs; ++k) {
-                q.dst[k] = pp.dst[k];
-                q.dst_fmt[k] = pp.dst_fmt[k];
-            }
+            for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
             q.njobs = g->njobs5;
             q.nframes = n;
             q.nq = n >= 64 ? ladder4_queues() : 1;
-            q.lds_dw = g->lds5 / 4;
             q.jobs = g->dev_jobs5;
             q.kinds = g->dev_kinds5;
             q.queue = g->dev_queue + kQueueWidth * (g->queue_next++ % kQueueSlots);
@@ -1583,6 +1573,11 @@ int dts_synth_device(dts_ctx *ctx, int w, int h, int fmt, int pattern, uint32_t 
     HIPCHK(ctx, launch_synth(w, h, fmt, pattern, seed, first, to_dev(*dst, fmt), nframes, st));
     return DTS_OK;
 }
+
+#ifdef DTS_L5_STAMP
+// diagnostic builds only (tools/build_stamp5.sh): per-phase cycle sums of k_ladder5
+int dts_debug_ladder5_stamps(unsigned long long *out, int reset) { return dts::ladder5_stamps(out, reset != 0); }
+#endif
 
 // vf_fps.c (FFmpeg 4.4) frame selection, round=near, constant-rate input
 // whose first pts is 0: t_i = round(i * in_den*out_num / (in_num*out_den)),

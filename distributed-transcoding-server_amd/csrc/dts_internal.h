@@ -134,16 +134,20 @@ hipError_t launch_ladder4(const Ladder4Params &p, int lds_bytes, int grid, hipSt
 int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
 
 // ---------------------------------------------------------------------------
-// v5 ladder (ladder5.hip): H on the matrix cores (v_mfma_i32_16x16x64_i8),
-// V by v_dot2_i32_i16 from a quad-major LDS ring, every rendition of a
-// column strip from one staged copy of the source rows.
+// v5 ladder (ladder5.hip): both FIR passes on the matrix cores
+// (v_mfma_i32_16x16x64_i8), every rendition of a column strip from one staged
+// copy of the source rows.
 // ---------------------------------------------------------------------------
-constexpr int kL5Rows = 16;         // source rows per step (the MFMA's M)
+constexpr int kL5Rows = 16;         // source rows per step (the H MFMA's M)
 constexpr int kL5Ent = 8;           // H entries (K blocks of 64 source columns) per wave
 constexpr int kL5MaxRings = 2 * DTS_MAX_OUTPUTS;
-constexpr int kL5MaxUnits = 2 * DTS_MAX_OUTPUTS;
 constexpr int kL5MaxLoads = 4;      // 16-B staging loads per thread per step
-constexpr int kL5Bias = 128 << 14;  // 128 * sum(taps): the (src ^ 0x80) offset of every H output
+constexpr int kL5MaxVkb = 2;        // V K blocks (64 source rows) per row group
+constexpr int kL5Bias = 128 << 14;  // 128 * sum(H taps): the (src ^ 0x80) offset of every H output
+constexpr int kL5VBias = (128 << 12) + (64 << 12);   // 128 * sum(V taps) ((y & 255) ^ 0x80) + flat dither
+// per-item rendition table in LDS (bytes 16..): per rendition 16 dwords {x0, nct, pitch[3] (32-bit),
+// pad, plane base lo/hi x 3 (this frame)}
+constexpr int kL5RungTab = 4 * 16 * DTS_MAX_OUTPUTS;
 
 struct Ent5 {                       // one K block of one H tile, run by one wave
     int32_t bfrag;                  // B fragment pair (hi 1 KB, lo 1 KB; 16 B per lane)
@@ -155,24 +159,31 @@ struct Ent5 {                       // one K block of one H tile, run by one wav
     int8_t pad_;
 };
 
-struct Ring5 {                      // H outputs of one (rendition, plane), quad-major:
-    int32_t lds;                    // dword (quad k, slot s, column m) at lds + k*qstride + 4 s + m
-    int32_t qstride;                // dwords per quad = 4 x slots allocated (slots = 1 mod 8)
+struct Ring5 {                      // H outputs of one (rendition, plane): two column-major byte planes
+    int32_t hi;                     // LDS byte offset: y >> 8 of (column c, source row r) at hi + c*CP + r % RR
+    int32_t lo;                     // LDS byte offset of (y & 255) ^ 0x80
+    int32_t CP;                     // column pitch, bytes (16 x odd: conflict-free V A reads)
+    int32_t RR;                     // rows held, a multiple of 16
 };
 
-struct Unit5 {                      // V work of one (rendition, output mode) of a plane kind
+struct VEnt5 {                      // one V row group of one rendition, ready after its step (one s_load)
     int32_t rung;
-    int32_t mode;                   // 0: 4 columns of one plane per lane, 1: nv12 chroma (2 columns x U, V)
-    int32_t plane;                  // mode 0: output plane (0 Y / 1 U / 2 V)
-    int32_t ring0, ring1;           // ring(s) read (mode 1: U, V)
-    int32_t np4;                    // V tap pairs per output row, rounded up to 4
-    int32_t dstW;                   // columns of the output plane
-    int32_t vco;                    // dword offset of this unit's per-step V staging (2 buffers of vco_dw)
-    int32_t vco_dw;                 // dwords per buffer: rows x (4 + np4)
+    int32_t G;                      // output rows 16 G .. 16 G + rows - 1
+    int32_t rows;                   // valid rows (<= 16)
+    int32_t w0;                     // ring row of the first source row of its K blocks (w0 % RR, multiple of 8)
+    int32_t nkb;                    // K blocks of 64 source rows
+    int32_t bfrag;                  // first V fragment pair (taps >> 8, taps & 255 as signed bytes)
+    int32_t fmt;                    // the rendition's output format
+    int32_t dstW;                   // columns of its output plane(s) of this kind
+    Ring5 ring0;                    // its ring (chroma: U)
+    int32_t hi1, lo1;               // chroma: the V plane's ring (same CP, RR)
+    int32_t pad_[2];
+};
+
+struct Out5 {                       // one rendition's output of this plane kind
+    int32_t fmt;                    // DTS_FMT_YUV420P / DTS_FMT_NV12
+    int32_t dstW, dstH;
     int32_t pad_;
-    const int32_t *vslot;           // [dstH] ring slot of the row's first tap pair
-    const uint32_t *vcoef;          // [dstH][np4] int16x2 tap pairs
-    const int32_t *vlim;            // [nsteps] output rows complete after step b
 };
 
 struct Strip5 {                     // one column strip of a plane kind
@@ -182,22 +193,21 @@ struct Strip5 {                     // one column strip of a plane kind
     int32_t pad_;
     int32_t ent0[4], nent[4];       // each wave's H entries
     int32_t x0[DTS_MAX_OUTPUTS];    // first output column per rendition (multiple of 16)
-    int32_t quads[kL5MaxUnits];     // V lane tasks per output row, per unit
+    int32_t nct[DTS_MAX_OUTPUTS];   // 16-column tiles per rendition
 };
 
 struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every rendition
     int32_t nplanes, nsteps, srcH;
     int32_t P;                      // staged row pitch, bytes (16 x odd: conflict-free A reads)
-    int32_t stage;                  // dword offset of the 2 stage buffers
-    int32_t nrings, nunits, nstrips;
-    int32_t R;                      // ring slots (row pairs) of every ring, a multiple of 8: pair p in slot p % R
-    int32_t M;                      // 8-pair blocks starting below M are also written at R + slot
-    int32_t pad_;
-    Ring5 ring[kL5MaxRings];
-    Unit5 unit[kL5MaxUnits];
+    int32_t stage;                  // byte offset of the 2 stage buffers
+    int32_t nrings, nrungs, nstrips;
+    Ring5 ring[kL5MaxRings];        // rendition r, plane p: ring[r * nplanes + p]
+    Out5 out[DTS_MAX_OUTPUTS];
     const Strip5 *strips;
     const Ent5 *ents;
-    const uint32_t *bfrag;
+    const uint32_t *bfrag;          // H then V fragment pairs, 512 dwords each
+    const VEnt5 *vsched;            // the V row groups of every step, step after step
+    const int4 *vstep;              // [nsteps + 1]: {first group, end, first group's bfrag, its nkb}
 };
 
 struct Job5 {
@@ -207,8 +217,7 @@ struct Job5 {
 struct Ladder5Params {
     DevPlanes src;
     DevPlanes dst[kMaxRungs];
-    int32_t dst_fmt[kMaxRungs];
-    int32_t njobs, nframes, nq, lds_dw;
+    int32_t njobs, nframes, nq, pad_;
     const Job5 *jobs;
     const Kind5 *kinds;
     unsigned int *queue;

@@ -92,15 +92,14 @@ struct Plan5In {
 };
 
 struct Plan5Kind {
-    int nplanes = 1, nsteps = 0, P = 0, stage = 0, nrings = 0, nunits = 0, lds_dw = 0, strip_width = 0;
-    int R = 0, M = 0;
+    int nplanes = 1, nsteps = 0, P = 0, stage = 0, nrings = 0, lds_bytes = 0, strip_width = 0;
     Ring5 ring[kL5MaxRings]{};
-    Unit5 unit[kL5MaxUnits]{};
+    Out5 out[DTS_MAX_OUTPUTS]{};
     std::vector<Strip5> strips;
     std::vector<Ent5> ents;
-    std::vector<uint32_t> bfrag;
-    std::vector<std::vector<int32_t>> vslot, vlim;   // per rendition
-    std::vector<std::vector<uint32_t>> vcoef;
+    std::vector<uint32_t> bfrag;     // H then V fragment pairs
+    std::vector<VEnt5> vsched;
+    std::vector<int32_t> vstep;      // [nsteps + 1][4]
 };
 
 // false: the geometry / format does not fit k_ladder5 (the kind then runs on v4 / v3)

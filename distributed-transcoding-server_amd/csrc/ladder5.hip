@@ -1,6 +1,6 @@
 // ladder5.hip -- k_ladder5, the v5 ladder kernel: every rendition of an
-// 8-bit 4:2:0 source in one persistent launch, the horizontal FIR on the
-// matrix cores.
+// 8-bit 4:2:0 source in one persistent launch, both FIR passes on the
+// matrix cores (v_mfma_i32_16x16x64_i8).
 //
 // Same arithmetic as libswscale hScale8To15_c -> yuv2planeX_8_c /
 // yuv2nv12cX_c under SWS_BITEXACT|SWS_ACCURATE_RND (FFmpeg 4.4; bit-exact,
@@ -11,25 +11,47 @@
 //    walked top to bottom in steps of 16 source rows.  Each step's rows are
 //    staged once in LDS (src ^ 0x80, i.e. the sample - 128 as i8) and read by
 //    every rendition, so the source is fetched from HBM once per frame;
-//  * H: a 16-output tile of one rendition over 16 source rows is one
-//    v_mfma_i32_16x16x64_i8 per 64-column K block and tap half: the int16
-//    taps c = 256 hi + lo (hi, lo signed bytes) are the B operands (held in
-//    VGPRs for the whole walk), the staged rows the A operand, so
-//      sum(src * c) = 256 sum(src' hi) + sum(src' lo) + 128 * 16384
-//    exactly in i32 (src' = src - 128; every row's taps sum to 1 << 14);
-//    then FFMIN(val >> 7, 32767) by v_cvt_pk_i16_i32 into the int16x2 row
-//    pairs of a per-rendition LDS ring;
-//  * V: lane = 4 output columns of one row (nv12 chroma: 2 columns of U and
-//    V), v_dot2_i32_i16 over the ring's row pairs (quad-major ring: the 4
-//    columns of a pair are one ds_read_b128, consecutive pairs 16 B apart,
-//    so a window is immediate offsets; slots [0, mirror) are also written
-//    past the ring's end so no window wraps), then + 64 << 12 (flat dither),
-//    v_ashr_pk_u8_i32 (>> 19, clip to u8) and one dword store per lane.
-//  * One barrier per step: H(b+1) of one wave overlaps V(b) of another (the
-//    planner sizes the ring so their slots never meet).
+//  * H: a 16-output tile of one rendition over 16 source rows is one MFMA per
+//    64-column K block and tap half: the int16 taps c = 256 hi + lo (signed
+//    bytes) are the B operands (held in VGPRs for the whole walk), the staged
+//    rows the A operand, so sum(src * c) = 256 sum(src' hi) + sum(src' lo) +
+//    128 * 16384 exactly in i32; FFMIN(val >> 7, 32767) (v_cvt_pk_i16_i32),
+//    and the int16 result y goes to the rendition's ring as two column-major
+//    byte planes, y >> 8 and (y & 255) ^ 0x80;
+//  * V: 16 output rows x 16 columns of a rendition are out^T = H^T C^T: the
+//    ring bytes (A: 16 columns x 64 source rows) times the V taps split the
+//    same way (B: 64 source rows x 16 output rows), four MFMAs per K block,
+//      sum(c y) = 65536 hh + 256 (hl + lh) + ll + 128 * 4096,
+//    then + 64 << 12 (flat dither), v_ashr_pk_u8_i32 (>> 19, clip to u8): each
+//    lane holds 4 consecutive columns of one row, one dword store (nv12
+//    chroma: U and V interleaved, 8 bytes);
+//  * one barrier per step: H(b+1) of one wave overlaps V(b) of another (the
+//    planner sizes each ring so their rows never meet).
 #include "dts_internal.h"
 
+#ifndef DTS_L5_ABLATE
+#define DTS_L5_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads, 8 skip V stores,
+                            // 16 skip the H epilogue (MFMAs kept)
+#endif
+
+#ifndef DTS_L5_STAMP
+#define DTS_L5_STAMP 0      // diagnostic builds only: per-phase s_memtime sums (tools/stamp5.py)
+#endif
+
 namespace dts {
+
+#if DTS_L5_STAMP
+// [phase]: cycles summed over every wave and step; [15]: steps
+__device__ unsigned long long g_l5_stamp[16];
+#define L5_STAMP(k)                                                        \
+    do {                                                                   \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
+        st_acc[k] += t_ - st_last;                                         \
+        st_last = t_;                                                      \
+    } while (0)
+#else
+#define L5_STAMP(k) (void)0
+#endif
 
 namespace {
 
@@ -45,10 +67,6 @@ typedef __attribute__((address_space(1))) uint8_t g_u8;
 
 __device__ __forceinline__ int uni5(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c)
-{
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, a), __builtin_bit_cast(short2v, b), c, false);
-}
 
 // wave-uniform struct / field read through the constant address space (s_load)
 template <class T>
@@ -67,10 +85,6 @@ __device__ __forceinline__ u32x2 lds_rd64(const uint32_t *lds, uint32_t byte)
 {
     return *reinterpret_cast<const u32x2 *>(reinterpret_cast<const uint8_t *>(lds) + byte);
 }
-__device__ __forceinline__ u32x4 lds_rd128(const uint32_t *lds, uint32_t byte)
-{
-    return *reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(lds) + byte);
-}
 __device__ __forceinline__ uint32_t *lds_at(uint32_t *lds, uint32_t byte)
 {
     return reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + byte);
@@ -84,30 +98,30 @@ __device__ __forceinline__ uint32_t pack_h(int hi, int lo, int hi2, int lo2)
 }
 
 struct Walk5 {
-    int nplanes, nsteps, srcH, Pb, stage_b, R, M, nunits;
+    int nplanes, nsteps, srcH, Pb, stage_b;
     int L, cpr, ne;
     int lane, wave, t;
 };
 
-// This thread's staging loads of a step: kL5MaxLoads 16-B chunks.
+// This thread's staging loads of a step: kL5MaxLoads 16-B source chunks.
 struct Loads5 {
     __amdgpu_buffer_rsrc_t rs[2];   // load planes (planar chroma: U, V)
-    int64_t pitch[2];
+    uint32_t pitch[2];
     uint32_t col[kL5MaxLoads];      // byte offset of the chunk in its source row
     int row[kL5MaxLoads];           // staged row (0..15), -1 = no chunk
     uint32_t dst[kL5MaxLoads];      // LDS byte offset of the chunk in stage buffer 0
     int nlp;                        // load planes
 };
 
-template <int SRC>
-__device__ __forceinline__ void issue_loads(const Loads5 &ld, int b, int srcH, u32x4 (&pre)[kL5MaxLoads])
+__device__ __forceinline__ void issue_loads(const Loads5 &ld, int b, const Walk5 &W, u32x4 (&pre)[kL5MaxLoads])
 {
+    if (b >= W.nsteps || (DTS_L5_ABLATE & 4)) return;
 #pragma unroll
     for (int k = 0; k < kL5MaxLoads; ++k) {
         const int lp = ld.nlp == 2 ? (k >> 1) : 0;
         if (ld.row[k] >= 0) {
-            const int r = min(kL5Rows * b + ld.row[k], srcH - 1);
-            const uint32_t off = (uint32_t)r * (uint32_t)ld.pitch[lp] + ld.col[k];
+            const int r = min(kL5Rows * b + ld.row[k], W.srcH - 1);
+            const uint32_t off = (uint32_t)r * ld.pitch[lp] + ld.col[k];
             pre[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(lp ? ld.rs[1] : ld.rs[0], off, 0, 0));
         }
     }
@@ -136,30 +150,117 @@ __device__ __forceinline__ void store_stage(uint32_t *lds, const Loads5 &ld, int
     }
 }
 
-// step b's V rows of every unit -> V staging buffer (b & 1): per row its ring slot, then np4 tap pairs
-__device__ __forceinline__ void stage_v(uint32_t *lds, const Kind5 *K, const Walk5 &W, int b)
+// H(b) of this wave: NE entries (K blocks), straight-line -- every A read, then
+// every MFMA, then the epilogues -- so the reads and the matrix pipe overlap.
+// A K block continuing a tile adds the previous block's sums (the lo MFMAs all
+// start at the bias: the continuation subtracts the extra one).  An epilogue
+// writes 4 rows of one column: their y >> 8 and (y & 255) ^ 0x80 bytes.
+template <int I0, int NE>
+__device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
+                                      const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
+                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t fl,
+                                      uint32_t boff, v4i &ch, v4i &cl)
 {
-    for (int u = 0; u < W.nunits; ++u) {
-        const Unit5 *U = K->unit + u;
-        const int32_t *vlim = kld(&U->vlim);
-        const int vlo = b > 0 ? kld(vlim + b - 1) : 0, vhi = kld(vlim + b);
-        const int np4 = kld(&U->np4), vco = kld(&U->vco), vdw = kld(&U->vco_dw);
-        const int stride = 4 + np4;
-        uint32_t *dst = lds + vco + (b & 1) * vdw;
-        const int32_t *vslot = kld(&U->vslot);
-        const uint32_t *vcoef = kld(&U->vcoef);
-        for (int i = W.t; i < vhi - vlo; i += 256) {
-            const int y = vlo + i;
-            dst[i * stride] = (uint32_t)vslot[y];
-            const u32x4 *c = reinterpret_cast<const u32x4 *>(vcoef + (int64_t)y * np4);
-            for (int g = 0; g < np4 / 4; ++g) *reinterpret_cast<u32x4 *>(dst + i * stride + 4 + 4 * g) = c[g];
+    const v4i zero = {0, 0, 0, 0}, bias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
+    v4i a[NE], ah[NE], al[NE];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        const u32x2 x = lds_rd64(lds, aad[I0 + i] + boff), y = lds_rd64(lds, aad[I0 + i] + boff + 32);
+        a[i] = __builtin_bit_cast(v4i, (u32x4){x.x, x.y, y.x, y.y});
+    }
+    __builtin_amdgcn_sched_barrier(0);                     // every A read in flight before the first MFMA
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        ah[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bh[I0 + i], zero, 0, 0, 0);
+        al[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bl[I0 + i], bias, 0, 0, 0);
+    }
+    if (DTS_L5_ABLATE & 16) {
+#pragma unroll
+        for (int i = 0; i < NE; ++i) asm volatile("" ::"v"(ah[i]), "v"(al[i]));
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        const uint32_t f = (fl >> (2 * (I0 + i))) & 3u;
+        if (!(f & 1u)) {                                   // continues the previous K block's tile
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                ah[i][r] += ch[r];
+                al[i][r] = al[i][r] + cl[r] - kL5Bias;
+            }
+        }
+        if (f & 2u) {
+            const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);    // rows 4g, 4g+1
+            const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);    // rows 4g+2, 4g+3
+            *lds_at(lds, whi[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
+            *lds_at(lds, wlo[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
+        } else {
+            ch = ah[i];
+            cl = al[i];
         }
     }
+}
+
+// H(b) of this wave: NE entries (K blocks) in halves of up to 4 -- every A read
+// of a half, then its MFMAs, then its epilogues -- so the reads and the matrix
+// pipe overlap.  A K block continuing a tile adds the previous block's sums
+// (the lo MFMAs all start at the bias: the continuation subtracts the extra
+// one).  An epilogue writes 4 rows of one column: their y >> 8 and
+// (y & 255) ^ 0x80 bytes.
+template <int NE>
+__device__ __forceinline__ void hstep(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
+                                      const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
+                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t fl,
+                                      uint32_t boff)
+{
+    v4i ch = {0, 0, 0, 0}, cl = {0, 0, 0, 0};
+    hpart<0, (NE < 4 ? NE : 4)>(lds, bh, bl, aad, whi, wlo, pos, fl, boff, ch, cl);
+    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1)>(lds, bh, bl, aad, whi, wlo, pos, fl, boff, ch, cl);
+}
+
+// V of one (row group, 16-column tile, plane): 4 MFMAs per K block, then the
+// 4 output bytes (columns 4g..4g+3 of output row lane & 15) packed in a dword
+__device__ __forceinline__ uint32_t vtile(const uint32_t *lds, const Ring5 &g, int col, int w0m, int nkb,
+                                          const v4i (&vh)[kL5MaxVkb], const v4i (&vl)[kL5MaxVkb], int lane)
+{
+    const v4i zero = {0, 0, 0, 0}, vbias = {kL5VBias, kL5VBias, kL5VBias, kL5VBias};
+    v4i hh = zero, hl = zero, ll = vbias;
+    const uint32_t cb = (uint32_t)(col * g.CP);
+    const int rr = g.RR;
+#pragma unroll
+    for (int kb = 0; kb < kL5MaxVkb; ++kb) {
+        if (kb < nkb) {
+            int r0 = w0m + 64 * kb + 8 * (lane >> 4), r1 = r0 + 32;
+            r0 = r0 >= rr ? r0 - rr : r0;
+            r1 = r1 >= rr ? r1 - rr : r1;
+            const u32x2 h0 = lds_rd64(lds, (uint32_t)g.hi + cb + (uint32_t)r0);
+            const u32x2 h1 = lds_rd64(lds, (uint32_t)g.hi + cb + (uint32_t)r1);
+            const u32x2 l0 = lds_rd64(lds, (uint32_t)g.lo + cb + (uint32_t)r0);
+            const u32x2 l1 = lds_rd64(lds, (uint32_t)g.lo + cb + (uint32_t)r1);
+            const v4i ahi = __builtin_bit_cast(v4i, (u32x4){h0.x, h0.y, h1.x, h1.y});
+            const v4i alo = __builtin_bit_cast(v4i, (u32x4){l0.x, l0.y, l1.x, l1.y});
+            hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahi, vh[kb], hh, 0, 0, 0);
+            hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahi, vl[kb], hl, 0, 0, 0);
+            hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(alo, vh[kb], hl, 0, 0, 0);
+            ll = __builtin_amdgcn_mfma_i32_16x16x64_i8(alo, vl[kb], ll, 0, 0, 0);
+        }
+    }
+    int v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (((hh[i] << 8) + hl[i]) << 8) + ll[i];
+    // av_clip_uint8(val >> 19) of 4 columns, packed
+    const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(v[0], v[1], 19);
+    const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(v[2], v[3], 19);
+    return (lo & 0xffffu) | (hi << 16);
 }
 
 // One output store of 4 bytes at byte column x of a row (fewer at the plane's right edge).
 __device__ __forceinline__ void store4(uint64_t row, int x, int ncols, uint32_t w)
 {
+    if (DTS_L5_ABLATE & 8) {
+        asm volatile("" ::"v"(w));
+        return;
+    }
     if (ncols >= 4) {
         *GP5(g_u32, row + x) = w;
     } else {
@@ -167,83 +268,125 @@ __device__ __forceinline__ void store4(uint64_t row, int x, int ncols, uint32_t 
     }
 }
 
-// V pass of step b for this wave
-__device__ __forceinline__ void vpass(uint32_t *lds, const Ladder5Params &P, const Kind5 *K, const Strip5 *S,
-                                      const Walk5 &W, int frame, int b)
+// V work of one step, fetched before the barrier it runs after: the fragments
+// of its first row group (their latency hides under the barrier wait)
+struct VPrep5 {
+    int e0, e1;
+    v4i vh[kL5MaxVkb], vl[kL5MaxVkb];
+};
+
+__device__ __forceinline__ void vfrags(const uint32_t *bf, int frag, int nkb, int lane, v4i (&vh)[kL5MaxVkb],
+                                       v4i (&vl)[kL5MaxVkb])
 {
-    int rot = 0;                                           // passes handed out so far (round robin over waves)
-    for (int u = 0; u < W.nunits; ++u) {
-        const Unit5 *U = K->unit + u;
-        const int32_t *vlim = kld(&U->vlim);
-        const int vlo = b > 0 ? kld(vlim + b - 1) : 0, nr = kld(vlim + b) - vlo;
-        if (nr <= 0) continue;
-        const int Q = kld(&S->quads[u]);
-        const int tasks = nr * Q;
-        const int npass = (tasks + 63) >> 6;
-        const int first = (W.wave - rot) & 3;
-        rot += npass;
-        if (first >= npass || Q <= 0) continue;
-        const int mode = kld(&U->mode), np4 = kld(&U->np4), vdw = kld(&U->vco_dw);
-        const int rung = kld(&U->rung), dstW = kld(&U->dstW), plane = kld(&U->plane);
-        const int x0 = kld(&S->x0[rung]);
-        const Ring5 *g0 = K->ring + kld(&U->ring0), *g1 = K->ring + kld(&U->ring1);
-        const int r0lds = kld(&g0->lds), r0qs = kld(&g0->qstride), r1lds = kld(&g1->lds);
-        const uint32_t vbase = (uint32_t)(kld(&U->vco) + (b & 1) * vdw);
-        const int stride = 4 + np4;
-        const DevPlanes dst = P.dst[rung];
-        const uint64_t pbase = (plane == 0 ? dst.data[0] : (plane == 1 ? dst.data[1] : dst.data[2])) +
-                               (uint64_t)frame * dst.fstride;
-        const int64_t pitch = plane == 0 ? dst.pitch[0] : (plane == 1 ? dst.pitch[1] : dst.pitch[2]);
-        const float rq = 1.0f / (float)Q;
-        for (int p = first; p < npass; p += 4) {
-            const int task = p * 64 + W.lane;
-            const int row = (int)(((float)task + 0.5f) * rq);
-            const int q = task - row * Q;
-            if (task >= tasks) continue;
-            const uint32_t vrow = 4u * (vbase + (uint32_t)(row * stride));
-            const int slot = (int)lds[vrow / 4];
-            int a0 = 64 << 12, a1 = 64 << 12, a2 = 64 << 12, a3 = 64 << 12;
-            if (mode == 0) {
-                uint32_t ra = 4u * (uint32_t)(r0lds + q * r0qs + slot * 4);
-                for (int g = 0; g < np4; g += 4, ra += 64) {
-                    const u32x4 c = lds_rd128(lds, vrow + 16 + 4 * g);
-                    const u32x4 d0 = lds_rd128(lds, ra), d1 = lds_rd128(lds, ra + 16);
-                    const u32x4 d2 = lds_rd128(lds, ra + 32), d3 = lds_rd128(lds, ra + 48);
-                    a0 = dot2(d0.x, c.x, a0); a1 = dot2(d0.y, c.x, a1); a2 = dot2(d0.z, c.x, a2); a3 = dot2(d0.w, c.x, a3);
-                    a0 = dot2(d1.x, c.y, a0); a1 = dot2(d1.y, c.y, a1); a2 = dot2(d1.z, c.y, a2); a3 = dot2(d1.w, c.y, a3);
-                    a0 = dot2(d2.x, c.z, a0); a1 = dot2(d2.y, c.z, a1); a2 = dot2(d2.z, c.z, a2); a3 = dot2(d2.w, c.z, a3);
-                    a0 = dot2(d3.x, c.w, a0); a1 = dot2(d3.y, c.w, a1); a2 = dot2(d3.z, c.w, a2); a3 = dot2(d3.w, c.w, a3);
-                }
-                // av_clip_uint8(val >> 19) of 4 columns, packed
-                const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(a0, a1, 19);
-                const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(a2, a3, 19);
-                const int x = x0 + 4 * q;
-                store4(pbase + (uint64_t)((int64_t)(vlo + row) * pitch), x, dstW - x, (lo & 0xffffu) | (hi << 16));
+    const u32x4 *f = reinterpret_cast<const u32x4 *>(bf + (size_t)frag * 512);
+    vh[0] = __builtin_bit_cast(v4i, f[lane]);
+    vl[0] = __builtin_bit_cast(v4i, f[64 + lane]);
+    vh[1] = vl[1] = (v4i){0, 0, 0, 0};
+    if (nkb > 1) {
+        vh[1] = __builtin_bit_cast(v4i, f[128 + lane]);
+        vl[1] = __builtin_bit_cast(v4i, f[192 + lane]);
+    }
+}
+
+// Kernel arguments are read through the kernarg segment pointer with scalar
+// loads: indexing the by-value parameter with a runtime rendition or plane
+// makes the compiler copy it to scratch.
+__device__ __forceinline__ const Ladder5Params *kargs()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (const Ladder5Params *)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    return nullptr;
+#endif
+}
+
+// Per-item rendition table (LDS bytes 16..): wave r < nrungs fills rendition r's
+// 16 dwords {x0, nct, pitch Y/U/V, 0, plane base lo/hi Y/U/V of this frame, 0...}
+__device__ __forceinline__ void rung_table(uint32_t *lds, const Strip5 *S, int nrungs, int frame, const Walk5 &W)
+{
+    const int r = W.wave;
+    if (r >= nrungs || W.lane >= 16) return;
+    const DevPlanes d = kld(&kargs()->dst[r]);
+    const uint64_t fb = (uint64_t)frame * d.fstride;
+    const uint64_t b0 = d.data[0] + fb, b1 = d.data[1] + fb, b2 = d.data[2] + fb;
+    const int k = W.lane;
+    uint32_t v = 0;
+    v = k == 0 ? (uint32_t)kld(&S->x0[r]) : v;
+    v = k == 1 ? (uint32_t)kld(&S->nct[r]) : v;
+    v = k == 2 ? (uint32_t)d.pitch[0] : v;
+    v = k == 3 ? (uint32_t)d.pitch[1] : v;
+    v = k == 4 ? (uint32_t)d.pitch[2] : v;
+    v = k == 6 ? (uint32_t)b0 : v;
+    v = k == 7 ? (uint32_t)(b0 >> 32) : v;
+    v = k == 8 ? (uint32_t)b1 : v;
+    v = k == 9 ? (uint32_t)(b1 >> 32) : v;
+    v = k == 10 ? (uint32_t)b2 : v;
+    v = k == 11 ? (uint32_t)(b2 >> 32) : v;
+    lds[4 + 16 * r + k] = v;
+}
+
+// V of one row group: its 16-column tiles dealt round robin over the 4 waves
+// (pitches and plane bases of this frame from the rendition table)
+__device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, const VEnt5 &VE, const v4i (&vh)[kL5MaxVkb],
+                                       const v4i (&vl)[kL5MaxVkb], int first, int nct, int x0, uint32_t pY,
+                                       uint32_t pU, uint32_t pV, uint64_t bY, uint64_t bU, uint64_t bV)
+{
+    const int n = W.lane & 15, g = W.lane >> 4;
+    const int y = 16 * VE.G + n;
+    const bool rowok = n < VE.rows;
+    if (W.nplanes == 1) {
+        const uint64_t orow = bY + (uint64_t)y * pY;
+        for (int ct = first; ct < nct; ct += 4) {
+            const uint32_t w = vtile(lds, VE.ring0, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
+            const int x = x0 + 16 * ct + 4 * g;
+            if (rowok) store4(orow, x, VE.dstW - x, w);
+        }
+    } else {
+        const Ring5 g1 = {VE.hi1, VE.lo1, VE.ring0.CP, VE.ring0.RR};
+        const bool nv = VE.fmt == DTS_FMT_NV12;
+        const uint64_t urow = bU + (uint64_t)y * pU;
+        const uint64_t vrow = bV + (uint64_t)y * pV;
+        for (int ct = first; ct < nct; ct += 4) {
+            const uint32_t wu = vtile(lds, VE.ring0, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
+            const uint32_t wv = vtile(lds, g1, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
+            const int x = x0 + 16 * ct + 4 * g;
+            if (!rowok) continue;
+            if (!nv) {
+                store4(urow, x, VE.dstW - x, wu);
+                store4(vrow, x, VE.dstW - x, wv);
             } else {
-                // nv12 chroma: columns 2q', 2q'+1 of U (ring0) and V (ring1); a0/a1 = U, a2/a3 = V
-                const uint32_t qo = 4u * (uint32_t)((q >> 1) * r0qs + slot * 4 + 2 * (q & 1));
-                uint32_t ru = 4u * (uint32_t)r0lds + qo, rv = 4u * (uint32_t)r1lds + qo;
-                for (int g = 0; g < np4; g += 4, ru += 64, rv += 64) {
-                    const u32x4 c = lds_rd128(lds, vrow + 16 + 4 * g);
-                    const u32x2 u0 = lds_rd64(lds, ru), u1 = lds_rd64(lds, ru + 16);
-                    const u32x2 u2 = lds_rd64(lds, ru + 32), u3 = lds_rd64(lds, ru + 48);
-                    const u32x2 v0 = lds_rd64(lds, rv), v1 = lds_rd64(lds, rv + 16);
-                    const u32x2 v2 = lds_rd64(lds, rv + 32), v3 = lds_rd64(lds, rv + 48);
-                    a0 = dot2(u0.x, c.x, a0); a1 = dot2(u0.y, c.x, a1); a2 = dot2(v0.x, c.x, a2); a3 = dot2(v0.y, c.x, a3);
-                    a0 = dot2(u1.x, c.y, a0); a1 = dot2(u1.y, c.y, a1); a2 = dot2(v1.x, c.y, a2); a3 = dot2(v1.y, c.y, a3);
-                    a0 = dot2(u2.x, c.z, a0); a1 = dot2(u2.y, c.z, a1); a2 = dot2(v2.x, c.z, a2); a3 = dot2(v2.y, c.z, a3);
-                    a0 = dot2(u3.x, c.w, a0); a1 = dot2(u3.y, c.w, a1); a2 = dot2(v3.x, c.w, a2); a3 = dot2(v3.y, c.w, a3);
-                }
-                const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(a0, a2, 19);   // U0 V0
-                const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(a1, a3, 19);   // U1 V1
-                const int c0 = x0 + 2 * q;
-                const uint64_t r = pbase + (uint64_t)((int64_t)(vlo + row) * pitch);
-                if (c0 + 2 <= dstW)
-                    *GP5(g_u32, r + 2 * c0) = (lo & 0xffffu) | (hi << 16);
-                else
-                    *GP5(g_u16, r + 2 * c0) = (uint16_t)lo;
+                // yuv2nv12cX: U0 V0 U1 V1 U2 V2 U3 V3
+                const uint32_t q0 = __builtin_amdgcn_perm(wv, wu, 0x05010400u);
+                const uint32_t q1 = __builtin_amdgcn_perm(wv, wu, 0x07030602u);
+                store4(urow, 2 * x, 2 * (VE.dstW - x), q0);
+                store4(urow, 2 * x + 4, 2 * (VE.dstW - x) - 4, q1);
             }
         }
+    }
+}
+
+// V of a step for this wave; the first group's fragments came from vprep
+__device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const Walk5 &W, const uint32_t *bf,
+                                     VPrep5 &V)
+{
+    int rot = 0;
+    for (int e = V.e0; e < V.e1; ++e) {
+        const VEnt5 VE = kld(K->vsched + e);
+        const uint32_t *tb = lds + 4 + 16 * VE.rung;
+        const u32x4 t0 = *reinterpret_cast<const u32x4 *>(tb);        // x0, nct, pitch Y, pitch U
+        const u32x4 t1 = *reinterpret_cast<const u32x4 *>(tb + 4);    // pitch V, 0, base Y
+        const u32x4 t2 = *reinterpret_cast<const u32x4 *>(tb + 8);    // base U, base V
+        const int nct = uni5((int)t0.y);
+        const int first = (W.wave - rot) & 3;
+        rot += nct;
+        if (first >= nct) continue;
+        if (e != V.e0) vfrags(bf, VE.bfrag, VE.nkb, W.lane, V.vh, V.vl);
+        auto u64 = [](uint32_t lo, uint32_t hi) {
+            return ((uint64_t)(uint32_t)uni5((int)hi) << 32) | (uint32_t)uni5((int)lo);
+        };
+        vgroup(lds, W, VE, V.vh, V.vl, first, nct, uni5((int)t0.x), (uint32_t)uni5((int)t0.z),
+               (uint32_t)uni5((int)t0.w), (uint32_t)uni5((int)t1.x), u64(t1.z, t1.w), u64(t2.x, t2.y),
+               u64(t2.z, t2.w));
     }
 }
 
@@ -259,10 +402,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     W.nsteps = kld(&K->nsteps);
     W.srcH = kld(&K->srcH);
     W.Pb = kld(&K->P);
-    W.stage_b = 4 * kld(&K->stage);
-    W.R = kld(&K->R);
-    W.M = kld(&K->M);
-    W.nunits = kld(&K->nunits);
+    W.stage_b = kld(&K->stage);
     const Strip5 *S = kld(&K->strips) + J.strip;
     W.L = kld(&S->L);
     W.cpr = kld(&S->cpr);
@@ -275,27 +415,40 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     // ---- this wave's H entries: B fragments in VGPRs, per-lane LDS addresses ----
     const int g = W.lane >> 4, n = W.lane & 15;
     v4i bh[kL5Ent], bl[kL5Ent];
-    uint32_t aad[kL5Ent], wad[kL5Ent];
+    uint32_t aad[kL5Ent], whi[kL5Ent], wlo[kL5Ent], pos[kL5Ent], rr[kL5Ent];
     uint32_t fl = 0;
 #pragma unroll
     for (int i = 0; i < kL5Ent; ++i) {
         bh[i] = bl[i] = (v4i){0, 0, 0, 0};
-        aad[i] = wad[i] = 0;
+        aad[i] = whi[i] = wlo[i] = pos[i] = 0;
+        rr[i] = 16;
         if (i < W.ne) {
             const Ent5 E = kld(ents + i);
             const u32x4 *f = reinterpret_cast<const u32x4 *>(bf + (size_t)E.bfrag * 512);
             bh[i] = __builtin_bit_cast(v4i, f[W.lane]);
             bl[i] = __builtin_bit_cast(v4i, f[64 + W.lane]);
             aad[i] = (uint32_t)(W.stage_b + E.plane * kL5Rows * W.Pb + n * W.Pb + E.soff + 8 * g);
-            const Ring5 *rg = K->ring + E.ring;
-            const int col = E.col0 + n;
-            wad[i] = 4u * (uint32_t)(kld(&rg->lds) + (col >> 2) * kld(&rg->qstride) + 8 * g + (col & 3));
+            const Ring5 rg = kld(K->ring + E.ring);
+            const uint32_t cb = (uint32_t)((E.col0 + n) * rg.CP + 4 * g);
+            whi[i] = (uint32_t)rg.hi + cb;
+            wlo[i] = (uint32_t)rg.lo + cb;
+            rr[i] = (uint32_t)rg.RR;
             fl |= (uint32_t)(E.flags & 3) << (2 * i);
         }
     }
     fl = (uint32_t)uni5((int)fl);
+    // ring row of each entry's step: kept in VGPRs (the SGPRs are the scarce file here)
+#pragma unroll
+    for (int i = 0; i < kL5Ent; ++i) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(pos[i]) : "v"(pos[i]));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rr[i]) : "v"(rr[i]));
+    }
+    // make the B fragments resident here: otherwise the compiler's wait for them sits
+    // inside the step loop, where it would also drain every prefetch load each step
+#pragma unroll
+    for (int i = 0; i < kL5Ent; ++i) asm volatile("" ::"v"(bh[i]), "v"(bl[i]));
 
-    // ---- staging loads of this thread ----
+    // ---- this thread's staging loads ----
     Loads5 ld;
     {
         const int nlp = (SRC == kSrcPlanar8 && chroma) ? 2 : 1;
@@ -304,13 +457,12 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
         for (int lp = 0; lp < 2; ++lp) {
             const int spl = chroma ? (nv12c ? 1 : 1 + lp) : 0;           // source plane
             const int sp = lp < nlp ? spl : 0;
-            const uint64_t base = (sp == 0 ? P.src.data[0] : (sp == 1 ? P.src.data[1] : P.src.data[2])) +
-                                  (uint64_t)frame * P.src.fstride;
-            const int64_t pitch = sp == 0 ? P.src.pitch[0] : (sp == 1 ? P.src.pitch[1] : P.src.pitch[2]);
+            const uint64_t base = kld(&kargs()->src.data[sp]) + (uint64_t)frame * kld(&kargs()->src.fstride);
+            const int64_t pitch = kld(&kargs()->src.pitch[sp]);
             const uint32_t lo = (uint32_t)uni5((int)(uint32_t)base), hi = (uint32_t)uni5((int)(uint32_t)(base >> 32));
             ld.rs[lp] = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0,
                                                           uni5((int)(pitch * W.srcH)), 0x00020000);
-            ld.pitch[lp] = pitch;
+            ld.pitch[lp] = (uint32_t)pitch;
         }
         const int per = kL5Rows * W.cpr;                                  // chunks per load plane
         const float rc = 1.0f / (float)W.cpr;
@@ -330,69 +482,70 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
         }
     }
 
-    // ---- prologue: block 0 -> stage 0, block 1 in flight ----
+    rung_table(lds, S, kld(&K->nrungs), frame, W);
+
+    // ---- prologue: block 0 -> stage 0; block 1 in flight ----
     u32x4 pre[kL5MaxLoads];
 #pragma unroll
     for (int k = 0; k < kL5MaxLoads; ++k) pre[k] = (u32x4){0, 0, 0, 0};
-    issue_loads<SRC>(ld, 0, W.srcH, pre);
+    issue_loads(ld, 0, W, pre);
     store_stage<SRC>(lds, ld, 0, W, pre, nv12c);
-    if (W.nsteps > 1) issue_loads<SRC>(ld, 1, W.srcH, pre);
+    issue_loads(ld, 1, W, pre);
     __syncthreads();
 
-    const v4i zero = {0, 0, 0, 0}, bias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
-    int sb = 0;                                            // ring slot of step b's first row pair = (8 b) % R
-    for (int b = 0; b < W.nsteps; ++b) {
-        // ---- H(b): MFMA tiles of this wave -> rings ----
+    // iteration b (after barrier b - 1: stage b written, H(b - 1) done): V(b - 1), whose
+    // fragments were fetched before the barrier; H(b); stage block b + 1 and issue the
+    // loads of b + 2 (the wait for the previous loads comes after H(b), so it does not
+    // wait on V's stores, which count in the same vmcnt); fetch V(b)'s fragments (its
+    // step record came one iteration earlier); barrier b.  V(b - 1) reads rows H(b) may
+    // be writing elsewhere in the ring: the planner's RR keeps them apart.
+    VPrep5 V;
+    V.e0 = V.e1 = 0;
+    int4 vs = kld(kld(&K->vstep));                          // step 0's record
+#if DTS_L5_STAMP
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
+    for (int b = 0; b <= W.nsteps; ++b) {
+        if (b > 0 && !(DTS_L5_ABLATE & 2)) vrun(lds, K, W, bf, V);
+        L5_STAMP(0);
+        if (b == W.nsteps) break;
         {
             const uint32_t boff = (uint32_t)((b & 1) * W.nplanes * kL5Rows * W.Pb);
-            const uint32_t soff = (uint32_t)(16 * sb);
-            const bool mir = sb < W.M;
-            const uint32_t moff = (uint32_t)(16 * W.R);
-            // every K block starts fresh accumulators (independent MFMA chains); a
-            // tile's earlier K blocks are carried in ch / cl and added at its last one
-            v4i ch = zero, cl = zero;
+            switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
+#define DTS_H5(k) \
+    case k: hstep<k>(lds, bh, bl, aad, whi, wlo, pos, fl, boff); break;
+                DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
+#undef DTS_H5
+            default:
+                break;
+            }
 #pragma unroll
-            for (int i = 0; i < kL5Ent; ++i) {
-                if (i < W.ne) {
-                    const uint32_t f = (fl >> (2 * i)) & 3u;
-                    const u32x2 x = lds_rd64(lds, aad[i] + boff), y = lds_rd64(lds, aad[i] + boff + 32);
-                    const v4i a = __builtin_bit_cast(v4i, (u32x4){x.x, x.y, y.x, y.y});
-                    v4i ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bh[i], zero, 0, 0, 0);
-                    v4i al = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bl[i], (f & 1u) ? bias : zero, 0, 0, 0);
-                    if (!(f & 1u)) {
-                        ah += ch;
-                        al += cl;
-                    }
-                    if (f & 2u) {
-                        const uint32_t p0 = pack_h(ah.x, al.x, ah.y, al.y);    // rows 4g, 4g+1
-                        const uint32_t p1 = pack_h(ah.z, al.z, ah.w, al.w);    // rows 4g+2, 4g+3
-                        uint32_t *w = lds_at(lds, wad[i] + soff);
-                        w[0] = p0;
-                        w[4] = p1;
-                        if (mir) {
-                            uint32_t *m = lds_at(lds, wad[i] + soff + moff);
-                            m[0] = p0;
-                            m[4] = p1;
-                        }
-                    } else {
-                        ch = ah;
-                        cl = al;
-                    }
-                }
+            for (int i = 0; i < kL5Ent; ++i) {                 // next step's rows: ring row (16 b) % RR
+                const uint32_t np = pos[i] + 16;
+                pos[i] = np >= rr[i] ? 0 : np;
             }
         }
-        // ---- V taps of step b, the next block's rows, the loads after it ----
-        stage_v(lds, K, W, b);
-        if (b + 1 < W.nsteps) {
-            store_stage<SRC>(lds, ld, b + 1, W, pre, nv12c);
-            if (b + 2 < W.nsteps) issue_loads<SRC>(ld, b + 2, W.srcH, pre);
+        L5_STAMP(1);
+        if (b + 1 < W.nsteps) store_stage<SRC>(lds, ld, b + 1, W, pre, nv12c);
+        L5_STAMP(2);
+        issue_loads(ld, b + 2, W, pre);
+        L5_STAMP(3);
+        if (!(DTS_L5_ABLATE & 2)) {
+            V.e0 = vs.x;
+            V.e1 = vs.y;
+            if (vs.x < vs.y) vfrags(bf, vs.z, vs.w, W.lane, V.vh, V.vl);
+            vs = kld(kld(&K->vstep) + b + 1);
         }
+        L5_STAMP(4);
         __syncthreads();
-        // ---- V(b) ----
-        vpass(lds, P, K, S, W, frame, b);
-        sb += 8;
-        if (sb >= W.R) sb -= W.R;
+        L5_STAMP(5);
     }
+#if DTS_L5_STAMP
+    if (W.lane == 0) {
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_l5_stamp[k], st_acc[k]);
+        atomicAdd(&g_l5_stamp[15], (unsigned long long)W.nsteps);
+    }
+#endif
 }
 
 } // namespace
@@ -444,6 +597,18 @@ hipError_t launch_ladder5(const Ladder5Params &p, int src_kind, int lds_bytes, i
     }
     return hipGetLastError();
 }
+
+#if DTS_L5_STAMP
+int ladder5_stamps(unsigned long long *out, bool reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l5_stamp), sizeof(g_l5_stamp)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_l5_stamp), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 16;
+}
+#endif
 
 int ladder5_blocks_per_cu(int src_kind, int lds_bytes)
 {

@@ -1,8 +1,8 @@
 // plan5.cpp -- host planning of the v5 ladder (ladder5.hip, dts_internal.h
-// "v5 ladder"): column strips, H tiles on the matrix cores, V rings and the
-// per-step V row lists.  The tables are the libswscale ones (filters.cpp
-// sws_build_filter = FFmpeg 4.4 utils.c initFilter), re-laid for
-// v_mfma_i32_16x16x64_i8; nothing here changes a tap.
+// "v5 ladder"): column strips, H tiles and V row groups on the matrix cores,
+// the H-output rings and the per-step V schedule.  The taps are the
+// libswscale ones (filters.cpp sws_build_filter = FFmpeg 4.4 utils.c
+// initFilter), re-laid for v_mfma_i32_16x16x64_i8; nothing here changes a tap.
 #include <algorithm>
 #include <cstring>
 
@@ -12,7 +12,7 @@ namespace dts {
 
 namespace {
 
-// first / last nonzero tap (source column) of output i
+// first / last nonzero tap (source column) of H output i
 void extent(const SwsFilter &f, int i, int &a, int &z)
 {
     a = f.pos[i];
@@ -26,13 +26,22 @@ void extent(const SwsFilter &f, int i, int &a, int &z)
         }
 }
 
-int tap(const SwsFilter &f, int i, int src)
+int htap(const SwsFilter &f, int i, int src)
 {
     const int j = src - f.pos[i];
     return (j >= 0 && j < f.size) ? f.coeff[(size_t)i * f.size + j] : 0;
 }
 
-struct Tile {                       // 16 outputs of one rendition
+// V tap of output row y on source row `row` (the packed pairs of filters.cpp pack_v)
+int vtap(const VTable &v, int y, int row)
+{
+    const int d = row - v.pos[y];
+    if (d < 0 || d >= 2 * v.nv) return 0;
+    const uint32_t w = v.coef[(size_t)y * v.nv + d / 2];
+    return (int16_t)(d & 1 ? w >> 16 : w & 0xffff);
+}
+
+struct Tile {                       // 16 H outputs of one rendition
     int base;                       // first staged column of its K blocks (multiple of 8)
     int nkb;                        // K blocks of 64 columns
     int centre;                     // strip assignment key
@@ -41,15 +50,40 @@ struct Tile {                       // 16 outputs of one rendition
 
 int round_up(int v, int a) { return (v + a - 1) / a * a; }
 
-} // namespace
+// 16 x odd >= v (column / row pitches whose 4-dword lane groups hit distinct banks)
+int pitch16odd(int v)
+{
+    int p = round_up(std::max(v, 16), 16);
+    if ((p / 16) % 2 == 0) p += 16;
+    return p;
+}
 
-// K order inside one lane's 16 A/B bytes (must match ladder5.hip a_frag):
-// bytes 0-7 = K block columns 8g..8g+7, bytes 8-15 = 32+8g..32+8g+7 (g = lane >> 4)
-static inline int kcol_of(int lane, int j)
+// K order inside one lane's 16 A/B bytes (ladder5.hip reads A this way):
+// bytes 0-7 = K block rows/columns 8g..8g+7, bytes 8-15 = 32+8g..32+8g+7 (g = lane >> 4)
+int kcol_of(int lane, int j)
 {
     const int g = lane >> 4;
     return j < 8 ? 8 * g + j : 32 + 8 * g + (j - 8);
 }
+
+// one fragment pair: tap(lane, k) split as 256 hi + lo (signed bytes); false if out of range
+template <class F>
+bool put_frag(std::vector<uint32_t> &bf, int frag, F tapf)
+{
+    uint8_t *hi = reinterpret_cast<uint8_t *>(bf.data() + (size_t)frag * 512);
+    uint8_t *lo = hi + 1024;
+    for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 16; ++j) {
+            const int c = tapf(lane, kcol_of(lane, j));
+            const int l = (int8_t)(c & 0xff), h = (c - l) >> 8;
+            if (h < -128 || h > 127) return false;
+            hi[lane * 16 + j] = (uint8_t)h;
+            lo[lane * 16 + j] = (uint8_t)l;
+        }
+    return true;
+}
+
+} // namespace
 
 bool plan5_kind(const Plan5In &in, Plan5Kind &out)
 {
@@ -57,6 +91,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
     const int nr = (int)in.rungs.size();
     if (nr < 1 || nr > DTS_MAX_OUTPUTS) return false;
     const int nplanes = in.chroma ? 2 : 1;
+    const int nsteps = (in.srcH + kL5Rows - 1) / kL5Rows;
     // ---- H tiles per rendition ---------------------------------------------
     std::vector<std::vector<Tile>> tiles(nr);
     int nfrag = 0;
@@ -87,61 +122,101 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             tiles[r].push_back(t);
         }
     }
-    // ---- B fragments: per K block a hi and a lo 1 KB fragment ----------------
-    out.bfrag.assign((size_t)nfrag * 2 * 256, 0);
+    // ---- V row groups per rendition: window, K blocks, ready step, fragments ----
+    struct Group { int rows, w0, nkb, step, frag; };
+    std::vector<std::vector<Group>> groups(nr);
+    std::vector<int> RR(nr, 32);
+    for (int r = 0; r < nr; ++r) {
+        const VTable &v = *in.rungs[r].v;
+        const int dstH = in.rungs[r].dstH;
+        for (int y = 0; y < dstH; ++y) {                                       // bias = 128 * 4096
+            int sum = 0;
+            for (int d = 0; d < 2 * v.nv; ++d) sum += vtap(v, y, v.pos[y] + d);
+            if (sum != 1 << 12) return false;
+        }
+        for (int G = 0; 16 * G < dstH; ++G) {
+            Group g{};
+            g.rows = std::min(16, dstH - 16 * G);
+            int a = 1 << 30, z = -1;
+            for (int y = 16 * G; y < 16 * G + g.rows; ++y)
+                for (int d = 0; d < 2 * v.nv; ++d)
+                    if (vtap(v, y, v.pos[y] + d)) {
+                        a = std::min(a, v.pos[y] + d);
+                        z = std::max(z, v.pos[y] + d);
+                    }
+            if (z < 0) return false;
+            g.w0 = a & ~7;
+            g.nkb = (z - g.w0) / 64 + 1;
+            if (g.nkb > kL5MaxVkb) return false;
+            g.step = std::min(z / kL5Rows, nsteps - 1);
+            // V(step) reads rows [w0, z] while H(step + 1) writes [16 (step + 1), 16 (step + 2))
+            RR[r] = std::max(RR[r], round_up(kL5Rows * (g.step + 2) - g.w0, 16));
+            g.frag = nfrag;
+            nfrag += g.nkb;
+            groups[r].push_back(g);
+        }
+        // the V A reads of a group cover w0 + [0, 64 nkb): with RR >= 64 nkb one
+        // conditional subtract wraps them (ladder5.hip vtile)
+        for (const Group &g : groups[r]) RR[r] = std::max(RR[r], 64 * g.nkb);
+        if (RR[r] > 4096) return false;
+    }
+    // ---- fragments: H (B = taps of 16 outputs over 64 source columns), V (B = taps of
+    // 16 output rows over 64 source rows)
+    out.bfrag.assign((size_t)nfrag * 512, 0);
     for (int r = 0; r < nr; ++r) {
         const SwsFilter &f = *in.rungs[r].fh;
         const int dstW = in.rungs[r].dstW;
         for (size_t ti = 0; ti < tiles[r].size(); ++ti) {
             const Tile &t = tiles[r][ti];
             for (int kb = 0; kb < t.nkb; ++kb) {
-                uint8_t *hi = reinterpret_cast<uint8_t *>(out.bfrag.data() + (size_t)(t.frag + kb) * 2 * 256);
-                uint8_t *lo = hi + 1024;
-                for (int lane = 0; lane < 64; ++lane)
-                    for (int j = 0; j < 16; ++j) {
-                        const int o = (int)ti * 16 + (lane & 15);
-                        const int c = o < dstW ? tap(f, o, t.base + 64 * kb + kcol_of(lane, j)) : 0;
-                        const int l = (int8_t)(c & 0xff), h = (c - l) >> 8;
-                        if (h < -128 || h > 127) return false;
-                        hi[lane * 16 + j] = (uint8_t)h;
-                        lo[lane * 16 + j] = (uint8_t)l;
-                    }
+                const bool ok = put_frag(out.bfrag, t.frag + kb, [&](int lane, int k) {
+                    const int o = (int)ti * 16 + (lane & 15);
+                    return o < dstW ? htap(f, o, t.base + 64 * kb + k) : 0;
+                });
+                if (!ok) return false;
             }
         }
-    }
-    // ---- V: per rendition, ring slots and the rows each 16-row step completes --
-    const int nsteps = (in.srcH + kL5Rows - 1) / kL5Rows;
-    const int pairs_total = (in.srcH + 1) / 2;
-    std::vector<int> Rslots(nr), np4(nr), rows_max(nr, 0);
-    std::vector<std::vector<int32_t>> vlim(nr);
-    for (int r = 0; r < nr; ++r) {
         const VTable &v = *in.rungs[r].v;
         const int dstH = in.rungs[r].dstH;
-        np4[r] = (v.nv + 3) & ~3;
-        if (np4[r] > 32) return false;
-        vlim[r].assign(nsteps, 0);
-        int y = 0, need = 16;
-        for (int b = 0; b < nsteps; ++b) {
-            const int done = std::min(8 * (b + 1), pairs_total), y0 = y;
-            int pmin = 1 << 30;
-            while (y < dstH && std::min(v.pos[y] / 2 + v.nv, pairs_total) <= done) {
-                pmin = std::min(pmin, v.pos[y] / 2);
-                ++y;
+        for (size_t G = 0; G < groups[r].size(); ++G) {
+            const Group &g = groups[r][G];
+            for (int kb = 0; kb < g.nkb; ++kb) {
+                const bool ok = put_frag(out.bfrag, g.frag + kb, [&](int lane, int k) {
+                    const int y = (int)G * 16 + (lane & 15);
+                    return y < dstH ? vtap(v, y, g.w0 + 64 * kb + k) : 0;
+                });
+                if (!ok) return false;
             }
-            vlim[r][b] = y;
-            rows_max[r] = std::max(rows_max[r], y - y0);
-            // V(b) reads pairs [pmin, done) while H(b + 1) writes [8(b + 1), 8(b + 2))
-            if (y > y0) need = std::max(need, 8 * (b + 2) - pmin);
         }
-        if (y != dstH) return false;
-        Rslots[r] = round_up(need, 8);
-        if (Rslots[r] > 256) return false;
     }
-    // one ring size for the kind (the kernel keeps one slot counter per step)
-    int Ru = 8, Mu = 0;
-    for (int r = 0; r < nr; ++r) {
-        Ru = std::max(Ru, Rslots[r]);
-        Mu = std::max(Mu, in.rungs[r].v->nv - 1);
+    // ---- per-step V schedule (ring fields filled in once the rings are laid out) --
+    std::vector<int> voff(nsteps + 1, 0);
+    for (int b = 0; b < nsteps; ++b) {
+        voff[b] = (int)out.vsched.size();
+        for (int r = 0; r < nr; ++r)
+            for (size_t G = 0; G < groups[r].size(); ++G) {
+                const Group &g = groups[r][G];
+                if (g.step != b) continue;
+                VEnt5 e{};
+                e.rung = r;
+                e.G = (int)G;
+                e.rows = g.rows;
+                e.w0 = g.w0 % RR[r];                  // ring row of the window start
+                e.nkb = g.nkb;
+                e.bfrag = g.frag;
+                e.fmt = in.rungs[r].fmt;
+                e.dstW = in.rungs[r].dstW;
+                out.vsched.push_back(e);
+            }
+    }
+    voff[nsteps] = (int)out.vsched.size();
+    out.vstep.assign((size_t)4 * (nsteps + 1), 0);
+    for (int b = 0; b <= nsteps; ++b) {
+        const int e0 = voff[b], e1 = b < nsteps ? voff[b + 1] : e0;
+        out.vstep[4 * b] = e0;
+        out.vstep[4 * b + 1] = e1;
+        out.vstep[4 * b + 2] = e0 < e1 ? out.vsched[e0].bfrag : 0;
+        out.vstep[4 * b + 3] = e0 < e1 ? out.vsched[e0].nkb : 0;
     }
     // ---- strips ---------------------------------------------------------------
     const int bps = in.nv12_chroma ? 2 : 1;
@@ -181,7 +256,8 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             st.L = L;
             st.cpr = W * bps / 16;
             st.nchunk = in.nv12_chroma ? kL5Rows * st.cpr : nplanes * kL5Rows * st.cpr;
-            if (st.nchunk > kL5MaxLoads * 256) {
+            // staging loads per thread: planar chroma 2 per plane, otherwise 4
+            if (kL5Rows * st.cpr > (in.chroma && !in.nv12_chroma ? 2 : 4) * 256) {
                 ok = false;
                 break;
             }
@@ -223,83 +299,45 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             }
             for (int r = 0; r < nr; ++r) {
                 st.x0[r] = 16 * t0[s][r];
-                pcols[r] = std::max(pcols[r], 16 * (t1[s][r] - t0[s][r]));
+                st.nct[r] = t1[s][r] - t0[s][r];
+                pcols[r] = std::max(pcols[r], 16 * st.nct[r]);
             }
             pk.strips.push_back(st);
         }
         if (!ok) continue;
-        // staged row pitch: 16 x odd bytes >= every strip's width (A reads conflict-free)
-        int P = round_up(Wmax, 16);
-        if ((P / 16) % 2 == 0) P += 16;
-        pk.P = P;
-        int lds = 4;                                       // dwords 0-3: the dequeue slot
+        // staged row pitch: 16 x odd bytes >= every strip's width (H A reads conflict-free)
+        pk.P = pitch16odd(Wmax);
+        int lds = 16 + kL5RungTab;                         // the dequeue slot, the per-item rendition table
         pk.stage = lds;
-        lds += 2 * nplanes * kL5Rows * P / 4;
-        // rings: (rendition, plane), quad-major, slots allocated = 1 mod 8
+        lds += 2 * nplanes * kL5Rows * pk.P;
+        // rings: (rendition, plane), two column-major byte planes each
         pk.nrings = nr * nplanes;
         for (int r = 0; r < nr; ++r)
             for (int p = 0; p < nplanes; ++p) {
                 Ring5 &g = pk.ring[r * nplanes + p];
-                int alloc = std::max(Ru + np4[r] - 1, Ru + round_up(std::max(Mu, 1), 8));
-                while (alloc % 8 != 1) ++alloc;
-                g.qstride = 4 * alloc;
-                g.lds = lds;
-                lds += (pcols[r] / 4) * g.qstride;
+                g.RR = RR[r];
+                g.CP = pitch16odd(RR[r]);
+                g.hi = lds;
+                lds += pcols[r] * g.CP;
+                g.lo = lds;
+                lds += pcols[r] * g.CP;
             }
-        // V units and their per-step staging
-        pk.nunits = 0;
+        if (lds > in.lds_cap) continue;
         for (int r = 0; r < nr; ++r) {
-            auto add = [&](int mode, int plane, int ring0, int ring1, int cols) {
-                Unit5 &u = pk.unit[pk.nunits++];
-                u.rung = r;
-                u.mode = mode;
-                u.plane = plane;
-                u.ring0 = ring0;
-                u.ring1 = ring1;
-                u.np4 = np4[r];
-                u.dstW = cols;
-                u.vco_dw = std::max(rows_max[r], 1) * (4 + np4[r]);
-                u.vco = lds;
-                lds += 2 * u.vco_dw;
-            };
-            const int W = in.rungs[r].dstW;
-            if (!in.chroma)
-                add(0, 0, r, r, W);
-            else if (in.rungs[r].fmt == DTS_FMT_NV12)
-                add(1, 1, 2 * r, 2 * r + 1, W);
-            else {
-                add(0, 1, 2 * r, 2 * r, W);
-                add(0, 2, 2 * r + 1, 2 * r + 1, W);
-            }
+            pk.out[r].fmt = in.rungs[r].fmt;
+            pk.out[r].dstW = in.rungs[r].dstW;
+            pk.out[r].dstH = in.rungs[r].dstH;
         }
-        for (size_t s = 0; s < pk.strips.size(); ++s) {
-            Strip5 &st = pk.strips[s];
-            for (int u = 0; u < pk.nunits; ++u) {
-                const Unit5 &U = pk.unit[u];
-                const int cols = std::max(0, std::min(16 * t1[s][U.rung], U.dstW) - 16 * t0[s][U.rung]);
-                st.quads[u] = U.mode == 1 ? (cols + 1) / 2 : (cols + 3) / 4;
-            }
-        }
-        pk.lds_dw = lds;
-        if (lds * 4 > in.lds_cap) continue;
-        // V tables
-        pk.vslot.resize(nr);
-        pk.vcoef.resize(nr);
-        pk.vlim = vlim;
-        for (int r = 0; r < nr; ++r) {
-            const VTable &v = *in.rungs[r].v;
-            const int dstH = in.rungs[r].dstH;
-            pk.vslot[r].resize(dstH);
-            pk.vcoef[r].assign((size_t)dstH * np4[r], 0);
-            for (int y = 0; y < dstH; ++y) {
-                pk.vslot[r][y] = (v.pos[y] / 2) % Ru;
-                for (int t = 0; t < v.nv; ++t) pk.vcoef[r][(size_t)y * np4[r] + t] = v.coef[(size_t)y * v.nv + t];
-            }
-        }
+        pk.lds_bytes = lds;
         pk.bfrag = std::move(out.bfrag);
+        pk.vsched = std::move(out.vsched);
+        pk.vstep = std::move(out.vstep);
+        for (VEnt5 &e : pk.vsched) {
+            e.ring0 = pk.ring[e.rung * nplanes];
+            e.hi1 = nplanes == 2 ? pk.ring[e.rung * 2 + 1].hi : e.ring0.hi;
+            e.lo1 = nplanes == 2 ? pk.ring[e.rung * 2 + 1].lo : e.ring0.lo;
+        }
         pk.strip_width = SW;
-        pk.R = Ru;
-        pk.M = Mu;
         out = std::move(pk);
         return true;
     }
