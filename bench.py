@@ -130,10 +130,28 @@ def cpu_baseline(wl_name, budget_s, threads):
         while time.perf_counter() - t0 < budget_s:
             done += sum(ex.map(one, range(done, done + threads)))
     dt = time.perf_counter() - t0
+    nproc = os.cpu_count() or threads
     return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "per_core": round(done / dt / threads, 3),
+            "all_cores_linear_est": round(done / dt / threads * nproc, 1),
             "sample": f"{done} synthetic {sw}x{sh} source frames through the {wl_name} graph by the CPU "
-                      f"oracle (plain-C libswscale / vf_* restatement, ctypes, 1 frame per thread) in {dt:.1f} s; "
+                      f"oracle (plain-C libswscale / vf_* restatement, ctypes, 1 frame per thread) in {dt:.1f} s "
+                      f"on {threads} threads = every CPU this process may use (sched_getaffinity; the box's share "
+                      f"for one GPU, of nproc = {nproc}); all_cores_linear_est scales per_core to nproc; "
                       "ffmpeg is not installed on the box"}
+
+
+def cpu_share():
+    """CPUs this process may run on: sched_getaffinity, capped by the box's
+    per-GPU share (OMP_NUM_THREADS, which the GPU box sets) when that is set."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def hip_runtimes():
@@ -372,7 +390,7 @@ def main():
                          "frames_per_launch": B},
         }
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
+            threads = cpu_share()
             line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, threads)
         print(json.dumps(line), flush=True)
     if g is not None:

@@ -828,8 +828,11 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
         k.nplanes = pk.nplanes;
         k.nsteps = pk.nsteps;
         k.srcH = kind ? (g->spec.src_h + 1) >> 1 : g->spec.src_h;
-        k.P = pk.P;
+        k.nlp = pk.nlp;
         k.stage = pk.stage;
+        k.SB = pk.SB;
+        k.FA = pk.FA;
+        k.nbfrag = (uint32_t)(pk.bfrag.size() / 512);
         k.nrings = pk.nrings;
         k.nrungs = g->spec.nout;
         k.nstrips = (int32_t)pk.strips.size();

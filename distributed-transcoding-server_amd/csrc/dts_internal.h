@@ -139,9 +139,12 @@ int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
 // copy of the source rows.
 // ---------------------------------------------------------------------------
 constexpr int kL5Rows = 16;         // source rows per step (the H MFMA's M)
+constexpr int kL5Waves = 8;         // waves per workgroup (one workgroup per CU: 2 waves per SIMD)
+constexpr int kL5Threads = 64 * kL5Waves;
 constexpr int kL5Ent = 8;           // H entries (K blocks of 64 source columns) per wave
 constexpr int kL5MaxRings = 2 * DTS_MAX_OUTPUTS;
-constexpr int kL5MaxLoads = 4;      // 16-B staging loads per thread per step
+constexpr int kL5Stages = 3;        // stage buffers (bundle s in buffer s % 3: two in flight behind the one H reads)
+constexpr int kL5MaxDma = 15;       // LDS-DMA instructions per wave per step (1 KB each)
 constexpr int kL5MaxVkb = 2;        // V K blocks (64 source rows) per row group
 constexpr int kL5Bias = 128 << 14;  // 128 * sum(H taps): the (src ^ 0x80) offset of every H output
 constexpr int kL5VBias = (128 << 12) + (64 << 12);   // 128 * sum(V taps) ((y & 255) ^ 0x80) + flat dither
@@ -149,13 +152,13 @@ constexpr int kL5VBias = (128 << 12) + (64 << 12);   // 128 * sum(V taps) ((y & 
 // pad, plane base lo/hi x 3 (this frame)}
 constexpr int kL5RungTab = 4 * 16 * DTS_MAX_OUTPUTS;
 
-struct Ent5 {                       // one K block of one H tile, run by one wave
+struct Ent5 {                       // 16, 8 or 4 H outputs over one K block of 64 source columns
     int32_t bfrag;                  // B fragment pair (hi 1 KB, lo 1 KB; 16 B per lane)
     int16_t soff;                   // byte offset of the K block in the staged row (multiple of 8)
-    int16_t col0;                   // ring column of the tile's first output (multiple of 16)
+    int16_t col0;                   // ring column of the entry's first output
     int8_t plane;                   // staged plane (chroma: 0 = U, 1 = V)
-    int8_t ring;                    // ring of the tile's outputs
-    int8_t flags;                   // 1: first K block of the tile, 2: last (epilogue)
+    int8_t ring;                    // ring of the entry's outputs
+    int8_t flags;                   // 4: nv12 V (odd bytes of the staged row); 8 / 16: 8 / 4 outputs
     int8_t pad_;
 };
 
@@ -172,7 +175,8 @@ struct VEnt5 {                      // one V row group of one rendition, ready a
     int32_t rows;                   // valid rows (<= 16)
     int32_t w0;                     // ring row of the first source row of its K blocks (w0 % RR, multiple of 8)
     int32_t nkb;                    // K blocks of 64 source rows
-    int32_t bfrag;                  // first V fragment pair (taps >> 8, taps & 255 as signed bytes)
+    int32_t foff;                   // byte offset of its first V fragment pair (taps >> 8, taps & 255 as
+                                    // signed bytes) in its step's fragment area
     int32_t fmt;                    // the rendition's output format
     int32_t dstW;                   // columns of its output plane(s) of this kind
     Ring5 ring0;                    // its ring (chroma: U)
@@ -188,26 +192,32 @@ struct Out5 {                       // one rendition's output of this plane kind
 
 struct Strip5 {                     // one column strip of a plane kind
     int32_t L;                      // first staged sample column (multiple of 16)
-    int32_t nchunk;                 // 16-B staging loads per step (all rows, all planes)
-    int32_t cpr;                    // 16-B loads per staged row per plane
-    int32_t pad_;
-    int32_t ent0[4], nent[4];       // each wave's H entries
+    int32_t cpr;                    // 16-B chunks per staged row per load plane (odd)
+    int32_t Pb;                     // staged row pitch = 16 cpr bytes (16 x odd: conflict-free A reads)
+    int32_t PS;                     // load plane stride in a stage buffer (16 rows, rounded up to 1 KB)
+    int32_t nsi;                    // source LDS-DMA instructions per step (load planes x PS / 1 KB)
+    int32_t pad_[3];
+    int32_t ent0[kL5Waves], nent[kL5Waves];   // each wave's H entries
     int32_t x0[DTS_MAX_OUTPUTS];    // first output column per rendition (multiple of 16)
     int32_t nct[DTS_MAX_OUTPUTS];   // 16-column tiles per rendition
 };
 
 struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every rendition
     int32_t nplanes, nsteps, srcH;
-    int32_t P;                      // staged row pitch, bytes (16 x odd: conflict-free A reads)
-    int32_t stage;                  // byte offset of the 2 stage buffers
+    int32_t nlp;                    // load planes (planar chroma 2; luma, nv12 chroma 1: U V interleaved)
+    int32_t stage;                  // byte offset of the kL5Stages stage buffers
+    int32_t SB;                     // stage buffer size: load planes, then the V fragment area
+    int32_t FA;                     // offset of the V fragment area in a stage buffer
     int32_t nrings, nrungs, nstrips;
     Ring5 ring[kL5MaxRings];        // rendition r, plane p: ring[r * nplanes + p]
     Out5 out[DTS_MAX_OUTPUTS];
     const Strip5 *strips;
     const Ent5 *ents;
-    const uint32_t *bfrag;          // H then V fragment pairs, 512 dwords each
+    const uint32_t *bfrag;          // H, then V fragment pairs (in step order), 512 dwords each
+    uint32_t nbfrag;                // fragment pairs
+    int32_t pad_;
     const VEnt5 *vsched;            // the V row groups of every step, step after step
-    const int4 *vstep;              // [nsteps + 1]: {first group, end, first group's bfrag, its nkb}
+    const int4 *vstep;              // [nsteps + 1]: {first group, end, first V fragment pair, its KB count}
 };
 
 struct Job5 {

@@ -87,12 +87,12 @@ struct Plan5In {
     bool chroma = false;             // U + V planes (else luma)
     bool nv12_chroma = false;        // chroma staged from an interleaved nv12 plane
     int srcW = 0, srcH = 0;          // plane size
-    int lds_cap = 80 * 1024;         // bytes per workgroup (2 per CU)
+    int lds_cap = 160 * 1024;        // bytes per workgroup (one per CU)
     std::vector<Plan5Rung> rungs;
 };
 
 struct Plan5Kind {
-    int nplanes = 1, nsteps = 0, P = 0, stage = 0, nrings = 0, lds_bytes = 0, strip_width = 0;
+    int nplanes = 1, nsteps = 0, nlp = 1, stage = 0, SB = 0, FA = 0, nrings = 0, lds_bytes = 0, strip_width = 0;
     Ring5 ring[kL5MaxRings]{};
     Out5 out[DTS_MAX_OUTPUTS]{};
     std::vector<Strip5> strips;

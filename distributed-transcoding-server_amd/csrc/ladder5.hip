@@ -61,6 +61,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(4))) const uint32_t k_u32;
 typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) u32x2 g_u32x2;
 typedef __attribute__((address_space(1))) uint16_t g_u16;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
 #define GP5(T, p) ((T *)(uintptr_t)(p))
@@ -98,75 +100,120 @@ __device__ __forceinline__ uint32_t pack_h(int hi, int lo, int hi2, int lo2)
 }
 
 struct Walk5 {
-    int nplanes, nsteps, srcH, Pb, stage_b;
-    int L, cpr, ne;
+    int nplanes, nsteps, srcH, stage, SB, FA;
+    int L, cpr, Pb, PS, nsi, ne;
     int lane, wave, t;
 };
 
-// This thread's staging loads of a step: kL5MaxLoads 16-B source chunks.
-struct Loads5 {
-    __amdgpu_buffer_rsrc_t rs[2];   // load planes (planar chroma: U, V)
+// This item's LDS-DMA sources: buffer descriptors (SGPRs) of the load planes and
+// of the fragment table
+struct Dma5 {
+    u32x4 rs[2];                    // load planes (planar chroma: U, V)
+    u32x4 rf;                       // B fragment pairs (V fragments in step order)
     uint32_t pitch[2];
-    uint32_t col[kL5MaxLoads];      // byte offset of the chunk in its source row
-    int row[kL5MaxLoads];           // staged row (0..15), -1 = no chunk
-    uint32_t dst[kL5MaxLoads];      // LDS byte offset of the chunk in stage buffer 0
-    int nlp;                        // load planes
+    uint32_t colb;                  // byte column of the strip's first staged sample
+    float rc;                       // 1 / cpr
+    int ipp;                        // DMA instructions per load plane (PS / 1 KB)
 };
 
-__device__ __forceinline__ void issue_loads(const Loads5 &ld, int b, const Walk5 &W, u32x4 (&pre)[kL5MaxLoads])
+__device__ __forceinline__ u32x4 rsrc5(uint64_t base, uint32_t bytes)
 {
-    if (b >= W.nsteps || (DTS_L5_ABLATE & 4)) return;
-#pragma unroll
-    for (int k = 0; k < kL5MaxLoads; ++k) {
-        const int lp = ld.nlp == 2 ? (k >> 1) : 0;
-        if (ld.row[k] >= 0) {
-            const int r = min(kL5Rows * b + ld.row[k], W.srcH - 1);
-            const uint32_t off = (uint32_t)r * ld.pitch[lp] + ld.col[k];
-            pre[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(lp ? ld.rs[1] : ld.rs[0], off, 0, 0));
-        }
-    }
+    u32x4 r;
+    r.x = (uint32_t)uni5((int)(uint32_t)base);
+    r.y = (uint32_t)uni5((int)(uint32_t)(base >> 32));      // stride 0
+    r.z = (uint32_t)uni5((int)bytes);                        // num_records: offsets past it read 0
+    r.w = 0x00020000u;
+    return r;
 }
 
-// prefetched chunks -> stage buffer (b & 1), as src ^ 0x80 (nv12 chroma: de-interleaved into U, V)
-template <int SRC>
-__device__ __forceinline__ void store_stage(uint32_t *lds, const Loads5 &ld, int b, const Walk5 &W,
-                                            const u32x4 (&pre)[kL5MaxLoads], bool nv12c)
+// One LDS-DMA instruction: 64 lanes x 16 B from voff (per lane) to LDS m0 + 16 lane.
+// M0 is the compiler's: saved and restored inside the statement.
+__device__ __forceinline__ void dma16(const u32x4 &rs, uint32_t voff, uint32_t m0)
 {
-    const uint32_t boff = (uint32_t)((b & 1) * W.nplanes * kL5Rows * W.Pb);
-#pragma unroll
-    for (int k = 0; k < kL5MaxLoads; ++k) {
-        if (ld.row[k] < 0) continue;
-        const u32x4 v = pre[k];
-        if (SRC == kSrcNV12 && nv12c) {
-            const uint32_t u0 = __builtin_amdgcn_perm(v.y, v.x, 0x06040200u) ^ 0x80808080u;
-            const uint32_t u1 = __builtin_amdgcn_perm(v.w, v.z, 0x06040200u) ^ 0x80808080u;
-            const uint32_t v0 = __builtin_amdgcn_perm(v.y, v.x, 0x07050301u) ^ 0x80808080u;
-            const uint32_t v1 = __builtin_amdgcn_perm(v.w, v.z, 0x07050301u) ^ 0x80808080u;
-            *reinterpret_cast<u32x2 *>(lds_at(lds, ld.dst[k] + boff)) = (u32x2){u0, u1};
-            *reinterpret_cast<u32x2 *>(lds_at(lds, ld.dst[k] + boff + kL5Rows * W.Pb)) = (u32x2){v0, v1};
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rs), "s"(m0)
+                 : "memory");
+}
+
+// Bundle s -> stage buffer s % kL5Stages: the 16 source rows of step s (s < nsteps),
+// as stored (row-major, pitch Pb, load plane p at p * PS), then the V fragments of
+// V(s - 1) (vf0, nfu: its step record's first fragment pair and 1 KB units).  Instruction i of the bundle is issued by wave i % kL5Waves; returns how
+// many this wave issued (its vmcnt share of the bundle).
+__device__ __forceinline__ int issue_bundle(const Walk5 &W, const Dma5 &D, int s, int vf0, int nfu)
+{
+    if (DTS_L5_ABLATE & 4) return 0;
+    const int nsi = s < W.nsteps ? W.nsi : 0;
+    const uint32_t buf = (uint32_t)(W.stage + (s % kL5Stages) * W.SB);
+    int m = 0;
+    for (int i = W.wave; i < nsi + nfu; i += kL5Waves, ++m) {
+        if (i < nsi) {
+            const int p = i >= D.ipp ? 1 : 0;
+            const int ii = i - p * D.ipp;
+            const int c = 64 * ii + W.lane;
+            const int row = (int)(((float)c + 0.5f) * D.rc), cc = c - row * W.cpr;
+            const int r = min(kL5Rows * s + row, W.srcH - 1);
+            const uint32_t off = (uint32_t)r * (p ? D.pitch[1] : D.pitch[0]) + D.colb + 16u * (uint32_t)cc;
+            dma16(p ? D.rs[1] : D.rs[0], row < kL5Rows ? off : 0x80000000u,
+                  buf + (uint32_t)(p * W.PS) + 1024u * (uint32_t)ii);
         } else {
-            *reinterpret_cast<u32x4 *>(lds_at(lds, ld.dst[k] + boff)) = v ^ 0x80808080u;
+            const int j = i - nsi;
+            dma16(D.rf, (uint32_t)vf0 * 2048u + 1024u * (uint32_t)j + 16u * (uint32_t)W.lane,
+                  buf + (uint32_t)W.FA + 1024u * (uint32_t)j);
         }
     }
+    return m;
 }
 
-// H(b) of this wave: NE entries (K blocks), straight-line -- every A read, then
-// every MFMA, then the epilogues -- so the reads and the matrix pipe overlap.
-// A K block continuing a tile adds the previous block's sums (the lo MFMAs all
-// start at the bias: the continuation subtracts the extra one).  An epilogue
-// writes 4 rows of one column: their y >> 8 and (y & 255) ^ 0x80 bytes.
-template <int I0, int NE>
+// End of a step: every DMA of this wave except the m it issued this step (so the
+// next bundle's) has landed, the ring writes too; then the barrier.  A raw barrier:
+// __syncthreads() would also wait for the DMAs still in flight.
+__device__ __forceinline__ void step_barrier(int m)
+{
+#define DTS_W5(k) \
+    case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    switch (m) {
+        DTS_W5(1) DTS_W5(2) DTS_W5(3) DTS_W5(4) DTS_W5(5) DTS_W5(6) DTS_W5(7) DTS_W5(8) DTS_W5(9)
+        DTS_W5(10) DTS_W5(11) DTS_W5(12) DTS_W5(13) DTS_W5(14) DTS_W5(15)
+    default:
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        break;
+    }
+#undef DTS_W5
+}
+
+__device__ __forceinline__ u32x4 lds_rd128(const uint32_t *lds, uint32_t byte)
+{
+    return *reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(lds) + byte);
+}
+
+// H(b) of this wave: NE entries, straight-line -- every A read, then every MFMA,
+// then the epilogues -- so the reads and the matrix pipe overlap.  An entry is
+// 16 (8, 4) outputs over one 64-column K block; its epilogue writes 4 rows of one
+// column per lane: their y >> 8 and (y & 255) ^ 0x80 bytes (lanes past the
+// entry's outputs hold an out-of-range LDS address: their writes are dropped).
+template <int I0, int NE, bool ILV>
 __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
                                       const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
-                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t fl,
-                                      uint32_t boff, v4i &ch, v4i &cl)
+                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t odd,
+                                      uint32_t boff)
 {
     const v4i zero = {0, 0, 0, 0}, bias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
     v4i a[NE], ah[NE], al[NE];
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
-        const u32x2 x = lds_rd64(lds, aad[I0 + i] + boff), y = lds_rd64(lds, aad[I0 + i] + boff + 32);
-        a[i] = __builtin_bit_cast(v4i, (u32x4){x.x, x.y, y.x, y.y});
+        if (ILV) {       // nv12 chroma: U V interleaved as stored; even (U) or odd (V) bytes
+            const u32x4 x = lds_rd128(lds, aad[I0 + i] + boff), y = lds_rd128(lds, aad[I0 + i] + boff + 64);
+            const uint32_t sel = (odd >> (I0 + i)) & 1u ? 0x07050301u : 0x06040200u;
+            a[i] = __builtin_bit_cast(v4i, (u32x4){__builtin_amdgcn_perm(x.y, x.x, sel), __builtin_amdgcn_perm(x.w, x.z, sel),
+                                                   __builtin_amdgcn_perm(y.y, y.x, sel), __builtin_amdgcn_perm(y.w, y.z, sel)} ^
+                                                   0x80808080u);
+        } else {
+            const u32x2 x = lds_rd64(lds, aad[I0 + i] + boff), y = lds_rd64(lds, aad[I0 + i] + boff + 32);
+            a[i] = __builtin_bit_cast(v4i, (u32x4){x.x, x.y, y.x, y.y} ^ 0x80808080u);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);                     // every A read in flight before the first MFMA
 #pragma unroll
@@ -181,77 +228,71 @@ __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], co
     }
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
-        const uint32_t f = (fl >> (2 * (I0 + i))) & 3u;
-        if (!(f & 1u)) {                                   // continues the previous K block's tile
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                ah[i][r] += ch[r];
-                al[i][r] = al[i][r] + cl[r] - kL5Bias;
-            }
-        }
-        if (f & 2u) {
-            const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);    // rows 4g, 4g+1
-            const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);    // rows 4g+2, 4g+3
-            *lds_at(lds, whi[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
-            *lds_at(lds, wlo[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
-        } else {
-            ch = ah[i];
-            cl = al[i];
-        }
+        const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);    // rows 4g, 4g+1
+        const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);    // rows 4g+2, 4g+3
+        *lds_at(lds, whi[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
+        *lds_at(lds, wlo[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
     }
 }
 
-// H(b) of this wave: NE entries (K blocks) in halves of up to 4 -- every A read
-// of a half, then its MFMAs, then its epilogues -- so the reads and the matrix
-// pipe overlap.  A K block continuing a tile adds the previous block's sums
-// (the lo MFMAs all start at the bias: the continuation subtracts the extra
-// one).  An epilogue writes 4 rows of one column: their y >> 8 and
-// (y & 255) ^ 0x80 bytes.
-template <int NE>
+// H(b) of this wave in parts of up to 4 entries
+template <int NE, bool ILV>
 __device__ __forceinline__ void hstep(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
                                       const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
-                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t fl,
+                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t odd,
                                       uint32_t boff)
 {
-    v4i ch = {0, 0, 0, 0}, cl = {0, 0, 0, 0};
-    hpart<0, (NE < 4 ? NE : 4)>(lds, bh, bl, aad, whi, wlo, pos, fl, boff, ch, cl);
-    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1)>(lds, bh, bl, aad, whi, wlo, pos, fl, boff, ch, cl);
+    hpart<0, (NE < 4 ? NE : 4), ILV>(lds, bh, bl, aad, whi, wlo, pos, odd, boff);
+    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1), ILV>(lds, bh, bl, aad, whi, wlo, pos, odd, boff);
 }
 
-// V of one (row group, 16-column tile, plane): 4 MFMAs per K block, then the
-// 4 output bytes (columns 4g..4g+3 of output row lane & 15) packed in a dword
-__device__ __forceinline__ uint32_t vtile(const uint32_t *lds, const Ring5 &g, int col, int w0m, int nkb,
-                                          const v4i (&vh)[kL5MaxVkb], const v4i (&vl)[kL5MaxVkb], int lane)
+// V of two (row group, 16-column tile, plane) tiles at once -- two independent
+// chains, so one's LDS reads overlap the other's MFMAs: 4 MFMAs per K block
+// each, then the 4 output bytes (columns 4g..4g+3 of output row lane & 15)
+// packed in a dword.  hiX / loX: LDS byte address of the tile's first column
+// in its hi / lo ring.
+__device__ __forceinline__ uint32_t vcombine(const v4i &hh, const v4i &hl, const v4i &ll)
 {
-    const v4i zero = {0, 0, 0, 0}, vbias = {kL5VBias, kL5VBias, kL5VBias, kL5VBias};
-    v4i hh = zero, hl = zero, ll = vbias;
-    const uint32_t cb = (uint32_t)(col * g.CP);
-    const int rr = g.RR;
-#pragma unroll
-    for (int kb = 0; kb < kL5MaxVkb; ++kb) {
-        if (kb < nkb) {
-            int r0 = w0m + 64 * kb + 8 * (lane >> 4), r1 = r0 + 32;
-            r0 = r0 >= rr ? r0 - rr : r0;
-            r1 = r1 >= rr ? r1 - rr : r1;
-            const u32x2 h0 = lds_rd64(lds, (uint32_t)g.hi + cb + (uint32_t)r0);
-            const u32x2 h1 = lds_rd64(lds, (uint32_t)g.hi + cb + (uint32_t)r1);
-            const u32x2 l0 = lds_rd64(lds, (uint32_t)g.lo + cb + (uint32_t)r0);
-            const u32x2 l1 = lds_rd64(lds, (uint32_t)g.lo + cb + (uint32_t)r1);
-            const v4i ahi = __builtin_bit_cast(v4i, (u32x4){h0.x, h0.y, h1.x, h1.y});
-            const v4i alo = __builtin_bit_cast(v4i, (u32x4){l0.x, l0.y, l1.x, l1.y});
-            hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahi, vh[kb], hh, 0, 0, 0);
-            hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahi, vl[kb], hl, 0, 0, 0);
-            hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(alo, vh[kb], hl, 0, 0, 0);
-            ll = __builtin_amdgcn_mfma_i32_16x16x64_i8(alo, vl[kb], ll, 0, 0, 0);
-        }
-    }
     int v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = (((hh[i] << 8) + hl[i]) << 8) + ll[i];
     // av_clip_uint8(val >> 19) of 4 columns, packed
     const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(v[0], v[1], 19);
     const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(v[2], v[3], 19);
-    return (lo & 0xffffu) | (hi << 16);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+template <int NKB>
+__device__ __forceinline__ void vtile2(const uint32_t *lds, uint32_t hiA, uint32_t loA, uint32_t hiB, uint32_t loB,
+                                       int w0m, int rr, const v4i (&vh)[kL5MaxVkb], const v4i (&vl)[kL5MaxVkb],
+                                       int lane, uint32_t &wa, uint32_t &wb)
+{
+    const v4i zero = {0, 0, 0, 0}, vbias = {kL5VBias, kL5VBias, kL5VBias, kL5VBias};
+    v4i hhA = zero, hlA = zero, llA = vbias, hhB = zero, hlB = zero, llB = vbias;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        int r0 = w0m + 64 * kb + 8 * (lane >> 4), r1 = r0 + 32;
+        r0 = r0 >= rr ? r0 - rr : r0;
+        r1 = r1 >= rr ? r1 - rr : r1;
+        const u32x2 ha0 = lds_rd64(lds, hiA + (uint32_t)r0), ha1 = lds_rd64(lds, hiA + (uint32_t)r1);
+        const u32x2 la0 = lds_rd64(lds, loA + (uint32_t)r0), la1 = lds_rd64(lds, loA + (uint32_t)r1);
+        const u32x2 hb0 = lds_rd64(lds, hiB + (uint32_t)r0), hb1 = lds_rd64(lds, hiB + (uint32_t)r1);
+        const u32x2 lb0 = lds_rd64(lds, loB + (uint32_t)r0), lb1 = lds_rd64(lds, loB + (uint32_t)r1);
+        const v4i ahA = __builtin_bit_cast(v4i, (u32x4){ha0.x, ha0.y, ha1.x, ha1.y});
+        const v4i alA = __builtin_bit_cast(v4i, (u32x4){la0.x, la0.y, la1.x, la1.y});
+        const v4i ahB = __builtin_bit_cast(v4i, (u32x4){hb0.x, hb0.y, hb1.x, hb1.y});
+        const v4i alB = __builtin_bit_cast(v4i, (u32x4){lb0.x, lb0.y, lb1.x, lb1.y});
+        hhA = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahA, vh[kb], hhA, 0, 0, 0);
+        hlA = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahA, vl[kb], hlA, 0, 0, 0);
+        llA = __builtin_amdgcn_mfma_i32_16x16x64_i8(alA, vl[kb], llA, 0, 0, 0);
+        hhB = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahB, vh[kb], hhB, 0, 0, 0);
+        hlB = __builtin_amdgcn_mfma_i32_16x16x64_i8(ahB, vl[kb], hlB, 0, 0, 0);
+        llB = __builtin_amdgcn_mfma_i32_16x16x64_i8(alB, vl[kb], llB, 0, 0, 0);
+        hlA = __builtin_amdgcn_mfma_i32_16x16x64_i8(alA, vh[kb], hlA, 0, 0, 0);
+        hlB = __builtin_amdgcn_mfma_i32_16x16x64_i8(alB, vh[kb], hlB, 0, 0, 0);
+    }
+    wa = vcombine(hhA, hlA, llA);
+    wb = vcombine(hhB, hlB, llB);
 }
 
 // One output store of 4 bytes at byte column x of a row (fewer at the plane's right edge).
@@ -268,23 +309,17 @@ __device__ __forceinline__ void store4(uint64_t row, int x, int ncols, uint32_t 
     }
 }
 
-// V work of one step, fetched before the barrier it runs after: the fragments
-// of its first row group (their latency hides under the barrier wait)
-struct VPrep5 {
-    int e0, e1;
-    v4i vh[kL5MaxVkb], vl[kL5MaxVkb];
-};
-
-__device__ __forceinline__ void vfrags(const uint32_t *bf, int frag, int nkb, int lane, v4i (&vh)[kL5MaxVkb],
+// V fragments of a row group from its step's fragment area (fb: LDS byte address)
+__device__ __forceinline__ void vfrags(const uint32_t *lds, uint32_t fb, int nkb, int lane, v4i (&vh)[kL5MaxVkb],
                                        v4i (&vl)[kL5MaxVkb])
 {
-    const u32x4 *f = reinterpret_cast<const u32x4 *>(bf + (size_t)frag * 512);
-    vh[0] = __builtin_bit_cast(v4i, f[lane]);
-    vl[0] = __builtin_bit_cast(v4i, f[64 + lane]);
+    const uint32_t o = fb + 16u * (uint32_t)lane;
+    vh[0] = __builtin_bit_cast(v4i, lds_rd128(lds, o));
+    vl[0] = __builtin_bit_cast(v4i, lds_rd128(lds, o + 1024));
     vh[1] = vl[1] = (v4i){0, 0, 0, 0};
     if (nkb > 1) {
-        vh[1] = __builtin_bit_cast(v4i, f[128 + lane]);
-        vl[1] = __builtin_bit_cast(v4i, f[192 + lane]);
+        vh[1] = __builtin_bit_cast(v4i, lds_rd128(lds, o + 2048));
+        vl[1] = __builtin_bit_cast(v4i, lds_rd128(lds, o + 3072));
     }
 }
 
@@ -325,8 +360,10 @@ __device__ __forceinline__ void rung_table(uint32_t *lds, const Strip5 *S, int n
     lds[4 + 16 * r + k] = v;
 }
 
-// V of one row group: its 16-column tiles dealt round robin over the 4 waves
+// V of one row group: its 16-column tiles dealt round robin over the waves,
+// two tiles per vtile2 (luma: tiles ct and ct + W; chroma: U and V of tile ct)
 // (pitches and plane bases of this frame from the rendition table)
+template <int NKB>
 __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, const VEnt5 &VE, const v4i (&vh)[kL5MaxVkb],
                                        const v4i (&vl)[kL5MaxVkb], int first, int nct, int x0, uint32_t pY,
                                        uint32_t pU, uint32_t pV, uint64_t bY, uint64_t bU, uint64_t bV)
@@ -334,23 +371,49 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
     const int n = W.lane & 15, g = W.lane >> 4;
     const int y = 16 * VE.G + n;
     const bool rowok = n < VE.rows;
+    const uint32_t CP = (uint32_t)VE.ring0.CP, dlo = (uint32_t)(VE.ring0.lo - VE.ring0.hi);
     if (W.nplanes == 1) {
         const uint64_t orow = bY + (uint64_t)y * pY;
-        for (int ct = first; ct < nct; ct += 4) {
-            const uint32_t w = vtile(lds, VE.ring0, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
-            const int x = x0 + 16 * ct + 4 * g;
-            if (rowok) store4(orow, x, VE.dstW - x, w);
+        for (int ct = first; ct < nct; ct += 2 * kL5Waves) {
+            const int ct2 = ct + kL5Waves < nct ? ct + kL5Waves : ct;
+            const uint32_t ha = (uint32_t)VE.ring0.hi + (uint32_t)(16 * ct + n) * CP;
+            const uint32_t hb = (uint32_t)VE.ring0.hi + (uint32_t)(16 * ct2 + n) * CP;
+            uint32_t wa, wb;
+            vtile2<NKB>(lds, ha, ha + dlo, hb, hb + dlo, VE.w0, VE.ring0.RR, vh, vl, W.lane, wa, wb);
+            if (!rowok) continue;
+            const int xa = x0 + 16 * ct + 4 * g, xb = x0 + 16 * ct2 + 4 * g;
+            if (x0 + 16 * ct2 + 16 <= VE.dstW) {            // both tiles inside the plane (uniform)
+                if (!(DTS_L5_ABLATE & 8)) {
+                    *GP5(g_u32, orow + xa) = wa;
+                    *GP5(g_u32, orow + xb) = wb;
+                }
+                continue;
+            }
+            store4(orow, xa, VE.dstW - xa, wa);
+            if (ct2 != ct) store4(orow, xb, VE.dstW - xb, wb);
         }
     } else {
-        const Ring5 g1 = {VE.hi1, VE.lo1, VE.ring0.CP, VE.ring0.RR};
         const bool nv = VE.fmt == DTS_FMT_NV12;
         const uint64_t urow = bU + (uint64_t)y * pU;
         const uint64_t vrow = bV + (uint64_t)y * pV;
-        for (int ct = first; ct < nct; ct += 4) {
-            const uint32_t wu = vtile(lds, VE.ring0, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
-            const uint32_t wv = vtile(lds, g1, 16 * ct + n, VE.w0, VE.nkb, vh, vl, W.lane);
+        for (int ct = first; ct < nct; ct += kL5Waves) {
+            const uint32_t cb = (uint32_t)(16 * ct + n) * CP;
+            uint32_t wu, wv;
+            vtile2<NKB>(lds, (uint32_t)VE.ring0.hi + cb, (uint32_t)VE.ring0.lo + cb, (uint32_t)VE.hi1 + cb,
+                        (uint32_t)VE.lo1 + cb, VE.w0, VE.ring0.RR, vh, vl, W.lane, wu, wv);
             const int x = x0 + 16 * ct + 4 * g;
             if (!rowok) continue;
+            if (x0 + 16 * ct + 16 <= VE.dstW) {              // the whole tile inside the plane (uniform)
+                if (DTS_L5_ABLATE & 8) continue;
+                if (!nv) {
+                    *GP5(g_u32, urow + x) = wu;
+                    *GP5(g_u32, vrow + x) = wv;
+                } else {                                    // yuv2nv12cX: U0 V0 U1 V1 U2 V2 U3 V3
+                    *GP5(g_u32x2, urow + 2 * x) = (u32x2){__builtin_amdgcn_perm(wv, wu, 0x05010400u),
+                                                          __builtin_amdgcn_perm(wv, wu, 0x07030602u)};
+                }
+                continue;
+            }
             if (!nv) {
                 store4(urow, x, VE.dstW - x, wu);
                 store4(vrow, x, VE.dstW - x, wv);
@@ -365,28 +428,35 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
     }
 }
 
-// V of a step for this wave; the first group's fragments came from vprep
-__device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const Walk5 &W, const uint32_t *bf,
-                                     VPrep5 &V)
+// V of a step for this wave: the row groups vs.x .. vs.y - 1, fragments from the
+// fragment area fa (LDS byte address) of the step's bundle
+__device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const Walk5 &W, const int2 &vs, uint32_t fa)
 {
+    const VEnt5 *vsched = kld(&K->vsched);
     int rot = 0;
-    for (int e = V.e0; e < V.e1; ++e) {
-        const VEnt5 VE = kld(K->vsched + e);
+    for (int e = vs.x; e < vs.y; ++e) {
+        const VEnt5 VE = kld(vsched + e);
         const uint32_t *tb = lds + 4 + 16 * VE.rung;
         const u32x4 t0 = *reinterpret_cast<const u32x4 *>(tb);        // x0, nct, pitch Y, pitch U
         const u32x4 t1 = *reinterpret_cast<const u32x4 *>(tb + 4);    // pitch V, 0, base Y
         const u32x4 t2 = *reinterpret_cast<const u32x4 *>(tb + 8);    // base U, base V
         const int nct = uni5((int)t0.y);
-        const int first = (W.wave - rot) & 3;
+        const int first = (W.wave - rot % kL5Waves + kL5Waves) % kL5Waves;
         rot += nct;
         if (first >= nct) continue;
-        if (e != V.e0) vfrags(bf, VE.bfrag, VE.nkb, W.lane, V.vh, V.vl);
+        v4i vh[kL5MaxVkb], vl[kL5MaxVkb];
+        vfrags(lds, fa + (uint32_t)VE.foff, VE.nkb, W.lane, vh, vl);
         auto u64 = [](uint32_t lo, uint32_t hi) {
             return ((uint64_t)(uint32_t)uni5((int)hi) << 32) | (uint32_t)uni5((int)lo);
         };
-        vgroup(lds, W, VE, V.vh, V.vl, first, nct, uni5((int)t0.x), (uint32_t)uni5((int)t0.z),
-               (uint32_t)uni5((int)t0.w), (uint32_t)uni5((int)t1.x), u64(t1.z, t1.w), u64(t2.x, t2.y),
-               u64(t2.z, t2.w));
+        const int x0 = uni5((int)t0.x);
+        const uint32_t pY = (uint32_t)uni5((int)t0.z), pU = (uint32_t)uni5((int)t0.w), pV = (uint32_t)uni5((int)t1.x);
+        if (VE.nkb > 1)
+            vgroup<2>(lds, W, VE, vh, vl, first, nct, x0, pY, pU, pV, u64(t1.z, t1.w), u64(t2.x, t2.y),
+                      u64(t2.z, t2.w));
+        else
+            vgroup<1>(lds, W, VE, vh, vl, first, nct, x0, pY, pU, pV, u64(t1.z, t1.w), u64(t2.x, t2.y),
+                      u64(t2.z, t2.w));
     }
 }
 
@@ -401,22 +471,27 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     W.nplanes = kld(&K->nplanes);
     W.nsteps = kld(&K->nsteps);
     W.srcH = kld(&K->srcH);
-    W.Pb = kld(&K->P);
-    W.stage_b = kld(&K->stage);
+    W.stage = kld(&K->stage);
+    W.SB = kld(&K->SB);
+    W.FA = kld(&K->FA);
     const Strip5 *S = kld(&K->strips) + J.strip;
     W.L = kld(&S->L);
     W.cpr = kld(&S->cpr);
+    W.Pb = kld(&S->Pb);
+    W.PS = kld(&S->PS);
+    W.nsi = kld(&S->nsi);
     W.ne = kld(&S->nent[W.wave]);
     const Ent5 *ents = kld(&K->ents) + kld(&S->ent0[W.wave]);
     const uint32_t *bf = kld(&K->bfrag);
     const bool chroma = W.nplanes == 2;
     const bool nv12c = SRC == kSrcNV12 && chroma;
+    const int nlp = kld(&K->nlp);
 
     // ---- this wave's H entries: B fragments in VGPRs, per-lane LDS addresses ----
     const int g = W.lane >> 4, n = W.lane & 15;
     v4i bh[kL5Ent], bl[kL5Ent];
     uint32_t aad[kL5Ent], whi[kL5Ent], wlo[kL5Ent], pos[kL5Ent], rr[kL5Ent];
-    uint32_t fl = 0;
+    uint32_t odd = 0;
 #pragma unroll
     for (int i = 0; i < kL5Ent; ++i) {
         bh[i] = bl[i] = (v4i){0, 0, 0, 0};
@@ -424,100 +499,89 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
         rr[i] = 16;
         if (i < W.ne) {
             const Ent5 E = kld(ents + i);
-            const u32x4 *f = reinterpret_cast<const u32x4 *>(bf + (size_t)E.bfrag * 512);
+            const g_u32x4 *f = GP5(const g_u32x4, bf + (size_t)E.bfrag * 512);
             bh[i] = __builtin_bit_cast(v4i, f[W.lane]);
             bl[i] = __builtin_bit_cast(v4i, f[64 + W.lane]);
-            aad[i] = (uint32_t)(W.stage_b + E.plane * kL5Rows * W.Pb + n * W.Pb + E.soff + 8 * g);
+            aad[i] = (uint32_t)(W.stage + (nlp == 2 ? E.plane * W.PS : 0) + n * W.Pb + E.soff + (nv12c ? 16 : 8) * g);
             const Ring5 rg = kld(K->ring + E.ring);
             const uint32_t cb = (uint32_t)((E.col0 + n) * rg.CP + 4 * g);
-            whi[i] = (uint32_t)rg.hi + cb;
-            wlo[i] = (uint32_t)rg.lo + cb;
+            const int nout = E.flags & 16 ? 4 : E.flags & 8 ? 8 : 16;
+            whi[i] = n < nout ? (uint32_t)rg.hi + cb : 0x40000000u;      // out of range: write dropped
+            wlo[i] = n < nout ? (uint32_t)rg.lo + cb : 0x40000000u;
             rr[i] = (uint32_t)rg.RR;
-            fl |= (uint32_t)(E.flags & 3) << (2 * i);
+            odd |= (uint32_t)((E.flags >> 2) & 1) << i;
         }
     }
-    fl = (uint32_t)uni5((int)fl);
-    // ring row of each entry's step: kept in VGPRs (the SGPRs are the scarce file here)
-#pragma unroll
-    for (int i = 0; i < kL5Ent; ++i) {
-        asm volatile("v_mov_b32 %0, %1" : "=v"(pos[i]) : "v"(pos[i]));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(rr[i]) : "v"(rr[i]));
-    }
-    // make the B fragments resident here: otherwise the compiler's wait for them sits
-    // inside the step loop, where it would also drain every prefetch load each step
-#pragma unroll
-    for (int i = 0; i < kL5Ent; ++i) asm volatile("" ::"v"(bh[i]), "v"(bl[i]));
+    odd = (uint32_t)uni5((int)odd);
 
-    // ---- this thread's staging loads ----
-    Loads5 ld;
+    // ---- this item's DMA sources ----
+    Dma5 D;
     {
-        const int nlp = (SRC == kSrcPlanar8 && chroma) ? 2 : 1;
-        ld.nlp = nlp;
         const int bps = nv12c ? 2 : 1;
         for (int lp = 0; lp < 2; ++lp) {
             const int spl = chroma ? (nv12c ? 1 : 1 + lp) : 0;           // source plane
             const int sp = lp < nlp ? spl : 0;
             const uint64_t base = kld(&kargs()->src.data[sp]) + (uint64_t)frame * kld(&kargs()->src.fstride);
             const int64_t pitch = kld(&kargs()->src.pitch[sp]);
-            const uint32_t lo = (uint32_t)uni5((int)(uint32_t)base), hi = (uint32_t)uni5((int)(uint32_t)(base >> 32));
-            ld.rs[lp] = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0,
-                                                          uni5((int)(pitch * W.srcH)), 0x00020000);
-            ld.pitch[lp] = (uint32_t)pitch;
+            D.rs[lp] = rsrc5(base, (uint32_t)(pitch * W.srcH));
+            D.pitch[lp] = (uint32_t)pitch;
         }
-        const int per = kL5Rows * W.cpr;                                  // chunks per load plane
-        const float rc = 1.0f / (float)W.cpr;
-#pragma unroll
-        for (int k = 0; k < kL5MaxLoads; ++k) {
-            const int lp = nlp == 2 ? (k >> 1) : 0;
-            const int c = W.t + 256 * (nlp == 2 ? (k & 1) : k);
-            ld.row[k] = -1;
-            ld.col[k] = 0;
-            ld.dst[k] = 0;
-            if (c < per) {
-                const int row = (int)(((float)c + 0.5f) * rc), cc = c - row * W.cpr;
-                ld.row[k] = row;
-                ld.col[k] = (uint32_t)(W.L * bps + 16 * cc);
-                ld.dst[k] = (uint32_t)(W.stage_b + lp * kL5Rows * W.Pb + row * W.Pb + (nv12c ? 8 : 16) * cc);
-            }
-        }
+        D.rf = rsrc5((uint64_t)(uintptr_t)bf, kld(&K->nbfrag) * 2048u);
+        D.colb = (uint32_t)(W.L * bps);
+        D.rc = 1.0f / (float)W.cpr;
+        D.ipp = W.PS >> 10;
     }
 
     rung_table(lds, S, kld(&K->nrungs), frame, W);
 
-    // ---- prologue: block 0 -> stage 0; block 1 in flight ----
-    u32x4 pre[kL5MaxLoads];
-#pragma unroll
-    for (int k = 0; k < kL5MaxLoads; ++k) pre[k] = (u32x4){0, 0, 0, 0};
-    issue_loads(ld, 0, W, pre);
-    store_stage<SRC>(lds, ld, 0, W, pre, nv12c);
-    issue_loads(ld, 1, W, pre);
+    // ---- prologue: bundles 0 and 1 ----
+    const int4 *vstep = kld(&K->vstep);
+    {
+        const int2 r0 = kld(reinterpret_cast<const int2 *>(vstep) + 1);          // step 0: .z, .w
+        issue_bundle(W, D, 0, 0, 0);
+        issue_bundle(W, D, 1, r0.x, r0.y);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // iteration b (after barrier b - 1: stage b written, H(b - 1) done): V(b - 1), whose
-    // fragments were fetched before the barrier; H(b); stage block b + 1 and issue the
-    // loads of b + 2 (the wait for the previous loads comes after H(b), so it does not
-    // wait on V's stores, which count in the same vmcnt); fetch V(b)'s fragments (its
-    // step record came one iteration earlier); barrier b.  V(b - 1) reads rows H(b) may
-    // be writing elsewhere in the ring: the planner's RR keeps them apart.
-    VPrep5 V;
-    V.e0 = V.e1 = 0;
-    int4 vs = kld(kld(&K->vstep));                          // step 0's record
+    // iteration b (after barrier b - 1: bundle b landed, H(b - 1) done): V(b - 1), its
+    // fragments in bundle b; H(b); bundle b + 2 into the buffer H(b - 1) read; wait for
+    // bundle b + 1 (not b + 2); barrier b.  V(b - 1) reads rows H(b) may be writing
+    // elsewhere in the ring: the planner's RR keeps them apart.
+    // step records, one iteration ahead of their use: V(b - 1)'s groups, and the
+    // fragments bundle b + 2 carries (those of step b + 1)
+    int2 vsV = {0, 0};
+    int2 vsD = W.nsteps > 1 ? kld(reinterpret_cast<const int2 *>(vstep + 1) + 1) : (int2){0, 0};
 #if DTS_L5_STAMP
     unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
 #endif
     for (int b = 0; b <= W.nsteps; ++b) {
-        if (b > 0 && !(DTS_L5_ABLATE & 2)) vrun(lds, K, W, bf, V);
+        const int2 nV = kld(reinterpret_cast<const int2 *>(vstep + b));            // V(b): next iteration
+        const int2 nD = b + 2 < W.nsteps ? kld(reinterpret_cast<const int2 *>(vstep + b + 2) + 1) : (int2){0, 0};
+        if (b > 0 && !(DTS_L5_ABLATE & 2))
+            vrun(lds, K, W, vsV, (uint32_t)(W.stage + (b % kL5Stages) * W.SB + W.FA));
         L5_STAMP(0);
         if (b == W.nsteps) break;
         {
-            const uint32_t boff = (uint32_t)((b & 1) * W.nplanes * kL5Rows * W.Pb);
-            switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
+            const uint32_t boff = (uint32_t)((b % kL5Stages) * W.SB);
+            if (nv12c) {
+                switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
 #define DTS_H5(k) \
-    case k: hstep<k>(lds, bh, bl, aad, whi, wlo, pos, fl, boff); break;
-                DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
+    case k: hstep<k, true>(lds, bh, bl, aad, whi, wlo, pos, odd, boff); break;
+                    DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
 #undef DTS_H5
-            default:
-                break;
+                default:
+                    break;
+                }
+            } else {
+                switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
+#define DTS_H5(k) \
+    case k: hstep<k, false>(lds, bh, bl, aad, whi, wlo, pos, odd, boff); break;
+                    DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
+#undef DTS_H5
+                default:
+                    break;
+                }
             }
 #pragma unroll
             for (int i = 0; i < kL5Ent; ++i) {                 // next step's rows: ring row (16 b) % RR
@@ -526,18 +590,14 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
             }
         }
         L5_STAMP(1);
-        if (b + 1 < W.nsteps) store_stage<SRC>(lds, ld, b + 1, W, pre, nv12c);
+        // after H: the V stores just issued sit in the same memory queue; by now they have drained
+        const int m = b + 2 <= W.nsteps ? issue_bundle(W, D, b + 2, vsD.x, vsD.y) : 0;
         L5_STAMP(2);
-        issue_loads(ld, b + 2, W, pre);
+        vsV = nV;
+        vsD = nD;
         L5_STAMP(3);
-        if (!(DTS_L5_ABLATE & 2)) {
-            V.e0 = vs.x;
-            V.e1 = vs.y;
-            if (vs.x < vs.y) vfrags(bf, vs.z, vs.w, W.lane, V.vh, V.vl);
-            vs = kld(kld(&K->vstep) + b + 1);
-        }
         L5_STAMP(4);
-        __syncthreads();
+        step_barrier(m);
         L5_STAMP(5);
     }
 #if DTS_L5_STAMP
@@ -555,7 +615,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
 // every strip of a frame -- and the source halos neighbouring strips share --
 // stays in one XCD's L2.
 template <int SRC>
-__global__ void __launch_bounds__(256, 2) k_ladder5(const Ladder5Params P)
+__global__ void __launch_bounds__(kL5Threads, 2) k_ladder5(const Ladder5Params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     volatile int *slot = reinterpret_cast<volatile int *>(lds);
@@ -577,7 +637,7 @@ template <int SRC>
 static int occ5(int lds)
 {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&k_ladder5<SRC>), 256,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&k_ladder5<SRC>), kL5Threads,
                                                      (size_t)lds) != hipSuccess)
         return 0;
     return n;
@@ -587,10 +647,10 @@ hipError_t launch_ladder5(const Ladder5Params &p, int src_kind, int lds_bytes, i
 {
     switch (src_kind) {
     case kSrcPlanar8:
-        hipLaunchKernelGGL(k_ladder5<kSrcPlanar8>, dim3((unsigned)grid), dim3(256), lds_bytes, s, p);
+        hipLaunchKernelGGL(k_ladder5<kSrcPlanar8>, dim3((unsigned)grid), dim3(kL5Threads), lds_bytes, s, p);
         break;
     case kSrcNV12:
-        hipLaunchKernelGGL(k_ladder5<kSrcNV12>, dim3((unsigned)grid), dim3(256), lds_bytes, s, p);
+        hipLaunchKernelGGL(k_ladder5<kSrcNV12>, dim3((unsigned)grid), dim3(kL5Threads), lds_bytes, s, p);
         break;
     default:
         return hipErrorInvalidValue;

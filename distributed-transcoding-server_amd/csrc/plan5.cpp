@@ -41,11 +41,12 @@ int vtap(const VTable &v, int y, int row)
     return (int16_t)(d & 1 ? w >> 16 : w & 0xffff);
 }
 
-struct Tile {                       // 16 H outputs of one rendition
-    int base;                       // first staged column of its K blocks (multiple of 8)
-    int nkb;                        // K blocks of 64 columns
+struct Tile {                       // 16 H outputs of one rendition (one V column tile)
+    int split;                      // H entries: 1, 2 or 4 (16 / split outputs each, one K block of
+                                    // 64 source columns per entry)
+    int base[4];                    // first staged column of each entry's K block (multiple of 8)
     int centre;                     // strip assignment key
-    int frag;                       // first B fragment pair
+    int frag;                       // first B fragment pair (split of them)
 };
 
 int round_up(int v, int a) { return (v + a - 1) / a * a; }
@@ -105,20 +106,32 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             if (sum != 1 << 14) return false;
         }
         for (int t0 = 0; t0 < R.dstW; t0 += 16) {
-            int a = 1 << 30, z = -1;
-            for (int i = t0; i < std::min(t0 + 16, R.dstW); ++i) {
-                int ai, zi;
-                extent(f, i, ai, zi);
-                a = std::min(a, ai);
-                z = std::max(z, zi);
+            // split the 16 outputs until every part's taps fit one 64-column K block
+            Tile t{};
+            int A = 1 << 30, Z = -1;
+            for (t.split = 1; t.split <= 4; t.split *= 2) {
+                const int no = 16 / t.split;
+                bool fits = true;
+                for (int s = 0; s < t.split; ++s) {
+                    int a = 1 << 30, z = -1;
+                    for (int i = t0 + s * no; i < std::min(t0 + (s + 1) * no, R.dstW); ++i) {
+                        int ai, zi;
+                        extent(f, i, ai, zi);
+                        a = std::min(a, ai);
+                        z = std::max(z, zi);
+                    }
+                    if (z < 0) a = z = A < (1 << 30) ? A : 0;      // a part past the plane's right edge
+                    t.base[s] = a & ~7;
+                    fits = fits && z - t.base[s] < 64;
+                    A = std::min(A, a);
+                    Z = std::max(Z, z);
+                }
+                if (fits) break;
             }
-            Tile t;
-            t.base = a & ~7;
-            t.nkb = (z - t.base) / 64 + 1;
-            if (t.nkb > 4) return false;
-            t.centre = (a + z) / 2;
+            if (t.split > 4) return false;
+            t.centre = (A + Z) / 2;
             t.frag = nfrag;
-            nfrag += t.nkb;
+            nfrag += t.split;
             tiles[r].push_back(t);
         }
     }
@@ -151,8 +164,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             g.step = std::min(z / kL5Rows, nsteps - 1);
             // V(step) reads rows [w0, z] while H(step + 1) writes [16 (step + 1), 16 (step + 2))
             RR[r] = std::max(RR[r], round_up(kL5Rows * (g.step + 2) - g.w0, 16));
-            g.frag = nfrag;
-            nfrag += g.nkb;
+            g.frag = -1;
             groups[r].push_back(g);
         }
         // the V A reads of a group cover w0 + [0, 64 nkb): with RR >= 64 nkb one
@@ -160,6 +172,22 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         for (const Group &g : groups[r]) RR[r] = std::max(RR[r], 64 * g.nkb);
         if (RR[r] > 4096) return false;
     }
+    // V fragments in step order: the groups of one step are one contiguous run, which
+    // the kernel copies into the step's stage buffer (its fragment area) by LDS-DMA
+    std::vector<int> vf0(nsteps + 1, 0), vkb(nsteps + 1, 0);
+    int FM = 0;                                            // most V K blocks of any step
+    for (int b = 0; b < nsteps; ++b) {
+        vf0[b] = nfrag;
+        for (int r = 0; r < nr; ++r)
+            for (Group &g : groups[r])
+                if (g.step == b) {
+                    g.frag = nfrag;
+                    nfrag += g.nkb;
+                }
+        vkb[b] = nfrag - vf0[b];
+        FM = std::max(FM, vkb[b]);
+    }
+    vf0[nsteps] = nfrag;
     // ---- fragments: H (B = taps of 16 outputs over 64 source columns), V (B = taps of
     // 16 output rows over 64 source rows)
     out.bfrag.assign((size_t)nfrag * 512, 0);
@@ -168,10 +196,11 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         const int dstW = in.rungs[r].dstW;
         for (size_t ti = 0; ti < tiles[r].size(); ++ti) {
             const Tile &t = tiles[r][ti];
-            for (int kb = 0; kb < t.nkb; ++kb) {
-                const bool ok = put_frag(out.bfrag, t.frag + kb, [&](int lane, int k) {
-                    const int o = (int)ti * 16 + (lane & 15);
-                    return o < dstW ? htap(f, o, t.base + 64 * kb + k) : 0;
+            const int no = 16 / t.split;
+            for (int s = 0; s < t.split; ++s) {
+                const bool ok = put_frag(out.bfrag, t.frag + s, [&](int lane, int k) {
+                    const int o = (int)ti * 16 + s * no + (lane & 15);
+                    return (lane & 15) < no && o < dstW ? htap(f, o, t.base[s] + k) : 0;
                 });
                 if (!ok) return false;
             }
@@ -203,7 +232,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
                 e.rows = g.rows;
                 e.w0 = g.w0 % RR[r];                  // ring row of the window start
                 e.nkb = g.nkb;
-                e.bfrag = g.frag;
+                e.foff = (g.frag - vf0[b]) * 2048;
                 e.fmt = in.rungs[r].fmt;
                 e.dstW = in.rungs[r].dstW;
                 out.vsched.push_back(e);
@@ -215,9 +244,10 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         const int e0 = voff[b], e1 = b < nsteps ? voff[b + 1] : e0;
         out.vstep[4 * b] = e0;
         out.vstep[4 * b + 1] = e1;
-        out.vstep[4 * b + 2] = e0 < e1 ? out.vsched[e0].bfrag : 0;
-        out.vstep[4 * b + 3] = e0 < e1 ? out.vsched[e0].nkb : 0;
+        out.vstep[4 * b + 2] = vf0[b];
+        out.vstep[4 * b + 3] = 2 * vkb[b];                  // 1 KB DMA units (hi, lo per K block)
     }
+    const int nlp = in.chroma && !in.nv12_chroma ? 2 : 1;  // load planes
     // ---- strips ---------------------------------------------------------------
     const int bps = in.nv12_chroma ? 2 : 1;
     for (int SW = round_up(std::min(in.srcW, 1024), 16); SW >= 64; SW -= 16) {
@@ -236,28 +266,32 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             }
         }
         bool ok = true;
-        int Wmax = 16;
+        int PSmax = 1024;
         std::vector<int> pcols(nr, 16);
         for (int s = 0; s < nstrips && ok; ++s) {
             Strip5 st{};
             int L = 1 << 30, E = 0;
             for (int r = 0; r < nr; ++r)
-                for (int ti = t0[s][r]; ti < t1[s][r]; ++ti) {
-                    L = std::min(L, tiles[r][ti].base);
-                    E = std::max(E, tiles[r][ti].base + 64 * tiles[r][ti].nkb);
-                }
+                for (int ti = t0[s][r]; ti < t1[s][r]; ++ti)
+                    for (int k = 0; k < tiles[r][ti].split; ++k) {
+                        L = std::min(L, tiles[r][ti].base[k]);
+                        E = std::max(E, tiles[r][ti].base[k] + 64);
+                    }
             if (L == 1 << 30) {
                 L = 0;
                 E = 16;
             }
             L &= ~15;
             const int W = round_up(E - L, 16);
-            Wmax = std::max(Wmax, W);
             st.L = L;
             st.cpr = W * bps / 16;
-            st.nchunk = in.nv12_chroma ? kL5Rows * st.cpr : nplanes * kL5Rows * st.cpr;
-            // staging loads per thread: planar chroma 2 per plane, otherwise 4
-            if (kL5Rows * st.cpr > (in.chroma && !in.nv12_chroma ? 2 : 4) * 256) {
+            st.cpr += 1 - (st.cpr & 1);                    // odd: 16 x odd row pitch
+            st.Pb = 16 * st.cpr;
+            st.PS = round_up(kL5Rows * st.Pb, 1024);       // one DMA instruction never spans two planes
+            st.nsi = nlp * st.PS / 1024;
+            PSmax = std::max(PSmax, st.PS);
+            // DMA instructions per step (source + V fragments), dealt over the waves
+            if ((st.nsi + 2 * FM + kL5Waves - 1) / kL5Waves > kL5MaxDma) {
                 ok = false;
                 break;
             }
@@ -267,32 +301,30 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             for (int r = 0; r < nr; ++r)
                 for (int ti = t0[s][r]; ti < t1[s][r]; ++ti)
                     for (int p = 0; p < nplanes; ++p) list.push_back({r, ti, p});
-            std::stable_sort(list.begin(), list.end(), [&](const TE &a, const TE &b) {
-                return tiles[a.r][a.ti].nkb > tiles[b.r][b.ti].nkb;
-            });
-            std::vector<std::vector<Ent5>> wl(4);
+            std::vector<std::vector<Ent5>> wl(kL5Waves);
+            int wnext = 0;
             for (const TE &e : list) {
                 const Tile &t = tiles[e.r][e.ti];
-                int w = 0;
-                for (int k = 1; k < 4; ++k)
-                    if (wl[k].size() < wl[w].size()) w = k;
-                if ((int)wl[w].size() + t.nkb > kL5Ent) {
-                    ok = false;
-                    break;
-                }
-                for (int kb = 0; kb < t.nkb; ++kb) {
+                for (int k = 0; k < t.split; ++k) {          // entries dealt round robin
+                    const int w = wnext;
+                    wnext = (wnext + 1) % kL5Waves;
+                    if ((int)wl[w].size() >= kL5Ent) {
+                        ok = false;
+                        break;
+                    }
                     Ent5 en{};
-                    en.bfrag = t.frag + kb;
-                    en.soff = (int16_t)(t.base + 64 * kb - L);
-                    en.col0 = (int16_t)(16 * (e.ti - t0[s][e.r]));
+                    en.bfrag = t.frag + k;
+                    en.soff = (int16_t)((t.base[k] - L) * bps);   // byte offset in the staged row
+                    en.col0 = (int16_t)(16 * (e.ti - t0[s][e.r]) + k * (16 / t.split));
                     en.plane = (int8_t)e.plane;
                     en.ring = (int8_t)(e.r * nplanes + e.plane);
-                    en.flags = (int8_t)((kb == 0 ? 1 : 0) | (kb == t.nkb - 1 ? 2 : 0));
+                    en.flags = (int8_t)((in.nv12_chroma && e.plane ? 4 : 0) | (t.split == 1 ? 0 : t.split == 2 ? 8 : 16));
                     wl[w].push_back(en);
                 }
+                if (!ok) break;
             }
             if (!ok) break;
-            for (int w = 0; w < 4; ++w) {
+            for (int w = 0; w < kL5Waves; ++w) {
                 st.ent0[w] = (int)pk.ents.size();
                 st.nent[w] = (int)wl[w].size();
                 pk.ents.insert(pk.ents.end(), wl[w].begin(), wl[w].end());
@@ -305,11 +337,13 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             pk.strips.push_back(st);
         }
         if (!ok) continue;
-        // staged row pitch: 16 x odd bytes >= every strip's width (H A reads conflict-free)
-        pk.P = pitch16odd(Wmax);
+        // stage buffers: the load planes (16 rows each), then the V fragment area
         int lds = 16 + kL5RungTab;                         // the dequeue slot, the per-item rendition table
+        pk.nlp = nlp;
         pk.stage = lds;
-        lds += 2 * nplanes * kL5Rows * pk.P;
+        pk.FA = nlp * PSmax;
+        pk.SB = pk.FA + 2048 * FM;
+        lds += kL5Stages * pk.SB;
         // rings: (rendition, plane), two column-major byte planes each
         pk.nrings = nr * nplanes;
         for (int r = 0; r < nr; ++r)

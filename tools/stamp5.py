@@ -18,7 +18,7 @@ lib.dts_debug_ladder5_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), cty
 buf = (ctypes.c_ulonglong * 16)()
 bench.main()
 lib.dts_debug_ladder5_stamps(buf, 0)
-names = ["V(b-1)", "H(b)", "store_stage", "issue_loads", "vprep", "barrier"]
+names = ["V(b-1)", "H(b)", "dma(b+2)", "vstep", "-", "barrier"]
 waves_steps = buf[15]      # lane 0 of every wave adds its item's step count
 tot = sum(buf[k] for k in range(6))
 print(f"wave-steps {waves_steps}, cycles per wave-step {tot / max(1, waves_steps):.0f}")
