@@ -832,6 +832,7 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
         k.stage = pk.stage;
         k.SB = pk.SB;
         k.FA = pk.FA;
+        k.FB = pk.FB;
         k.nbfrag = (uint32_t)(pk.bfrag.size() / 512);
         k.nrings = pk.nrings;
         k.nrungs = g->spec.nout;

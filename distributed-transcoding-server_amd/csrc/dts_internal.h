@@ -139,9 +139,9 @@ int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
 // copy of the source rows.
 // ---------------------------------------------------------------------------
 constexpr int kL5Rows = 16;         // source rows per step (the H MFMA's M)
-constexpr int kL5Waves = 8;         // waves per workgroup (one workgroup per CU: 2 waves per SIMD)
+constexpr int kL5Waves = 12;        // waves per workgroup (one workgroup per CU: 3 waves per SIMD)
 constexpr int kL5Threads = 64 * kL5Waves;
-constexpr int kL5Ent = 8;           // H entries (K blocks of 64 source columns) per wave
+constexpr int kL5Ent = 5;           // H entries (K blocks of 64 source columns) per wave
 constexpr int kL5MaxRings = 2 * DTS_MAX_OUTPUTS;
 constexpr int kL5Stages = 3;        // stage buffers (bundle s in buffer s % 3: two in flight behind the one H reads)
 constexpr int kL5MaxDma = 15;       // LDS-DMA instructions per wave per step (1 KB each)
@@ -205,9 +205,10 @@ struct Strip5 {                     // one column strip of a plane kind
 struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every rendition
     int32_t nplanes, nsteps, srcH;
     int32_t nlp;                    // load planes (planar chroma 2; luma, nv12 chroma 1: U V interleaved)
-    int32_t stage;                  // byte offset of the kL5Stages stage buffers
-    int32_t SB;                     // stage buffer size: load planes, then the V fragment area
-    int32_t FA;                     // offset of the V fragment area in a stage buffer
+    int32_t stage;                  // byte offset of the kL5Stages stage buffers (source rows)
+    int32_t SB;                     // stage buffer size (load planes)
+    int32_t FA;                     // byte offset of the 2 V fragment buffers (V(b): buffer b & 1)
+    int32_t FB;                     // fragment buffer size
     int32_t nrings, nrungs, nstrips;
     Ring5 ring[kL5MaxRings];        // rendition r, plane p: ring[r * nplanes + p]
     Out5 out[DTS_MAX_OUTPUTS];
@@ -215,7 +216,6 @@ struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every
     const Ent5 *ents;
     const uint32_t *bfrag;          // H, then V fragment pairs (in step order), 512 dwords each
     uint32_t nbfrag;                // fragment pairs
-    int32_t pad_;
     const VEnt5 *vsched;            // the V row groups of every step, step after step
     const int4 *vstep;              // [nsteps + 1]: {first group, end, first V fragment pair, its KB count}
 };

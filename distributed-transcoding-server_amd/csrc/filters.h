@@ -92,7 +92,7 @@ struct Plan5In {
 };
 
 struct Plan5Kind {
-    int nplanes = 1, nsteps = 0, nlp = 1, stage = 0, SB = 0, FA = 0, nrings = 0, lds_bytes = 0, strip_width = 0;
+    int nplanes = 1, nsteps = 0, nlp = 1, stage = 0, SB = 0, FA = 0, FB = 0, nrings = 0, lds_bytes = 0, strip_width = 0;
     Ring5 ring[kL5MaxRings]{};
     Out5 out[DTS_MAX_OUTPUTS]{};
     std::vector<Strip5> strips;

@@ -69,6 +69,10 @@ typedef __attribute__((address_space(1))) uint8_t g_u8;
 
 __device__ __forceinline__ int uni5(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// V works two tiles at once (two independent MFMA chains) when the register budget
+// allows it: 2 waves per SIMD (256 VGPRs), not 4 (128)
+constexpr bool kL5VPair = kL5Waves <= 8;
+
 
 // wave-uniform struct / field read through the constant address space (s_load)
 template <class T>
@@ -100,7 +104,7 @@ __device__ __forceinline__ uint32_t pack_h(int hi, int lo, int hi2, int lo2)
 }
 
 struct Walk5 {
-    int nplanes, nsteps, srcH, stage, SB, FA;
+    int nplanes, nsteps, srcH, stage, SB, FA, FB;
     int L, cpr, Pb, PS, nsi, ne;
     int lane, wave, t;
 };
@@ -138,33 +142,35 @@ __device__ __forceinline__ void dma16(const u32x4 &rs, uint32_t voff, uint32_t m
                  : "memory");
 }
 
-// Bundle s -> stage buffer s % kL5Stages: the 16 source rows of step s (s < nsteps),
-// as stored (row-major, pitch Pb, load plane p at p * PS), then the V fragments of
-// V(s - 1) (vf0, nfu: its step record's first fragment pair and 1 KB units).  Instruction i of the bundle is issued by wave i % kL5Waves; returns how
-// many this wave issued (its vmcnt share of the bundle).
-__device__ __forceinline__ int issue_bundle(const Walk5 &W, const Dma5 &D, int s, int vf0, int nfu)
+// Bundle s -> stage buffer s % kL5Stages: the 16 source rows of step s, as stored
+// (row-major, pitch Pb, load plane p at p * PS).  Instruction i of the bundle is
+// issued by wave i % kL5Waves; returns how many this wave issued (its vmcnt share).
+__device__ __forceinline__ int issue_bundle(const Walk5 &W, const Dma5 &D, int s)
 {
     if (DTS_L5_ABLATE & 4) return 0;
-    const int nsi = s < W.nsteps ? W.nsi : 0;
     const uint32_t buf = (uint32_t)(W.stage + (s % kL5Stages) * W.SB);
     int m = 0;
-    for (int i = W.wave; i < nsi + nfu; i += kL5Waves, ++m) {
-        if (i < nsi) {
-            const int p = i >= D.ipp ? 1 : 0;
-            const int ii = i - p * D.ipp;
-            const int c = 64 * ii + W.lane;
-            const int row = (int)(((float)c + 0.5f) * D.rc), cc = c - row * W.cpr;
-            const int r = min(kL5Rows * s + row, W.srcH - 1);
-            const uint32_t off = (uint32_t)r * (p ? D.pitch[1] : D.pitch[0]) + D.colb + 16u * (uint32_t)cc;
-            dma16(p ? D.rs[1] : D.rs[0], row < kL5Rows ? off : 0x80000000u,
-                  buf + (uint32_t)(p * W.PS) + 1024u * (uint32_t)ii);
-        } else {
-            const int j = i - nsi;
-            dma16(D.rf, (uint32_t)vf0 * 2048u + 1024u * (uint32_t)j + 16u * (uint32_t)W.lane,
-                  buf + (uint32_t)W.FA + 1024u * (uint32_t)j);
-        }
+    for (int i = W.wave; i < W.nsi; i += kL5Waves, ++m) {
+        const int p = i >= D.ipp ? 1 : 0;
+        const int ii = i - p * D.ipp;
+        const int c = 64 * ii + W.lane;
+        const int row = (int)(((float)c + 0.5f) * D.rc), cc = c - row * W.cpr;
+        const int r = min(kL5Rows * s + row, W.srcH - 1);
+        const uint32_t off = (uint32_t)r * (p ? D.pitch[1] : D.pitch[0]) + D.colb + 16u * (uint32_t)cc;
+        dma16(p ? D.rs[1] : D.rs[0], row < kL5Rows ? off : 0x80000000u,
+              buf + (uint32_t)(p * W.PS) + 1024u * (uint32_t)ii);
     }
     return m;
+}
+
+// V(b)'s fragments (nfu 1 KB units from fragment pair vf0 on, one contiguous run)
+// -> fragment buffer b & 1, dealt over the waves after the source instructions
+__device__ __forceinline__ void issue_frags(const Walk5 &W, const Dma5 &D, int b, int vf0, int nfu)
+{
+    if (DTS_L5_ABLATE & 4) return;
+    const uint32_t buf = (uint32_t)(W.FA + (b & 1) * W.FB);
+    for (int j = (W.wave - W.nsi % kL5Waves + kL5Waves) % kL5Waves; j < nfu; j += kL5Waves)
+        dma16(D.rf, (uint32_t)vf0 * 2048u + 1024u * (uint32_t)j + 16u * (uint32_t)W.lane, buf + 1024u * (uint32_t)j);
 }
 
 // End of a step: every DMA of this wave except the m it issued this step (so the
@@ -194,24 +200,42 @@ __device__ __forceinline__ u32x4 lds_rd128(const uint32_t *lds, uint32_t byte)
 // 16 (8, 4) outputs over one 64-column K block; its epilogue writes 4 rows of one
 // column per lane: their y >> 8 and (y & 255) ^ 0x80 bytes (lanes past the
 // entry's outputs hold an out-of-range LDS address: their writes are dropped).
+// Per-entry constants (wave-uniform, SGPRs) and the lane's part of the addresses
+struct HEnt5 {
+    uint32_t ao[kL5Ent];            // stage offset of the entry's K block (+ lane part abase)
+    uint32_t hb[kL5Ent];            // ring hi byte plane + col0 * CP
+    uint32_t dl[kL5Ent];            // lo - hi byte plane offset
+    uint32_t cp[kL5Ent];            // ring column pitch
+    uint32_t no[kL5Ent];            // outputs (16, 8, 4): lanes n >= no write nowhere
+    uint32_t pos[kL5Ent];           // ring row of this step (16 b % RR)
+    uint32_t rr[kL5Ent];
+};
+
+// ring write address of entry i for this lane: column col0 + n, rows 4g..4g+3 of this step
+__device__ __forceinline__ uint32_t hwaddr(const HEnt5 &E, int i, int n, int g)
+{
+    const uint32_t a = E.hb[i] + (uint32_t)n * E.cp[i] + 4u * (uint32_t)g + E.pos[i];
+    return (uint32_t)n < E.no[i] ? a : 0x40000000u;        // out of range: the write is dropped
+}
+
 template <int I0, int NE, bool ILV>
 __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
-                                      const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
-                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t odd,
-                                      uint32_t boff)
+                                      const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff)
 {
     const v4i zero = {0, 0, 0, 0}, bias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
     v4i a[NE], ah[NE], al[NE];
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
         if (ILV) {       // nv12 chroma: U V interleaved as stored; even (U) or odd (V) bytes
-            const u32x4 x = lds_rd128(lds, aad[I0 + i] + boff), y = lds_rd128(lds, aad[I0 + i] + boff + 64);
+            const uint32_t ad = abase + E.ao[I0 + i] + boff;
+            const u32x4 x = lds_rd128(lds, ad), y = lds_rd128(lds, ad + 64);
             const uint32_t sel = (odd >> (I0 + i)) & 1u ? 0x07050301u : 0x06040200u;
             a[i] = __builtin_bit_cast(v4i, (u32x4){__builtin_amdgcn_perm(x.y, x.x, sel), __builtin_amdgcn_perm(x.w, x.z, sel),
                                                    __builtin_amdgcn_perm(y.y, y.x, sel), __builtin_amdgcn_perm(y.w, y.z, sel)} ^
                                                    0x80808080u);
         } else {
-            const u32x2 x = lds_rd64(lds, aad[I0 + i] + boff), y = lds_rd64(lds, aad[I0 + i] + boff + 32);
+            const uint32_t ad = abase + E.ao[I0 + i] + boff;
+            const u32x2 x = lds_rd64(lds, ad), y = lds_rd64(lds, ad + 32);
             a[i] = __builtin_bit_cast(v4i, (u32x4){x.x, x.y, y.x, y.y} ^ 0x80808080u);
         }
     }
@@ -220,7 +244,17 @@ __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], co
     for (int i = 0; i < NE; ++i) {
         ah[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bh[I0 + i], zero, 0, 0, 0);
         al[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bl[I0 + i], bias, 0, 0, 0);
+        if (!kL5VPair) {        // 128-VGPR budget: finish each entry before the next one's MFMAs
+            const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);
+            const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);
+            if (!(DTS_L5_ABLATE & 16)) {
+                const uint32_t w = hwaddr(E, I0 + i, n, g);
+                *lds_at(lds, w) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                *lds_at(lds, w + E.dl[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
+            }
+        }
     }
+    if (!kL5VPair) return;
     if (DTS_L5_ABLATE & 16) {
 #pragma unroll
         for (int i = 0; i < NE; ++i) asm volatile("" ::"v"(ah[i]), "v"(al[i]));
@@ -230,20 +264,19 @@ __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], co
     for (int i = 0; i < NE; ++i) {
         const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);    // rows 4g, 4g+1
         const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);    // rows 4g+2, 4g+3
-        *lds_at(lds, whi[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
-        *lds_at(lds, wlo[I0 + i] + pos[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
+        const uint32_t w = hwaddr(E, I0 + i, n, g);
+        *lds_at(lds, w) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
+        *lds_at(lds, w + E.dl[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
     }
 }
 
 // H(b) of this wave in parts of up to 4 entries
 template <int NE, bool ILV>
 __device__ __forceinline__ void hstep(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
-                                      const uint32_t (&aad)[kL5Ent], const uint32_t (&whi)[kL5Ent],
-                                      const uint32_t (&wlo)[kL5Ent], const uint32_t (&pos)[kL5Ent], uint32_t odd,
-                                      uint32_t boff)
+                                      const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff)
 {
-    hpart<0, (NE < 4 ? NE : 4), ILV>(lds, bh, bl, aad, whi, wlo, pos, odd, boff);
-    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1), ILV>(lds, bh, bl, aad, whi, wlo, pos, odd, boff);
+    hpart<0, (NE < 4 ? NE : 4), ILV>(lds, bh, bl, E, abase, n, g, odd, boff);
+    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1), ILV>(lds, bh, bl, E, abase, n, g, odd, boff);
 }
 
 // V of two (row group, 16-column tile, plane) tiles at once -- two independent
@@ -262,6 +295,30 @@ __device__ __forceinline__ uint32_t vcombine(const v4i &hh, const v4i &hl, const
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+template <int NKB>
+__device__ __forceinline__ uint32_t vtile1(const uint32_t *lds, uint32_t hiA, uint32_t loA, int w0m, int rr,
+                                           const v4i (&vh)[kL5MaxVkb], const v4i (&vl)[kL5MaxVkb], int lane)
+{
+    const v4i zero = {0, 0, 0, 0}, vbias = {kL5VBias, kL5VBias, kL5VBias, kL5VBias};
+    v4i hh = zero, hl = zero, ll = vbias;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        int r0 = w0m + 64 * kb + 8 * (lane >> 4), r1 = r0 + 32;
+        r0 = r0 >= rr ? r0 - rr : r0;
+        r1 = r1 >= rr ? r1 - rr : r1;
+        const u32x2 h0 = lds_rd64(lds, hiA + (uint32_t)r0), h1 = lds_rd64(lds, hiA + (uint32_t)r1);
+        const u32x2 l0 = lds_rd64(lds, loA + (uint32_t)r0), l1 = lds_rd64(lds, loA + (uint32_t)r1);
+        const v4i ah = __builtin_bit_cast(v4i, (u32x4){h0.x, h0.y, h1.x, h1.y});
+        const v4i al = __builtin_bit_cast(v4i, (u32x4){l0.x, l0.y, l1.x, l1.y});
+        hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, vh[kb], hh, 0, 0, 0);
+        hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, vl[kb], hl, 0, 0, 0);
+        ll = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, vl[kb], ll, 0, 0, 0);
+        hl = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, vh[kb], hl, 0, 0, 0);
+    }
+    return vcombine(hh, hl, ll);
+}
+
+// two tiles as two independent chains (when registers allow: kL5VPair)
 template <int NKB>
 __device__ __forceinline__ void vtile2(const uint32_t *lds, uint32_t hiA, uint32_t loA, uint32_t hiB, uint32_t loB,
                                        int w0m, int rr, const v4i (&vh)[kL5MaxVkb], const v4i (&vl)[kL5MaxVkb],
@@ -379,7 +436,13 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
             const uint32_t ha = (uint32_t)VE.ring0.hi + (uint32_t)(16 * ct + n) * CP;
             const uint32_t hb = (uint32_t)VE.ring0.hi + (uint32_t)(16 * ct2 + n) * CP;
             uint32_t wa, wb;
-            vtile2<NKB>(lds, ha, ha + dlo, hb, hb + dlo, VE.w0, VE.ring0.RR, vh, vl, W.lane, wa, wb);
+            if (kL5VPair) {
+                vtile2<NKB>(lds, ha, ha + dlo, hb, hb + dlo, VE.w0, VE.ring0.RR, vh, vl, W.lane, wa, wb);
+            } else {
+                wa = vtile1<NKB>(lds, ha, ha + dlo, VE.w0, VE.ring0.RR, vh, vl, W.lane);
+                __builtin_amdgcn_sched_barrier(0);
+                wb = ct2 != ct ? vtile1<NKB>(lds, hb, hb + dlo, VE.w0, VE.ring0.RR, vh, vl, W.lane) : wa;
+            }
             if (!rowok) continue;
             const int xa = x0 + 16 * ct + 4 * g, xb = x0 + 16 * ct2 + 4 * g;
             if (x0 + 16 * ct2 + 16 <= VE.dstW) {            // both tiles inside the plane (uniform)
@@ -399,8 +462,15 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
         for (int ct = first; ct < nct; ct += kL5Waves) {
             const uint32_t cb = (uint32_t)(16 * ct + n) * CP;
             uint32_t wu, wv;
-            vtile2<NKB>(lds, (uint32_t)VE.ring0.hi + cb, (uint32_t)VE.ring0.lo + cb, (uint32_t)VE.hi1 + cb,
-                        (uint32_t)VE.lo1 + cb, VE.w0, VE.ring0.RR, vh, vl, W.lane, wu, wv);
+            if (kL5VPair) {
+                vtile2<NKB>(lds, (uint32_t)VE.ring0.hi + cb, (uint32_t)VE.ring0.lo + cb, (uint32_t)VE.hi1 + cb,
+                            (uint32_t)VE.lo1 + cb, VE.w0, VE.ring0.RR, vh, vl, W.lane, wu, wv);
+            } else {
+                wu = vtile1<NKB>(lds, (uint32_t)VE.ring0.hi + cb, (uint32_t)VE.ring0.lo + cb, VE.w0, VE.ring0.RR, vh,
+                                 vl, W.lane);
+                __builtin_amdgcn_sched_barrier(0);
+                wv = vtile1<NKB>(lds, (uint32_t)VE.hi1 + cb, (uint32_t)VE.lo1 + cb, VE.w0, VE.ring0.RR, vh, vl, W.lane);
+            }
             const int x = x0 + 16 * ct + 4 * g;
             if (!rowok) continue;
             if (x0 + 16 * ct + 16 <= VE.dstW) {              // the whole tile inside the plane (uniform)
@@ -474,6 +544,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     W.stage = kld(&K->stage);
     W.SB = kld(&K->SB);
     W.FA = kld(&K->FA);
+    W.FB = kld(&K->FB);
     const Strip5 *S = kld(&K->strips) + J.strip;
     W.L = kld(&S->L);
     W.cpr = kld(&S->cpr);
@@ -490,25 +561,26 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     // ---- this wave's H entries: B fragments in VGPRs, per-lane LDS addresses ----
     const int g = W.lane >> 4, n = W.lane & 15;
     v4i bh[kL5Ent], bl[kL5Ent];
-    uint32_t aad[kL5Ent], whi[kL5Ent], wlo[kL5Ent], pos[kL5Ent], rr[kL5Ent];
+    HEnt5 HE;
+    const uint32_t abase = (uint32_t)(n * W.Pb + (nv12c ? 16 : 8) * g);
     uint32_t odd = 0;
 #pragma unroll
     for (int i = 0; i < kL5Ent; ++i) {
         bh[i] = bl[i] = (v4i){0, 0, 0, 0};
-        aad[i] = whi[i] = wlo[i] = pos[i] = 0;
-        rr[i] = 16;
+        HE.ao[i] = HE.hb[i] = HE.dl[i] = HE.cp[i] = HE.no[i] = HE.pos[i] = 0;
+        HE.rr[i] = 16;
         if (i < W.ne) {
             const Ent5 E = kld(ents + i);
             const g_u32x4 *f = GP5(const g_u32x4, bf + (size_t)E.bfrag * 512);
             bh[i] = __builtin_bit_cast(v4i, f[W.lane]);
             bl[i] = __builtin_bit_cast(v4i, f[64 + W.lane]);
-            aad[i] = (uint32_t)(W.stage + (nlp == 2 ? E.plane * W.PS : 0) + n * W.Pb + E.soff + (nv12c ? 16 : 8) * g);
+            HE.ao[i] = (uint32_t)(W.stage + (nlp == 2 ? E.plane * W.PS : 0) + E.soff);
             const Ring5 rg = kld(K->ring + E.ring);
-            const uint32_t cb = (uint32_t)((E.col0 + n) * rg.CP + 4 * g);
-            const int nout = E.flags & 16 ? 4 : E.flags & 8 ? 8 : 16;
-            whi[i] = n < nout ? (uint32_t)rg.hi + cb : 0x40000000u;      // out of range: write dropped
-            wlo[i] = n < nout ? (uint32_t)rg.lo + cb : 0x40000000u;
-            rr[i] = (uint32_t)rg.RR;
+            HE.hb[i] = (uint32_t)(rg.hi + E.col0 * rg.CP);
+            HE.dl[i] = (uint32_t)(rg.lo - rg.hi);
+            HE.cp[i] = (uint32_t)rg.CP;
+            HE.no[i] = E.flags & 16 ? 4u : E.flags & 8 ? 8u : 16u;
+            HE.rr[i] = (uint32_t)rg.RR;
             odd |= (uint32_t)((E.flags >> 2) & 1) << i;
         }
     }
@@ -536,65 +608,59 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
 
     // ---- prologue: bundles 0 and 1 ----
     const int4 *vstep = kld(&K->vstep);
-    {
-        const int2 r0 = kld(reinterpret_cast<const int2 *>(vstep) + 1);          // step 0: .z, .w
-        issue_bundle(W, D, 0, 0, 0);
-        issue_bundle(W, D, 1, r0.x, r0.y);
-    }
+    issue_bundle(W, D, 0);
+    if (W.nsteps > 1) issue_bundle(W, D, 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // iteration b (after barrier b - 1: bundle b landed, H(b - 1) done): V(b - 1), its
-    // fragments in bundle b; H(b); bundle b + 2 into the buffer H(b - 1) read; wait for
-    // bundle b + 1 (not b + 2); barrier b.  V(b - 1) reads rows H(b) may be writing
-    // elsewhere in the ring: the planner's RR keeps them apart.
-    // step records, one iteration ahead of their use: V(b - 1)'s groups, and the
-    // fragments bundle b + 2 carries (those of step b + 1)
-    int2 vsV = {0, 0};
-    int2 vsD = W.nsteps > 1 ? kld(reinterpret_cast<const int2 *>(vstep + 1) + 1) : (int2){0, 0};
+    // iteration b (after barrier b - 1: bundle b and V(b - 1)'s fragments landed, H(b - 1)
+    // done): V(b - 1); H(b); V(b)'s fragments into buffer b & 1 (V(b - 2) read it);
+    // bundle b + 2 into the buffer H(b - 1) read; wait for all but bundle b + 2; barrier b.
+    // V(b - 1) reads rows H(b) may be writing elsewhere in the ring: the planner's RR
+    // keeps them apart.  Step records come one iteration ahead of their use.
+    int2 vsV = {0, 0};                                      // V(b - 1)'s groups
+    int2 vsF = kld(reinterpret_cast<const int2 *>(vstep) + 1);   // V(b)'s fragments
 #if DTS_L5_STAMP
     unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
 #endif
     for (int b = 0; b <= W.nsteps; ++b) {
-        const int2 nV = kld(reinterpret_cast<const int2 *>(vstep + b));            // V(b): next iteration
-        const int2 nD = b + 2 < W.nsteps ? kld(reinterpret_cast<const int2 *>(vstep + b + 2) + 1) : (int2){0, 0};
-        if (b > 0 && !(DTS_L5_ABLATE & 2))
-            vrun(lds, K, W, vsV, (uint32_t)(W.stage + (b % kL5Stages) * W.SB + W.FA));
+        const int2 nV = kld(reinterpret_cast<const int2 *>(vstep + b));
+        const int2 nF = kld(reinterpret_cast<const int2 *>(vstep + b + 1) + 1);
+        if (b > 0 && !(DTS_L5_ABLATE & 2)) vrun(lds, K, W, vsV, (uint32_t)(W.FA + ((b - 1) & 1) * W.FB));
         L5_STAMP(0);
         if (b == W.nsteps) break;
-        {
-            const uint32_t boff = (uint32_t)((b % kL5Stages) * W.SB);
-            if (nv12c) {
-                switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
+        const uint32_t boff = (uint32_t)((b % kL5Stages) * W.SB);
+        if (nv12c) {
+            switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
 #define DTS_H5(k) \
-    case k: hstep<k, true>(lds, bh, bl, aad, whi, wlo, pos, odd, boff); break;
-                    DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
+    case k: hstep<k, true>(lds, bh, bl, HE, abase, n, g, odd, boff); break;
+                DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5)
 #undef DTS_H5
-                default:
-                    break;
-                }
-            } else {
-                switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
-#define DTS_H5(k) \
-    case k: hstep<k, false>(lds, bh, bl, aad, whi, wlo, pos, odd, boff); break;
-                    DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5) DTS_H5(6) DTS_H5(7) DTS_H5(8)
-#undef DTS_H5
-                default:
-                    break;
-                }
+            default:
+                break;
             }
+        } else {
+            switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
+#define DTS_H5(k) \
+    case k: hstep<k, false>(lds, bh, bl, HE, abase, n, g, odd, boff); break;
+                DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5)
+#undef DTS_H5
+            default:
+                break;
+            }
+        }
 #pragma unroll
-            for (int i = 0; i < kL5Ent; ++i) {                 // next step's rows: ring row (16 b) % RR
-                const uint32_t np = pos[i] + 16;
-                pos[i] = np >= rr[i] ? 0 : np;
-            }
+        for (int i = 0; i < kL5Ent; ++i) {                  // next step's rows: ring row (16 b) % RR
+            const uint32_t np = HE.pos[i] + 16;
+            HE.pos[i] = np >= HE.rr[i] ? 0 : np;
         }
         L5_STAMP(1);
         // after H: the V stores just issued sit in the same memory queue; by now they have drained
-        const int m = b + 2 <= W.nsteps ? issue_bundle(W, D, b + 2, vsD.x, vsD.y) : 0;
+        issue_frags(W, D, b, vsF.x, vsF.y);
+        const int m = b + 2 < W.nsteps ? issue_bundle(W, D, b + 2) : 0;
         L5_STAMP(2);
         vsV = nV;
-        vsD = nD;
+        vsF = nF;
         L5_STAMP(3);
         L5_STAMP(4);
         step_barrier(m);
@@ -615,7 +681,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
 // every strip of a frame -- and the source halos neighbouring strips share --
 // stays in one XCD's L2.
 template <int SRC>
-__global__ void __launch_bounds__(kL5Threads, 2) k_ladder5(const Ladder5Params P)
+__global__ void __launch_bounds__(kL5Threads, kL5Waves / 4) k_ladder5(const Ladder5Params P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     volatile int *slot = reinterpret_cast<volatile int *>(lds);

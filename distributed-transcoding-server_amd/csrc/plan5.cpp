@@ -4,6 +4,8 @@
 // libswscale ones (filters.cpp sws_build_filter = FFmpeg 4.4 utils.c
 // initFilter), re-laid for v_mfma_i32_16x16x64_i8; nothing here changes a tap.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "filters.h"
@@ -161,19 +163,61 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             g.w0 = a & ~7;
             g.nkb = (z - g.w0) / 64 + 1;
             if (g.nkb > kL5MaxVkb) return false;
-            g.step = std::min(z / kL5Rows, nsteps - 1);
-            // V(step) reads rows [w0, z] while H(step + 1) writes [16 (step + 1), 16 (step + 2))
-            RR[r] = std::max(RR[r], round_up(kL5Rows * (g.step + 2) - g.w0, 16));
+            g.step = std::min(z / kL5Rows, nsteps - 1);      // ready: after H(step)
             g.frag = -1;
             groups[r].push_back(g);
         }
+    }
+    // ---- V schedule: groups run at their ready step or up to kMaxDefer steps later, so
+    // that no step runs more than `cap` K blocks (the fragment buffers are sized by the
+    // busiest step; a later step costs its ring 16 more rows: measured, the rings cost
+    // more LDS than the fragment buffers save, so kMaxDefer = 0) --------------------
+    constexpr int kMaxDefer = 0;
+    {
+        struct QG { int r, G, ready; };
+        std::vector<QG> order;
+        int maxkb = 1;
+        for (int r = 0; r < nr; ++r)
+            for (int G = 0; G < (int)groups[r].size(); ++G) {
+                order.push_back({r, G, groups[r][G].step});
+                maxkb = std::max(maxkb, groups[r][G].nkb);
+            }
+        std::stable_sort(order.begin(), order.end(), [](const QG &a, const QG &b) { return a.ready < b.ready; });
+        for (int cap = maxkb;; ++cap) {
+            bool ok = true;
+            size_t q = 0;
+            std::vector<int> when(order.size(), -1);
+            for (int b = 0; b < nsteps && ok; ++b) {
+                int used = 0;
+                for (size_t k = q; k < order.size() && order[k].ready <= b; ++k) {
+                    if (when[k] >= 0) continue;
+                    const int nkb = groups[order[k].r][order[k].G].nkb;
+                    if (used + nkb > cap && b < nsteps - 1) {
+                        if (b - order[k].ready >= kMaxDefer) ok = false;   // too late: raise the cap
+                        continue;
+                    }
+                    when[k] = b;
+                    used += nkb;
+                }
+                while (q < order.size() && when[q] >= 0) ++q;
+            }
+            if (!ok) continue;
+            for (size_t k = 0; k < order.size(); ++k) groups[order[k].r][order[k].G].step = when[k];
+            break;
+        }
+    }
+    for (int r = 0; r < nr; ++r) {
+        // V(step) reads rows [w0, z] while H(step + 1) writes [16 (step + 1), 16 (step + 2));
         // the V A reads of a group cover w0 + [0, 64 nkb): with RR >= 64 nkb one
-        // conditional subtract wraps them (ladder5.hip vtile)
-        for (const Group &g : groups[r]) RR[r] = std::max(RR[r], 64 * g.nkb);
+        // conditional subtract wraps them (ladder5.hip vtile2)
+        for (const Group &g : groups[r]) {
+            RR[r] = std::max(RR[r], round_up(kL5Rows * (g.step + 2) - g.w0, 16));
+            RR[r] = std::max(RR[r], 64 * g.nkb);
+        }
         if (RR[r] > 4096) return false;
     }
     // V fragments in step order: the groups of one step are one contiguous run, which
-    // the kernel copies into the step's stage buffer (its fragment area) by LDS-DMA
+    // the kernel copies into a fragment buffer by LDS-DMA the step before they run
     std::vector<int> vf0(nsteps + 1, 0), vkb(nsteps + 1, 0);
     int FM = 0;                                            // most V K blocks of any step
     for (int b = 0; b < nsteps; ++b) {
@@ -290,8 +334,8 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             st.PS = round_up(kL5Rows * st.Pb, 1024);       // one DMA instruction never spans two planes
             st.nsi = nlp * st.PS / 1024;
             PSmax = std::max(PSmax, st.PS);
-            // DMA instructions per step (source + V fragments), dealt over the waves
-            if ((st.nsi + 2 * FM + kL5Waves - 1) / kL5Waves > kL5MaxDma) {
+            // source DMA instructions per step, dealt over the waves
+            if ((st.nsi + kL5Waves - 1) / kL5Waves > kL5MaxDma) {
                 ok = false;
                 break;
             }
@@ -341,9 +385,14 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         int lds = 16 + kL5RungTab;                         // the dequeue slot, the per-item rendition table
         pk.nlp = nlp;
         pk.stage = lds;
-        pk.FA = nlp * PSmax;
-        pk.SB = pk.FA + 2048 * FM;
+        pk.SB = nlp * PSmax;
         lds += kL5Stages * pk.SB;
+        pk.FA = lds;                                       // 2 fragment buffers (V(b) in buffer b & 1)
+        pk.FB = 2048 * std::max(FM, 1);
+        lds += 2 * pk.FB;
+        if (std::getenv("DTS_PLAN_DEBUG"))
+            std::fprintf(stderr, "plan5 %s SW %d FM %d SB %d lds %d RR %d %d %d\n", in.chroma ? "chroma" : "luma", SW, FM,
+                         pk.SB, lds, RR[0], nr > 1 ? RR[1] : 0, nr > 2 ? RR[2] : 0);
         // rings: (rendition, plane), two column-major byte planes each
         pk.nrings = nr * nplanes;
         for (int r = 0; r < nr; ++r)
