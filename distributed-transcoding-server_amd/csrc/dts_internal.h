@@ -138,12 +138,15 @@ int ladder4_blocks_per_cu(int src_kind, int lds_bytes);
 // (v_mfma_i32_16x16x64_i8), every rendition of a column strip from one staged
 // copy of the source rows.
 // ---------------------------------------------------------------------------
-constexpr int kL5Rows = 16;         // source rows per step (the H MFMA's M)
+constexpr int kL5Rows = 16;         // source rows of one H row block (the H MFMA's M)
+constexpr int kL5Blk = 2;           // H row blocks per step (one barrier per step)
+constexpr int kL5StepRows = kL5Rows * kL5Blk;
 constexpr int kL5Waves = 12;        // waves per workgroup (one workgroup per CU: 3 waves per SIMD)
 constexpr int kL5Threads = 64 * kL5Waves;
 constexpr int kL5Ent = 5;           // H entries (K blocks of 64 source columns) per wave
 constexpr int kL5MaxRings = 2 * DTS_MAX_OUTPUTS;
 constexpr int kL5Stages = 3;        // stage buffers (bundle s in buffer s % 3: two in flight behind the one H reads)
+constexpr int kL5FragBufs = 2;      // V fragment buffers (V(b)'s in buffer b % 2, loaded the step before)
 constexpr int kL5MaxDma = 15;       // LDS-DMA instructions per wave per step (1 KB each)
 constexpr int kL5MaxVkb = 2;        // V K blocks (64 source rows) per row group
 constexpr int kL5Bias = 128 << 14;  // 128 * sum(H taps): the (src ^ 0x80) offset of every H output
@@ -196,7 +199,8 @@ struct Strip5 {                     // one column strip of a plane kind
     int32_t Pb;                     // staged row pitch = 16 cpr bytes (16 x odd: conflict-free A reads)
     int32_t PS;                     // load plane stride in a stage buffer (16 rows, rounded up to 1 KB)
     int32_t nsi;                    // source LDS-DMA instructions per step (load planes x PS / 1 KB)
-    int32_t pad_[3];
+    int32_t hextra;                 // waves 0 .. hextra - 1 hold one H entry more than the rest
+    int32_t pad_[2];
     int32_t ent0[kL5Waves], nent[kL5Waves];   // each wave's H entries
     int32_t x0[DTS_MAX_OUTPUTS];    // first output column per rendition (multiple of 16)
     int32_t nct[DTS_MAX_OUTPUTS];   // 16-column tiles per rendition
@@ -207,7 +211,7 @@ struct Kind5 {                      // luma (1 plane) or chroma (U + V) of every
     int32_t nlp;                    // load planes (planar chroma 2; luma, nv12 chroma 1: U V interleaved)
     int32_t stage;                  // byte offset of the kL5Stages stage buffers (source rows)
     int32_t SB;                     // stage buffer size (load planes)
-    int32_t FA;                     // byte offset of the 2 V fragment buffers (V(b): buffer b & 1)
+    int32_t FA;                     // byte offset of the kL5FragBufs V fragment buffers (V(b): buffer b % 2)
     int32_t FB;                     // fragment buffer size
     int32_t nrings, nrungs, nstrips;
     Ring5 ring[kL5MaxRings];        // rendition r, plane p: ring[r * nplanes + p]

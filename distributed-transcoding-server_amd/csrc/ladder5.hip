@@ -30,8 +30,8 @@
 #include "dts_internal.h"
 
 #ifndef DTS_L5_ABLATE
-#define DTS_L5_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip source loads, 8 skip V stores,
-                            // 16 skip the H epilogue (MFMAs kept)
+#define DTS_L5_ABLATE 0     // diagnostic builds only: 1 skip H, 2 skip V, 4 skip every DMA, 8 skip V stores,
+                            // 16 skip the H epilogue (MFMAs kept), 32 skip the source DMA (fragments kept)
 #endif
 
 #ifndef DTS_L5_STAMP
@@ -106,6 +106,7 @@ __device__ __forceinline__ uint32_t pack_h(int hi, int lo, int hi2, int lo2)
 struct Walk5 {
     int nplanes, nsteps, srcH, stage, SB, FA, FB;
     int L, cpr, Pb, PS, nsi, ne;
+    int vrank;                      // V tile order: the waves with fewer H entries first
     int lane, wave, t;
 };
 
@@ -147,7 +148,7 @@ __device__ __forceinline__ void dma16(const u32x4 &rs, uint32_t voff, uint32_t m
 // issued by wave i % kL5Waves; returns how many this wave issued (its vmcnt share).
 __device__ __forceinline__ int issue_bundle(const Walk5 &W, const Dma5 &D, int s)
 {
-    if (DTS_L5_ABLATE & 4) return 0;
+    if (DTS_L5_ABLATE & (4 | 32)) return 0;
     const uint32_t buf = (uint32_t)(W.stage + (s % kL5Stages) * W.SB);
     int m = 0;
     for (int i = W.wave; i < W.nsi; i += kL5Waves, ++m) {
@@ -155,40 +156,48 @@ __device__ __forceinline__ int issue_bundle(const Walk5 &W, const Dma5 &D, int s
         const int ii = i - p * D.ipp;
         const int c = 64 * ii + W.lane;
         const int row = (int)(((float)c + 0.5f) * D.rc), cc = c - row * W.cpr;
-        const int r = min(kL5Rows * s + row, W.srcH - 1);
+        const int r = min(kL5StepRows * s + row, W.srcH - 1);
         const uint32_t off = (uint32_t)r * (p ? D.pitch[1] : D.pitch[0]) + D.colb + 16u * (uint32_t)cc;
-        dma16(p ? D.rs[1] : D.rs[0], row < kL5Rows ? off : 0x80000000u,
+        dma16(p ? D.rs[1] : D.rs[0], row < kL5StepRows ? off : 0x80000000u,
               buf + (uint32_t)(p * W.PS) + 1024u * (uint32_t)ii);
     }
     return m;
 }
 
 // V(b)'s fragments (nfu 1 KB units from fragment pair vf0 on, one contiguous run)
-// -> fragment buffer b & 1, dealt over the waves after the source instructions
-__device__ __forceinline__ void issue_frags(const Walk5 &W, const Dma5 &D, int b, int vf0, int nfu)
+// -> fragment buffer b % kL5FragBufs, dealt over the waves after the source
+// instructions; returns how many this wave issued
+__device__ __forceinline__ int issue_frags(const Walk5 &W, const Dma5 &D, int b, int vf0, int nfu)
 {
-    if (DTS_L5_ABLATE & 4) return;
-    const uint32_t buf = (uint32_t)(W.FA + (b & 1) * W.FB);
-    for (int j = (W.wave - W.nsi % kL5Waves + kL5Waves) % kL5Waves; j < nfu; j += kL5Waves)
+    if (DTS_L5_ABLATE & 4) return 0;
+    const uint32_t buf = (uint32_t)(W.FA + (b % kL5FragBufs) * W.FB);
+    int m = 0;
+    for (int j = (W.wave - W.nsi % kL5Waves + kL5Waves) % kL5Waves; j < nfu; j += kL5Waves, ++m)
         dma16(D.rf, (uint32_t)vf0 * 2048u + 1024u * (uint32_t)j + 16u * (uint32_t)W.lane, buf + 1024u * (uint32_t)j);
+    return m;
 }
 
-// End of a step: every DMA of this wave except the m it issued this step (so the
-// next bundle's) has landed, the ring writes too; then the barrier.  A raw barrier:
+// End of a step: every load of this wave except its m youngest memory operations (the
+// bundle it issued this step and the V stores after it) has landed, the ring writes
+// too; then the barrier.  A raw barrier:
 // __syncthreads() would also wait for the DMAs still in flight.
-__device__ __forceinline__ void step_barrier(int m)
+__device__ __forceinline__ void step_wait(int m)
 {
 #define DTS_W5(k) \
-    case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    switch (m) {
-        DTS_W5(1) DTS_W5(2) DTS_W5(3) DTS_W5(4) DTS_W5(5) DTS_W5(6) DTS_W5(7) DTS_W5(8) DTS_W5(9)
-        DTS_W5(10) DTS_W5(11) DTS_W5(12) DTS_W5(13) DTS_W5(14) DTS_W5(15)
+    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+#define DTS_W5x8(k) DTS_W5(k) DTS_W5(k + 1) DTS_W5(k + 2) DTS_W5(k + 3) DTS_W5(k + 4) DTS_W5(k + 5) DTS_W5(k + 6) DTS_W5(k + 7)
+    switch (m < 63 ? m : 63) {                 // fewer than issued: waits longer, never shorter
+        DTS_W5x8(0) DTS_W5x8(8) DTS_W5x8(16) DTS_W5x8(24) DTS_W5x8(32) DTS_W5x8(40) DTS_W5x8(48)
+        DTS_W5(56) DTS_W5(57) DTS_W5(58) DTS_W5(59) DTS_W5(60) DTS_W5(61) DTS_W5(62) DTS_W5(63)
     default:
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         break;
     }
+#undef DTS_W5x8
 #undef DTS_W5
 }
+
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ u32x4 lds_rd128(const uint32_t *lds, uint32_t byte)
 {
@@ -211,14 +220,18 @@ struct HEnt5 {
     uint32_t rr[kL5Ent];
 };
 
-// ring write address of entry i for this lane: column col0 + n, rows 4g..4g+3 of this step
+// ring write address of entry i for this lane: column col0 + n, rows 4g..4g+3 of row
+// block BLK of this step
+template <int BLK>
 __device__ __forceinline__ uint32_t hwaddr(const HEnt5 &E, int i, int n, int g)
 {
-    const uint32_t a = E.hb[i] + (uint32_t)n * E.cp[i] + 4u * (uint32_t)g + E.pos[i];
+    uint32_t p = E.pos[i] + (uint32_t)(kL5Rows * BLK);
+    p = p >= E.rr[i] ? p - E.rr[i] : p;
+    const uint32_t a = E.hb[i] + (uint32_t)n * E.cp[i] + 4u * (uint32_t)g + p;
     return (uint32_t)n < E.no[i] ? a : 0x40000000u;        // out of range: the write is dropped
 }
 
-template <int I0, int NE, bool ILV>
+template <int I0, int NE, bool ILV, int BLK>
 __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
                                       const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff)
 {
@@ -248,7 +261,7 @@ __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], co
             const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);
             const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);
             if (!(DTS_L5_ABLATE & 16)) {
-                const uint32_t w = hwaddr(E, I0 + i, n, g);
+                const uint32_t w = hwaddr<BLK>(E, I0 + i, n, g);
                 *lds_at(lds, w) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
                 *lds_at(lds, w + E.dl[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
             }
@@ -264,19 +277,30 @@ __device__ __forceinline__ void hpart(uint32_t *lds, const v4i (&bh)[kL5Ent], co
     for (int i = 0; i < NE; ++i) {
         const uint32_t p0 = pack_h(ah[i].x, al[i].x, ah[i].y, al[i].y);    // rows 4g, 4g+1
         const uint32_t p1 = pack_h(ah[i].z, al[i].z, ah[i].w, al[i].w);    // rows 4g+2, 4g+3
-        const uint32_t w = hwaddr(E, I0 + i, n, g);
+        const uint32_t w = hwaddr<BLK>(E, I0 + i, n, g);
         *lds_at(lds, w) = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
         *lds_at(lds, w + E.dl[I0 + i]) = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
     }
 }
 
 // H(b) of this wave in parts of up to 4 entries
+template <int NE, bool ILV, int BLK>
+__device__ __forceinline__ void hblock(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
+                                       const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff)
+{
+    hpart<0, (NE < 4 ? NE : 4), ILV, BLK>(lds, bh, bl, E, abase, n, g, odd, boff);
+    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1), ILV, BLK>(lds, bh, bl, E, abase, n, g, odd, boff);
+}
+
+// H of a step: its kL5Blk row blocks (staged kL5Rows rows apart)
 template <int NE, bool ILV>
 __device__ __forceinline__ void hstep(uint32_t *lds, const v4i (&bh)[kL5Ent], const v4i (&bl)[kL5Ent],
-                                      const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff)
+                                      const HEnt5 &E, uint32_t abase, int n, int g, uint32_t odd, uint32_t boff,
+                                      uint32_t blkb)
 {
-    hpart<0, (NE < 4 ? NE : 4), ILV>(lds, bh, bl, E, abase, n, g, odd, boff);
-    if (NE > 4) hpart<4, (NE > 4 ? NE - 4 : 1), ILV>(lds, bh, bl, E, abase, n, g, odd, boff);
+    static_assert(kL5Blk == 2, "two row blocks per step");
+    hblock<NE, ILV, 0>(lds, bh, bl, E, abase, n, g, odd, boff);
+    hblock<NE, ILV, 1>(lds, bh, bl, E, abase, n, g, odd, boff + blkb);
 }
 
 // V of two (row group, 16-column tile, plane) tiles at once -- two independent
@@ -423,7 +447,7 @@ __device__ __forceinline__ void rung_table(uint32_t *lds, const Strip5 *S, int n
 template <int NKB>
 __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, const VEnt5 &VE, const v4i (&vh)[kL5MaxVkb],
                                        const v4i (&vl)[kL5MaxVkb], int first, int nct, int x0, uint32_t pY,
-                                       uint32_t pU, uint32_t pV, uint64_t bY, uint64_t bU, uint64_t bV)
+                                       uint32_t pU, uint32_t pV, uint64_t bY, uint64_t bU, uint64_t bV, int &nst)
 {
     const int n = W.lane & 15, g = W.lane >> 4;
     const int y = 16 * VE.G + n;
@@ -449,6 +473,7 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
                 if (!(DTS_L5_ABLATE & 8)) {
                     *GP5(g_u32, orow + xa) = wa;
                     *GP5(g_u32, orow + xb) = wb;
+                    nst += 2;                               // counted: the step's vmcnt wait skips them
                 }
                 continue;
             }
@@ -478,9 +503,11 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
                 if (!nv) {
                     *GP5(g_u32, urow + x) = wu;
                     *GP5(g_u32, vrow + x) = wv;
+                    nst += 2;
                 } else {                                    // yuv2nv12cX: U0 V0 U1 V1 U2 V2 U3 V3
                     *GP5(g_u32x2, urow + 2 * x) = (u32x2){__builtin_amdgcn_perm(wv, wu, 0x05010400u),
                                                           __builtin_amdgcn_perm(wv, wu, 0x07030602u)};
+                    nst += 1;
                 }
                 continue;
             }
@@ -500,7 +527,8 @@ __device__ __forceinline__ void vgroup(const uint32_t *lds, const Walk5 &W, cons
 
 // V of a step for this wave: the row groups vs.x .. vs.y - 1, fragments from the
 // fragment area fa (LDS byte address) of the step's bundle
-__device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const Walk5 &W, const int2 &vs, uint32_t fa)
+__device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const Walk5 &W, const int2 &vs, uint32_t fa,
+                                     int &nst)
 {
     const VEnt5 *vsched = kld(&K->vsched);
     int rot = 0;
@@ -511,7 +539,7 @@ __device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const 
         const u32x4 t1 = *reinterpret_cast<const u32x4 *>(tb + 4);    // pitch V, 0, base Y
         const u32x4 t2 = *reinterpret_cast<const u32x4 *>(tb + 8);    // base U, base V
         const int nct = uni5((int)t0.y);
-        const int first = (W.wave - rot % kL5Waves + kL5Waves) % kL5Waves;
+        const int first = (W.vrank - rot % kL5Waves + kL5Waves) % kL5Waves;
         rot += nct;
         if (first >= nct) continue;
         v4i vh[kL5MaxVkb], vl[kL5MaxVkb];
@@ -523,10 +551,10 @@ __device__ __forceinline__ void vrun(const uint32_t *lds, const Kind5 *K, const 
         const uint32_t pY = (uint32_t)uni5((int)t0.z), pU = (uint32_t)uni5((int)t0.w), pV = (uint32_t)uni5((int)t1.x);
         if (VE.nkb > 1)
             vgroup<2>(lds, W, VE, vh, vl, first, nct, x0, pY, pU, pV, u64(t1.z, t1.w), u64(t2.x, t2.y),
-                      u64(t2.z, t2.w));
+                      u64(t2.z, t2.w), nst);
         else
             vgroup<1>(lds, W, VE, vh, vl, first, nct, x0, pY, pU, pV, u64(t1.z, t1.w), u64(t2.x, t2.y),
-                      u64(t2.z, t2.w));
+                      u64(t2.z, t2.w), nst);
     }
 }
 
@@ -552,6 +580,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     W.PS = kld(&S->PS);
     W.nsi = kld(&S->nsi);
     W.ne = kld(&S->nent[W.wave]);
+    W.vrank = (W.wave - kld(&S->hextra) + kL5Waves) % kL5Waves;
     const Ent5 *ents = kld(&K->ents) + kld(&S->ent0[W.wave]);
     const uint32_t *bf = kld(&K->bfrag);
     const bool chroma = W.nplanes == 2;
@@ -568,7 +597,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     for (int i = 0; i < kL5Ent; ++i) {
         bh[i] = bl[i] = (v4i){0, 0, 0, 0};
         HE.ao[i] = HE.hb[i] = HE.dl[i] = HE.cp[i] = HE.no[i] = HE.pos[i] = 0;
-        HE.rr[i] = 16;
+        HE.rr[i] = kL5StepRows;
         if (i < W.ne) {
             const Ent5 E = kld(ents + i);
             const g_u32x4 *f = GP5(const g_u32x4, bf + (size_t)E.bfrag * 512);
@@ -614,26 +643,32 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
     __syncthreads();
 
     // iteration b (after barrier b - 1: bundle b and V(b - 1)'s fragments landed, H(b - 1)
-    // done): V(b - 1); H(b); V(b)'s fragments into buffer b & 1 (V(b - 2) read it);
-    // bundle b + 2 into the buffer H(b - 1) read; wait for all but bundle b + 2; barrier b.
+    // done): V(b)'s fragments into buffer b % kL5FragBufs (V(b - 2) read it); V(b - 1);
+    // H(b); bundle b + 2 into the buffer H(b - 1) read; wait for all but bundle b + 2 and
+    // the counted V stores; barrier b.
     // V(b - 1) reads rows H(b) may be writing elsewhere in the ring: the planner's RR
     // keeps them apart.  Step records come one iteration ahead of their use.
     int2 vsV = {0, 0};                                      // V(b - 1)'s groups
-    int2 vsF = kld(reinterpret_cast<const int2 *>(vstep) + 1);   // V(b)'s fragments
+    int2 vsF = kld(reinterpret_cast<const int2 *>(vstep) + 1);       // V(b)'s fragments
 #if DTS_L5_STAMP
     unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
 #endif
     for (int b = 0; b <= W.nsteps; ++b) {
         const int2 nV = kld(reinterpret_cast<const int2 *>(vstep + b));
         const int2 nF = kld(reinterpret_cast<const int2 *>(vstep + b + 1) + 1);
-        if (b > 0 && !(DTS_L5_ABLATE & 2)) vrun(lds, K, W, vsV, (uint32_t)(W.FA + ((b - 1) & 1) * W.FB));
+        // V(b)'s fragments first: the oldest loads of the step
+        if (b < W.nsteps) issue_frags(W, D, b, vsF.x, vsF.y);
+        int nst = 0;                                        // V stores issued (counted)
+        if (b > 0 && !(DTS_L5_ABLATE & 2))
+            vrun(lds, K, W, vsV, (uint32_t)(W.FA + ((b - 1) % kL5FragBufs) * W.FB), nst);
         L5_STAMP(0);
         if (b == W.nsteps) break;
         const uint32_t boff = (uint32_t)((b % kL5Stages) * W.SB);
+        const uint32_t blkb = (uint32_t)(kL5Rows * W.Pb);      // second row block of the step
         if (nv12c) {
             switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
 #define DTS_H5(k) \
-    case k: hstep<k, true>(lds, bh, bl, HE, abase, n, g, odd, boff); break;
+    case k: hstep<k, true>(lds, bh, bl, HE, abase, n, g, odd, boff, blkb); break;
                 DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5)
 #undef DTS_H5
             default:
@@ -642,7 +677,7 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
         } else {
             switch ((DTS_L5_ABLATE & 1) ? 0 : W.ne) {
 #define DTS_H5(k) \
-    case k: hstep<k, false>(lds, bh, bl, HE, abase, n, g, odd, boff); break;
+    case k: hstep<k, false>(lds, bh, bl, HE, abase, n, g, odd, boff, blkb); break;
                 DTS_H5(1) DTS_H5(2) DTS_H5(3) DTS_H5(4) DTS_H5(5)
 #undef DTS_H5
             default:
@@ -650,20 +685,23 @@ __device__ __forceinline__ void run5(const Ladder5Params &P, int frame, const Jo
             }
         }
 #pragma unroll
-        for (int i = 0; i < kL5Ent; ++i) {                  // next step's rows: ring row (16 b) % RR
-            const uint32_t np = HE.pos[i] + 16;
-            HE.pos[i] = np >= HE.rr[i] ? 0 : np;
+        for (int i = 0; i < kL5Ent; ++i) {                  // next step's rows: ring row (32 b) % RR
+            const uint32_t np = HE.pos[i] + kL5StepRows;
+            HE.pos[i] = np >= HE.rr[i] ? np - HE.rr[i] : np;
         }
         L5_STAMP(1);
-        // after H: the V stores just issued sit in the same memory queue; by now they have drained
-        issue_frags(W, D, b, vsF.x, vsF.y);
+        // bundle b + 2 after H: the V stores ahead of it in the memory queue have drained by now
         const int m = b + 2 < W.nsteps ? issue_bundle(W, D, b + 2) : 0;
         L5_STAMP(2);
         vsV = nV;
         vsF = nF;
         L5_STAMP(3);
+        // bundle b + 1 and V(b)'s fragments have landed: younger are this step's V stores
+        // and bundle b + 2
+        step_wait(m);
+        (void)nst;
         L5_STAMP(4);
-        step_barrier(m);
+        step_barrier();
         L5_STAMP(5);
     }
 #if DTS_L5_STAMP

@@ -94,7 +94,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
     const int nr = (int)in.rungs.size();
     if (nr < 1 || nr > DTS_MAX_OUTPUTS) return false;
     const int nplanes = in.chroma ? 2 : 1;
-    const int nsteps = (in.srcH + kL5Rows - 1) / kL5Rows;
+    const int nsteps = (in.srcH + kL5StepRows - 1) / kL5StepRows;
     // ---- H tiles per rendition ---------------------------------------------
     std::vector<std::vector<Tile>> tiles(nr);
     int nfrag = 0;
@@ -163,7 +163,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             g.w0 = a & ~7;
             g.nkb = (z - g.w0) / 64 + 1;
             if (g.nkb > kL5MaxVkb) return false;
-            g.step = std::min(z / kL5Rows, nsteps - 1);      // ready: after H(step)
+            g.step = std::min(z / kL5StepRows, nsteps - 1);  // ready: after H(step)
             g.frag = -1;
             groups[r].push_back(g);
         }
@@ -211,7 +211,8 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         // the V A reads of a group cover w0 + [0, 64 nkb): with RR >= 64 nkb one
         // conditional subtract wraps them (ladder5.hip vtile2)
         for (const Group &g : groups[r]) {
-            RR[r] = std::max(RR[r], round_up(kL5Rows * (g.step + 2) - g.w0, 16));
+            RR[r] = std::max(RR[r], round_up(kL5StepRows * (g.step + 2) - g.w0, 16));
+            RR[r] = std::max(RR[r], kL5StepRows);
             RR[r] = std::max(RR[r], 64 * g.nkb);
         }
         if (RR[r] > 4096) return false;
@@ -331,7 +332,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
             st.cpr = W * bps / 16;
             st.cpr += 1 - (st.cpr & 1);                    // odd: 16 x odd row pitch
             st.Pb = 16 * st.cpr;
-            st.PS = round_up(kL5Rows * st.Pb, 1024);       // one DMA instruction never spans two planes
+            st.PS = round_up(kL5StepRows * st.Pb, 1024);   // one DMA instruction never spans two planes
             st.nsi = nlp * st.PS / 1024;
             PSmax = std::max(PSmax, st.PS);
             // source DMA instructions per step, dealt over the waves
@@ -368,6 +369,7 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
                 if (!ok) break;
             }
             if (!ok) break;
+            st.hextra = wnext;                             // entries were dealt round robin from wave 0
             for (int w = 0; w < kL5Waves; ++w) {
                 st.ent0[w] = (int)pk.ents.size();
                 st.nent[w] = (int)wl[w].size();
@@ -387,9 +389,9 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         pk.stage = lds;
         pk.SB = nlp * PSmax;
         lds += kL5Stages * pk.SB;
-        pk.FA = lds;                                       // 2 fragment buffers (V(b) in buffer b & 1)
+        pk.FA = lds;                                       // fragment buffers (V(b) in buffer b % kL5FragBufs)
         pk.FB = 2048 * std::max(FM, 1);
-        lds += 2 * pk.FB;
+        lds += kL5FragBufs * pk.FB;
         if (std::getenv("DTS_PLAN_DEBUG"))
             std::fprintf(stderr, "plan5 %s SW %d FM %d SB %d lds %d RR %d %d %d\n", in.chroma ? "chroma" : "luma", SW, FM,
                          pk.SB, lds, RR[0], nr > 1 ? RR[1] : 0, nr > 2 ? RR[2] : 0);

@@ -7,7 +7,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DTS_LIB"] = os.path.join(ROOT, "distributed-transcoding-server_amd", "lib", "libdts_stamp.so")
+os.environ["DTS_LIB"] = os.path.join(ROOT, "distributed-transcoding-server_amd", "lib", os.environ.get("STAMP_LIB", "libdts_stamp.so"))
 sys.path.insert(0, ROOT)
 sys.argv = ["bench.py", "--steps", "3", "--warmup", "1", "--no-cpu", "--no-verify"] + sys.argv[1:]
 import bench  # noqa: E402
@@ -18,7 +18,7 @@ lib.dts_debug_ladder5_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), cty
 buf = (ctypes.c_ulonglong * 16)()
 bench.main()
 lib.dts_debug_ladder5_stamps(buf, 0)
-names = ["V(b-1)", "H(b)", "dma(b+2)", "vstep", "-", "barrier"]
+names = ["V(b-1)", "H(b)", "dma(b+2)", "vstep", "dma wait", "barrier"]
 waves_steps = buf[15]      # lane 0 of every wave adds its item's step count
 tot = sum(buf[k] for k in range(6))
 print(f"wave-steps {waves_steps}, cycles per wave-step {tot / max(1, waves_steps):.0f}")
