@@ -22,6 +22,7 @@ host cores; ffmpeg itself is not installed on the box.
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -55,6 +56,16 @@ WORKLOADS = {
              "tonemap": None, "quality": True, "batch": 64,
              "desc": "cfg4: 8K30 yuv420p -> 4K lanczos + per-frame vf_psnr/vf_ssim of the output vs a 4K "
                      "reference"},
+    # BASELINE config 5 on one GPU: a step is one 600-frame segment of the cfg2 ladder plus
+    # vf_psnr/vf_ssim of every rendition against a reference rendition of the same size
+    # (the source scaled with lanczos: computed once, outside the timed region); the
+    # per-segment records (u64 sse[rung][3], f64 ssim_sum[rung][3]) are all-gathered over
+    # RCCL at the end
+    "cfg5": {"src": (SRC_W, SRC_H, D.FMT_YUV420P), "outs": LADDER, "tonemap": None, "quality": False,
+             "rung_quality": True, "batch": 600, "ring": 600,
+             "desc": "cfg5: 2-hour 4K60 ABR ladder as 600-frame segments sharded over GPUs (weak scaling): "
+                     "1080p/720p/854x480 nv12 bicubic + per-rung vf_psnr/vf_ssim vs lanczos reference "
+                     "renditions; per-segment quality records all-gathered over RCCL"},
     # not a BASELINE config: the vf_yadif kernel on a 4K sequence
     "yadif": {"src": (SRC_W, SRC_H, D.FMT_YUV420P), "outs": [(SRC_W, SRC_H, D.FMT_YUV420P, 0)], "tonemap": None,
               "quality": False, "yadif": 0, "batch": 64,
@@ -87,6 +98,15 @@ def frame_bytes(w, h, fmt, pitch_align=256):
     return (off + 4095) // 4096 * 4096
 
 
+def planar420(planes, fmt):
+    """Y, U, V of an 8-bit 4:2:0 frame (nv12 de-interleaved: vf_psnr / vf_ssim take planar
+    yuv420p, so ffmpeg converts nv12 before them)."""
+    if fmt != D.FMT_NV12:
+        return planes
+    uv = planes[1]
+    return [planes[0], uv[:, 0::2].copy(), uv[:, 1::2].copy()]
+
+
 def oracle_outputs(wl, src, qref=None, prev=None, nxt=None):
     """The CPU oracle's outputs (and quality record) for one source frame of workload wl."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -107,6 +127,10 @@ def oracle_outputs(wl, src, qref=None, prev=None, nxt=None):
     if wl["quality"] and qref is not None:
         w, h = wl["outs"][0][:2]
         q = orc.quality_frame(w, h, outs[0], qref)
+    if wl.get("rung_quality"):             # cfg5: every rendition vs its lanczos reference rendition
+        q = [orc.quality_frame(w, h, planar420(o, fmt),
+                               planar420(orc.scale_frame(src, sw, sh, sfmt, w, h, fmt, D.SCALE_LANCZOS), fmt))
+             for (w, h, fmt, _m), o in zip(wl["outs"], outs)]
     return outs, q
 
 
@@ -177,7 +201,7 @@ def unpack_dev_frame(raw, w, h, fmt):
     return planes
 
 
-def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_first=None):
+def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_first=None, rung_qraws=None):
     """Frame 0 of the last batch against the CPU oracle: bit-exact for the
     integer paths, +-1 LSB for the HDR float path, 1e-4 for SSIM."""
     import numpy as np
@@ -196,7 +220,14 @@ def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_firs
             d = np.abs(a.astype(np.int16) - b.astype(np.int16))
             if d.max() > (1 if wl["tonemap"] else 0):
                 return False
-    if wq is not None and qraw is not None:
+    if rung_qraws is not None:             # cfg5: each rendition's record vs the oracle's (lanczos reference)
+        for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
+            oq = wq[k]
+            r = D.QRaw.from_buffer_copy(rung_qraws[k][0].cpu().numpy().tobytes())
+            gq = D.qstat_finalize(w, h, [r])[0]
+            if gq["sse"] != oq["sse"] or abs(gq["ssim_all"] - oq["ssim_all"]) > 1e-4:
+                return False
+    if wq is not None and qraw is not None and not wl.get("rung_quality"):
         w, h = wl["outs"][0][:2]
         r = D.QRaw.from_buffer_copy(qraw[0].cpu().numpy().tobytes())
         gq = D.qstat_finalize(w, h, [r])[0]
@@ -217,6 +248,44 @@ def load_traffic():
         return j.get("hbm_bytes_per_frame"), j.get("tag")
     except Exception:
         return None, None
+
+
+def gather_quality(sse, ssim, world):
+    """cfg5's quality-stat gather, the path's only data collective: every rank's
+    per-segment records -- int64 sse[seg][rung][3] and float64 ssim_sum[seg][rung][3],
+    fixed size, equal segment counts on every rank (weak scaling) -- all-gathered over
+    RCCL (gloo in the CPU tests).  Returns both concatenated in rank order, which is
+    segment order (rank r owns segments segment_base(r) ...), on the host."""
+    if world > 1:
+        gs = [torch.zeros_like(sse) for _ in range(world)]
+        gq = [torch.zeros_like(ssim) for _ in range(world)]
+        dist.all_gather(gs, sse.contiguous())
+        dist.all_gather(gq, ssim.contiguous())
+        sse, ssim = torch.cat(gs), torch.cat(gq)
+    return sse.cpu(), ssim.cpu()
+
+
+def job_quality(outs, sse, ssim, frames_per_segment):
+    """vf_psnr / vf_ssim end-of-stream averages per rendition from the gathered segment
+    records: mse per plane = sum(sse) / (frames * plane pixels), ssim per plane =
+    sum(ssim_sum) / (frames * 4x4-window count), combined over planes by area as the
+    per-frame statistics are (dts_qstat_finalize)."""
+    def psnr(m):
+        return float("inf") if m == 0 else 10 * math.log10(255 * 255 / m)
+    res = []
+    n = sse.shape[0] * frames_per_segment
+    for k, (w, h, _fmt, _m) in enumerate(outs):
+        pw = [w, (w + 1) >> 1, (w + 1) >> 1]
+        ph = [h, (h + 1) >> 1, (h + 1) >> 1]
+        area = sum(a * b for a, b in zip(pw, ph))
+        mse = [int(sse[:, k, c].sum()) / (n * pw[c] * ph[c]) for c in range(3)]
+        ssimp = [float(ssim[:, k, c].sum()) / (n * ((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1)) for c in range(3)]
+        mse_avg = sum(mse[c] * pw[c] * ph[c] / area for c in range(3))
+        ssim_all = sum(ssimp[c] * pw[c] * ph[c] / area for c in range(3))
+        res.append({"rendition": f"{w}x{h}", "frames": n, "psnr": [round(psnr(m), 4) for m in mse],
+                    "psnr_avg": round(psnr(mse_avg), 4), "ssim": [round(x, 6) for x in ssimp],
+                    "ssim_all": round(ssim_all, 6)})
+    return res
 
 
 def segment_base(rank):
@@ -281,12 +350,17 @@ def main():
     if len(runtimes) != 1:
         print(f"WARNING: {len(runtimes)} HIP runtimes mapped: {runtimes}", file=sys.stderr)
     B, R = args.batch, max(args.ring, 2 * args.batch)
+    if "ring" in wl and args.ring == ap.get_default("ring"):
+        R = max(wl["ring"], B)                 # cfg5: one segment resident (7.4 GB), re-read every step
     R = (R // B) * B
+    rungq = bool(wl.get("rung_quality"))
     yadif = wl.get("yadif")
     if yadif is None:
         g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, wl["outs"], quality=D.Q_BOTH if wl["quality"] else D.Q_NONE,
                                      max_batch=B, tonemap=wl["tonemap"]))
         algo_bytes = g.info.algo_bytes_per_frame
+        if rungq:                          # + each rendition's reference read once
+            algo_bytes += sum(g.info.out_frame_bytes[k] for k in range(len(wl["outs"])))
     else:
         g = None
         # each frame of the sequence is new once (prev/next re-reads hit cache) + one output frame
@@ -313,6 +387,44 @@ def main():
         ctx.synth_device(w, h, fmt, 0, 0x0EF, 0, qrd, 1, sptr)
         qraw = torch.zeros((B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev)
 
+    # cfg5: reference renditions (the ring scaled with lanczos) and per-rung quality records
+    qrefs, qraws, seg_sse, seg_ssim = [], [], [], []
+    if rungq:
+        ref_outs = [(w, h, fmt, D.SCALE_LANCZOS) for (w, h, fmt, _m) in wl["outs"]]
+        qg = D.Graph(ctx, D.make_spec(sw, sh, sfmt, ref_outs, max_batch=B))
+        for (w, h, fmt, _m) in wl["outs"]:
+            t = torch.empty((R, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
+            d, _ = dev_batch(t, w, h, fmt)
+            qrefs.append((t, d))
+            qraws.append(torch.zeros((B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev))
+        for i0 in range(0, R, B):
+            sdi = D.DevFrames()
+            for p in range(3):
+                sdi.data[p] = (sd.data[p] or 0) + i0 * sd.frame_stride
+                sdi.pitch[p] = sd.pitch[p]
+            sdi.frame_stride = sd.frame_stride
+            dsts = []
+            for (t, d) in qrefs:
+                dd = D.DevFrames()
+                for p in range(3):
+                    dd.data[p] = (d.data[p] or 0) + i0 * d.frame_stride
+                    dd.pitch[p] = d.pitch[p]
+                dd.frame_stride = d.frame_stride
+                dsts.append(dd)
+            qg.run_device(sdi, B, dsts, stream=sptr)
+        torch.cuda.synchronize(dev)
+        qg.close()
+
+    def qref_batch(k, step):
+        t, d = qrefs[k]
+        i0 = (step * B) % R
+        dd = D.DevFrames()
+        for p in range(3):
+            dd.data[p] = (d.data[p] or 0) + i0 * d.frame_stride
+            dd.pitch[p] = d.pitch[p]
+        dd.frame_stride = d.frame_stride
+        return dd
+
     def batch_src(step):
         i0 = (step * B) % R
         d = D.DevFrames()
@@ -328,6 +440,12 @@ def main():
             return
         g.run_device(batch_src(i), B, ods, qref=qrd, qraw_ptr=qraw.data_ptr() if qraw is not None else 0,
                      stream=sptr)
+        if rungq:                          # every rendition vs its reference, then the segment's record
+            for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
+                ctx.quality_device(w, h, fmt, ods[k], qref_batch(k, i), B, qraws[k].data_ptr(), sptr)
+            if i >= args.warmup:
+                seg_sse.append(torch.stack([q.view(torch.int64)[:, :3].sum(0) for q in qraws]))
+                seg_ssim.append(torch.stack([q.view(torch.float64)[:, 3:].sum(0) for q in qraws]))
 
     for s in range(args.warmup):
         step(s)
@@ -352,6 +470,11 @@ def main():
     # segment records: frames + an output checksum per rank, gathered over RCCL
     checksum = sum(int(o.sum().item()) for o in outs) % (1 << 40)
     frames_total, wall_max, _records = gather_records(args.steps * B, checksum, wall, world, dev)
+    jq = None
+    if rungq:                              # the per-segment quality records of every rank, in segment order
+        all_sse, all_ssim = gather_quality(torch.stack(seg_sse), torch.stack(seg_ssim), world)
+        jq = {"segments": int(all_sse.shape[0]), "frames_per_segment": B,
+              "renditions": job_quality(wl["outs"], all_sse, all_ssim, B)}
 
     verified = None
     if rank == 0 and not args.no_verify:
@@ -360,7 +483,8 @@ def main():
         if wl["quality"]:
             w, h, fmt, _m = wl["outs"][0]
             qhost = D.synth_host(w, h, fmt, 0, 0x0EF, 0)
-        verified = verify_first_frame(wl, first + (last * B) % R, outs, qhost, qraw, ring_first=first)
+        verified = verify_first_frame(wl, first + (last * B) % R, outs, qhost, qraw, ring_first=first,
+                                      rung_qraws=qraws if rungq else None)
     if rank == 0:
         fps = frames_total / wall_max
         algo = algo_bytes
@@ -389,6 +513,8 @@ def main():
                          "traffic_profile": traffic_tag, "kernel_ms_per_launch": round(kern_ms, 4),
                          "frames_per_launch": B},
         }
+        if jq is not None:
+            line["quality"] = jq
         if world == 1 and not args.no_cpu:
             threads = cpu_share()
             line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, threads)

@@ -95,3 +95,45 @@ def test_graph_quality_host_path(ctx):
         want_img = orc.scale_frame(frames[f], sw, sh, 0, w, h, 0, D.SCALE_LANCZOS)
         assert all(np.array_equal(a, b) for a, b in zip(outs[f][0], want_img))
         check_q(qs[f], orc.quality_frame(w, h, want_img, ref[f]))
+
+
+@pytest.mark.parametrize("w,h", [(64, 36), (130, 74), (854, 480)])
+def test_quality_nv12_vs_oracle(ctx, w, h):
+    """nv12 batches (cfg5's renditions): the kernel reads U / V from the interleaved
+    plane; vf_psnr / vf_ssim take planar yuv420p, so the oracle gets the
+    de-interleaved planes (the conversion ffmpeg inserts in front of them)."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(w + h)
+    fr_a = [random_frame(w, h, D.FMT_YUV420P, rng) for _ in range(2)]
+    fr_b = [[np.clip(p.astype(np.int16) + rng.integers(-9, 10, p.shape), 0, 255).astype(np.uint8) for p in f]
+            for f in fr_a]
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    py, puv = (w + 15) // 16 * 16, (2 * cw + 15) // 16 * 16
+    fsz = py * h + puv * ch
+
+    def upload(frames):
+        host = np.zeros((len(frames), fsz), np.uint8)
+        for f, (y, u, v) in enumerate(frames):
+            host[f, :py * h].reshape(h, py)[:, :w] = y
+            uv = host[f, py * h:].reshape(ch, puv)
+            uv[:, 0:2 * cw:2] = u
+            uv[:, 1:2 * cw:2] = v
+        t = torch.from_numpy(host).cuda()
+        d = D.DevFrames()
+        d.data[0], d.pitch[0] = t.data_ptr(), py
+        d.data[1], d.pitch[1] = t.data_ptr() + py * h, puv
+        d.data[2], d.pitch[2] = None, 0
+        d.frame_stride = fsz
+        return t, d
+    ta, da = upload(fr_a)
+    tb, db = upload(fr_b)
+    raw = torch.zeros((2, 6), dtype=torch.float64, device="cuda")
+    ctx.quality_device(w, h, D.FMT_NV12, da, db, 2, raw.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    host = raw.cpu().numpy()
+    for i in range(2):
+        r = D.QRaw()
+        ctypes.memmove(ctypes.addressof(r), host[i].tobytes(), ctypes.sizeof(r))
+        got = D.qstat_finalize(w, h, [r])[0]
+        check_q(got, orc.quality_frame(w, h, fr_a[i], fr_b[i]))

@@ -45,6 +45,73 @@ def test_gather_records_gloo_world2():
     assert out[0][3] != out[1][3]                          # disjoint segments per rank
 
 
+def _qworker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sse, ssim = _segment_records(rank)
+        gs, gq = bench.gather_quality(sse, ssim, world)
+        out[rank] = (gs.numpy().tolist(), gq.numpy().tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+def _segment_records(rank, nseg=3, nrung=3):
+    """Deterministic per-segment quality records of one rank (u64 SSE in int64, f64 SSIM sums)."""
+    g = torch.Generator().manual_seed(100 + rank)
+    sse = torch.randint(0, 1 << 40, (nseg, nrung, 3), generator=g, dtype=torch.int64)
+    ssim = torch.rand((nseg, nrung, 3), generator=g, dtype=torch.float64) * 1e5
+    return sse, ssim
+
+
+def test_gather_quality_gloo_world2():
+    """cfg5's quality-stat all-gather (RCCL on the GPU box) at world size 2 on gloo:
+    every rank ends with every rank's segment records in rank (= segment) order, equal
+    to what a single rank holding all the segments would have."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_qworker, args=(world, _free_port(), out), nprocs=world, join=True)
+    want_sse = torch.cat([_segment_records(r)[0] for r in range(world)])
+    want_ssim = torch.cat([_segment_records(r)[1] for r in range(world)])
+    for rank in range(world):
+        gs, gq = out[rank]
+        assert gs == want_sse.tolist()
+        assert gq == want_ssim.tolist()
+    sys.path.insert(0, ROOT)
+    import bench
+    single = bench.gather_quality(want_sse, want_ssim, 1)
+    assert torch.equal(single[0], want_sse) and torch.equal(single[1], want_ssim)
+
+
+def test_job_quality_matches_per_frame_finish():
+    """Segment sums -> vf_psnr/vf_ssim averages: one frame per segment of a single
+    rendition must equal dts_qstat_finalize's mse_avg / ssim_all over the same records."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import dtsffi as D
+    w, h = 64, 36
+    recs = []
+    for s in range(4):
+        r = D.QRaw()
+        for c in range(3):
+            r.sse[c] = 1000 * (s + 1) + 7 * c
+            r.ssim_sum[c] = 50.0 + s + c
+        recs.append(r)
+    sse = torch.tensor([[list(r.sse)] for r in recs], dtype=torch.int64)
+    ssim = torch.tensor([[list(r.ssim_sum)] for r in recs], dtype=torch.float64)
+    got = bench.job_quality([(w, h, D.FMT_YUV420P, D.SCALE_BICUBIC)], sse, ssim, 1)[0]
+    per = D.qstat_finalize(w, h, recs)
+    mse_avg = sum(q["mse_avg"] for q in per) / 4
+    ssim_all = sum(q["ssim_all"] for q in per) / 4
+    import math
+    assert got["psnr_avg"] == pytest.approx(round(10 * math.log10(255 * 255 / mse_avg), 4))
+    assert got["ssim_all"] == pytest.approx(round(ssim_all, 6))
+    assert got["frames"] == 4
+
+
 def test_gather_records_single():
     sys.path.insert(0, ROOT)
     import bench
