@@ -453,6 +453,98 @@ static napi_value js_run(napi_env env, napi_callback_info info)
     return promise;
 }
 
+/* ---- quality(ctx, w, h, fmt, a[], b[]) -> Promise<qstat[]> --------------- */
+/* vf_psnr + vf_ssim of a[i] against b[i] (8-bit yuv420p / nv12 frames of one size)
+ * on the ctx's GPU, off the event loop (dts_quality_run_host). */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref keep[3];            /* ctx, a, b kept alive */
+    dts_ctx *ctx;
+    dts_frame *a, *b;
+    dts_qstat *q;
+    int w, h, fmt, n, status;
+} quality_job;
+
+static void free_qjob(quality_job *j)
+{
+    free(j->a);
+    free(j->b);
+    free(j->q);
+    free(j);
+}
+
+static void quality_execute(napi_env env, void *data)
+{
+    (void)env;
+    quality_job *j = (quality_job *)data;
+    j->status = dts_quality_run_host(j->ctx, j->w, j->h, j->fmt, j->a, j->b, j->n, j->q);
+}
+
+static void quality_complete(napi_env env, napi_status st, void *data)
+{
+    quality_job *j = (quality_job *)data;
+    if (st != napi_ok || j->status) {
+        napi_value err, msg, code;
+        char buf[160], cb[32];
+        int e = j->status ? j->status : DTS_E_INVAL;
+        snprintf(buf, sizeof buf, "dts quality: %s (%d)", dts_strerror(e), e);
+        snprintf(cb, sizeof cb, "%d", e);
+        napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &msg);
+        napi_create_string_utf8(env, cb, NAPI_AUTO_LENGTH, &code);
+        napi_create_error(env, code, msg, &err);
+        napi_reject_deferred(env, j->deferred, err);
+    } else {
+        napi_value res;
+        napi_create_array_with_length(env, (size_t)j->n, &res);
+        for (int i = 0; i < j->n; ++i) napi_set_element(env, res, (uint32_t)i, qstat_obj(env, &j->q[i]));
+        napi_resolve_deferred(env, j->deferred, res);
+    }
+    for (int k = 0; k < 3; ++k)
+        if (j->keep[k]) napi_delete_reference(env, j->keep[k]);
+    napi_delete_async_work(env, j->work);
+    free_qjob(j);
+}
+
+static napi_value js_quality(napi_env env, napi_callback_info info)
+{
+    size_t argc = 6;
+    napi_value argv[6];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 6) return throw_dts(env, DTS_E_INVAL, "quality(ctx, w, h, fmt, a, b)");
+    quality_job *j = (quality_job *)calloc(1, sizeof(quality_job));
+    if (!j) return throw_dts(env, DTS_E_NOMEM, "quality");
+    if (napi_get_value_external(env, argv[0], (void **)&j->ctx) != napi_ok || !j->ctx) {
+        free_qjob(j);
+        return throw_dts(env, DTS_E_INVAL, "quality: ctx");
+    }
+    napi_get_value_int32(env, argv[1], &j->w);
+    napi_get_value_int32(env, argv[2], &j->h);
+    napi_get_value_int32(env, argv[3], &j->fmt);
+    uint32_t na = 0, nb = 0;
+    if (j->w < 1 || j->h < 1 || (j->fmt != DTS_FMT_YUV420P && j->fmt != DTS_FMT_NV12) ||
+        parse_frames(env, argv[4], &j->a, &na, &j->w, &j->h, &j->fmt, 1) ||
+        parse_frames(env, argv[5], &j->b, &nb, &j->w, &j->h, &j->fmt, 1) || na != nb) {
+        free_qjob(j);
+        return throw_dts(env, DTS_E_INVAL, "quality: frames (8-bit 4:2:0, equal counts, planes that fit)");
+    }
+    j->n = (int)na;
+    j->q = (dts_qstat *)calloc(na ? na : 1, sizeof(dts_qstat));
+    if (!j->q) {
+        free_qjob(j);
+        return throw_dts(env, DTS_E_NOMEM, "quality");
+    }
+    napi_create_reference(env, argv[0], 1, &j->keep[0]);
+    napi_create_reference(env, argv[4], 1, &j->keep[1]);
+    napi_create_reference(env, argv[5], 1, &j->keep[2]);
+    napi_value promise, name;
+    NAPI_OK(env, napi_create_promise(env, &j->deferred, &promise));
+    napi_create_string_utf8(env, "dts_quality", NAPI_AUTO_LENGTH, &name);
+    NAPI_OK(env, napi_create_async_work(env, NULL, name, quality_execute, quality_complete, j, &j->work));
+    NAPI_OK(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
 /* ---- synthFrame(w, h, fmt, pattern, seed, index, frame) ---------------- */
 static napi_value js_synth_frame(napi_env env, napi_callback_info info)
 {
@@ -553,6 +645,7 @@ static napi_value init(napi_env env, napi_value exports)
         {"synthFrame", NULL, js_synth_frame, NULL, NULL, NULL, napi_default, NULL},
         {"frameLayout", NULL, js_frame_layout, NULL, NULL, NULL, napi_default, NULL},
         {"fpsMap", NULL, js_fps_map, NULL, NULL, NULL, napi_default, NULL},
+        {"quality", NULL, js_quality, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

@@ -1234,6 +1234,62 @@ int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
     return quality_enqueue(ctx, ctx->qs, w, h, fmt, *a, *b, nframes, qraw_dev, st);
 }
 
+// Host frames -> device batches -> k_quality -> finished statistics (the Node worker's
+// per-rendition vf_psnr / vf_ssim against a reference rendition).  Synchronous on the
+// ctx's stream 0; device buffers live for the call only.
+int dts_quality_run_host(dts_ctx *ctx, int w, int h, int fmt, const dts_frame *a, const dts_frame *b, int nframes,
+                         dts_qstat *out)
+{
+    if (!ctx || !a || !b || !out || nframes < 0 || w < 1 || h < 1) return DTS_E_INVAL;
+    if (!fmt_8bit(fmt)) return DTS_E_UNSUPPORTED;
+    if (nframes == 0) return DTS_OK;
+    int64_t rowb[3], rows[3];
+    plane_geom(w, h, fmt, rowb, rows);
+    for (int f = 0; f < nframes; ++f)
+        for (int p = 0; p < 3; ++p)
+            if (rowb[p] && (!a[f].data[p] || !b[f].data[p] || a[f].pitch[p] < rowb[p] || b[f].pitch[p] < rowb[p]))
+                return DTS_E_INVAL;
+    hipSetDevice(ctx->device);
+    DevLayout lay;
+    lay.init(w, h, fmt);
+    const size_t fb = (size_t)lay.fstride, n = (size_t)nframes;
+    uint8_t *dev = nullptr;
+    dts_qraw *qd = nullptr;
+    std::vector<dts_qraw> qh(n);
+    hipStream_t st = ctx->stream[0];
+    auto run = [&]() -> int {
+        HIPCHK(ctx, hipMalloc(&dev, 2 * fb * n));
+        HIPCHK(ctx, hipMalloc(&qd, n * sizeof(dts_qraw)));
+        for (size_t f = 0; f < n; ++f)
+            for (int p = 0; p < 3; ++p) {
+                if (!rowb[p]) continue;
+                HIPCHK(ctx, hipMemcpy2DAsync(dev + f * fb + lay.off[p], (size_t)lay.pitch[p], a[f].data[p],
+                                             (size_t)a[f].pitch[p], (size_t)rowb[p], (size_t)rows[p],
+                                             hipMemcpyHostToDevice, st));
+                HIPCHK(ctx, hipMemcpy2DAsync(dev + (n + f) * fb + lay.off[p], (size_t)lay.pitch[p], b[f].data[p],
+                                             (size_t)b[f].pitch[p], (size_t)rowb[p], (size_t)rows[p],
+                                             hipMemcpyHostToDevice, st));
+            }
+        dts_dev_frames da{}, db{};
+        for (int p = 0; p < 3; ++p) {
+            const int pp = rowb[p] ? p : 1;
+            da.data[p] = dev + lay.off[pp];
+            db.data[p] = dev + n * fb + lay.off[pp];
+            da.pitch[p] = db.pitch[p] = lay.pitch[pp];
+        }
+        da.frame_stride = db.frame_stride = (int64_t)fb;
+        int e = quality_enqueue(ctx, ctx->qs, w, h, fmt, da, db, nframes, qd, st);
+        if (e) return e;
+        HIPCHK(ctx, hipMemcpyAsync(qh.data(), qd, n * sizeof(dts_qraw), hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        return dts_qstat_finalize(w, h, qh.data(), nframes, out);
+    };
+    const int e = run();
+    if (dev) hipFree(dev);
+    if (qd) hipFree(qd);
+    return e;
+}
+
 int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames *seq, int nseq,
                          int first, int count, const dts_dev_frames *dst, void *stream)
 {

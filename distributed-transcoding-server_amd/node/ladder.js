@@ -21,7 +21,11 @@ const MAX_OUTPUTS = 4;
 // Jobs.codecSettings is free text in the reference (database.js:78).  The GPU
 // worker reads an optional JSON object from it with the filtergraph knobs a CPU
 // worker would put on its ffmpeg command line:
-//   {"scale": "bicubic", "format": "nv12", "param": [b, c], "tonemap": {"mode": "hable", ...}}
+//   {"scale": "bicubic", "format": "nv12", "param": [b, c], "tonemap": {"mode": "hable", ...},
+//    "quality": "psnr" | "ssim" | "both", "qualityRef": "lanczos"}
+// quality: `[rendition][reference]psnr` / `ssim` per segment against a reference
+// rendition of the same size -- the source scaled with `qualityRef` (default
+// lanczos) -- reported in JobChunks.result.quality.
 function parseSettings(text) {
     if (!text) return {};
     try {
@@ -41,6 +45,19 @@ function outputOf(job) {
     const o = { w: job.width | 0, h: job.height | 0, fmt: fmt, method: method };
     if (Array.isArray(s.param)) o.param = s.param.slice(0, 2);
     return o;
+}
+
+const QUALITY = { psnr: 1, ssim: 2, both: 3, true: 3 };
+
+// {mode: DTS_Q_*, ref: DTS_SCALE_*} or null
+function qualityOf(job) {
+    const s = parseSettings(job.codecSettings);
+    if (!s.quality) return null;
+    const mode = QUALITY[String(s.quality).toLowerCase()];
+    if (mode === undefined) throw new Error("job " + job.id + ": unknown quality " + s.quality);
+    const ref = METHOD[String(s.qualityRef || "lanczos").toLowerCase()];
+    if (ref === undefined) throw new Error("job " + job.id + ": unknown qualityRef " + s.qualityRef);
+    return { mode: mode, ref: ref };
 }
 
 function tonemapOf(job) {
@@ -80,7 +97,18 @@ function planLadders(jobs, sources) {
             const spec = { src: { w: src.w, h: src.h, fmt: src.fmt }, outputs: part.map(outputOf), quality: 0,
                            maxBatch: 32 };
             if (tm) spec.tonemap = tm;
-            plans.push({ sourceID: sid, framerate: part[0].framerate || 0, jobs: part, spec: spec });
+            // per-rendition quality (codecSettings.quality): run by the scheduler after the
+            // ladder, each requesting row against its reference rendition
+            const q = part.map(qualityOf);
+            const quality = q.some(function (x) { return x; }) ? {
+                rows: q.map(function (x) { return x ? x.mode : 0; }),
+                refSpec: { src: spec.src, quality: 0, maxBatch: spec.maxBatch,
+                           outputs: spec.outputs.map(function (o, k) {
+                               return { w: o.w, h: o.h, fmt: o.fmt, method: q[k] ? q[k].ref : o.method };
+                           }) }
+            } : null;
+            if (quality && tm) throw new Error("job " + part[0].id + ": quality with tonemap is not supported");
+            plans.push({ sourceID: sid, framerate: part[0].framerate || 0, jobs: part, spec: spec, quality: quality });
         }
     });
     return plans;
@@ -99,6 +127,33 @@ function fpsFrames(addon, n, srcFps, outFps) {
     return addon.fpsMap(n, srcFps[0], srcFps[1], r[0], r[1]);
 }
 
+// Segment summary of per-frame statistics, as vf_psnr / vf_ssim print at the end of
+// a stream: PSNR from the mean MSE (per plane and area-weighted overall), mean SSIM.
+function summarizeQuality(stats, w, h) {
+    const pw = [w, (w + 1) >> 1, (w + 1) >> 1], ph = [h, (h + 1) >> 1, (h + 1) >> 1];
+    const area = pw[0] * ph[0] + pw[1] * ph[1] + pw[2] * ph[2];
+    const comp = ["y", "u", "v"], n = stats.length;
+    const mse = [0, 0, 0], ssim = [0, 0, 0];
+    let ssimAll = 0;
+    stats.forEach(function (q) {
+        comp.forEach(function (c, i) {
+            mse[i] += q.sse[c] / (pw[i] * ph[i]) / n;
+            ssim[i] += q.ssim[c] / n;
+        });
+        ssimAll += q.ssimAll / n;
+    });
+    const psnr = function (m) { return m === 0 ? Infinity : 10 * Math.log10(255 * 255 / m); };
+    const mseAvg = mse.reduce(function (a, m, i) { return a + m * pw[i] * ph[i] / area; }, 0);
+    const r = { frames: n, psnr: {}, ssim: {} };
+    comp.forEach(function (c, i) {
+        r.psnr[c] = psnr(mse[i]);
+        r.ssim[c] = ssim[i];
+    });
+    r.psnr.avg = psnr(mseAvg);
+    r.ssim.all = ssimAll;
+    return r;
+}
+
 module.exports = { FMT: FMT, METHOD: METHOD, TONEMAP: TONEMAP, MAX_OUTPUTS: MAX_OUTPUTS, parseSettings: parseSettings,
-                   outputOf: outputOf, tonemapOf: tonemapOf, planLadders: planLadders, rateOf: rateOf,
-                   fpsFrames: fpsFrames };
+                   outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, planLadders: planLadders,
+                   rateOf: rateOf, fpsFrames: fpsFrames, summarizeQuality: summarizeQuality };

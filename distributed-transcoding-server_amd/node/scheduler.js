@@ -17,7 +17,15 @@
 //     `assignedTo` is the worker account id, `result` a JSON record (frames,
 //     output bytes, sha1 of each rendition, GPU, ms, quality);
 //   * every status change is reported through `onUpdate(row, fields)`, which is
-//     where a maintainer calls JobChunks.update(...) (database.js:97-129).
+//     where a maintainer calls JobChunks.update(...) (database.js:97-129);
+//   * with `outDir`, the source comes from the Y4M file named by the source row
+//     (`sources[id].path`) and every rendition segment is written as
+//     outDir/job<id>/<chunkOffset>.y4m; once all of a job's chunks are done the
+//     segments are assembled into Jobs.assembledData = {size, chunk: [1 MiB block
+//     ids]} (assemble.js) and reported through `onJobUpdate(job, fields)`;
+//   * `result` carries per-phase timings (readMs, gpuMs, qualityMs, writeMs) and,
+//     for rows whose codecSettings ask for it, the segment's PSNR / SSIM against
+//     the reference rendition (ladder.js qualityOf).
 //
 // The addon's run() executes on the libuv thread pool: set UV_THREADPOOL_SIZE
 // >= the GPU count before the first async call (worker.js does).
@@ -25,7 +33,11 @@
 
 const crypto = require("crypto");
 const EventEmitter = require("events");
+const fs = require("fs");
+const path = require("path");
 const ladder = require("./ladder");
+const y4m = require("./y4m");
+const assemble = require("./assemble");
 
 function planeShapes(w, h, fmt) {
     const cw = (w + 1) >> 1, ch = (h + 1) >> 1;
@@ -58,6 +70,16 @@ function synthSource(addon, seed) {
     };
 }
 
+// Y4M source: frame indices past the end of the file are dropped (the last segment
+// of a job is usually short)
+function y4mSource(readers) {
+    return function (plan, frameIdx) {
+        const r = readers[plan.sourceID];
+        if (!r) throw new Error("source " + plan.sourceID + " has no Y4M path");
+        return frameIdx.filter(function (i) { return i < r.frames; }).map(function (i) { return r.read(i); });
+    };
+}
+
 class GpuSegmentScheduler extends EventEmitter {
     // opts: addon (dts_napi.node or a stand-in), gpus ([device...], default all),
     // workerId (WorkerAccounts id written to assignedTo), maxRetries (2),
@@ -73,8 +95,12 @@ class GpuSegmentScheduler extends EventEmitter {
         this.maxRetries = opts.maxRetries === undefined ? 2 : opts.maxRetries;
         this.segmentFrames = opts.segmentFrames || 600;
         this.source = opts.source || synthSource(this.addon, 0x5EED);
+        this._userSource = !!opts.source;
         this.sink = opts.sink || null;
+        this.outDir = opts.outDir || null;
         this.onUpdate = opts.onUpdate || function () {};
+        this.onJobUpdate = opts.onJobUpdate || function () {};
+        this.readers = {};
         this.slots = this.gpus.map(function (dev) {
             return { dev: dev, ctx: null, graphs: new Map(), busy: false, done: 0, failed: 0, ms: 0 };
         });
@@ -85,10 +111,15 @@ class GpuSegmentScheduler extends EventEmitter {
         return slot.ctx;
     }
 
-    _graph(slot, plan) {
-        const key = plan.key;
-        if (!slot.graphs.has(key)) slot.graphs.set(key, this.addon.createGraph(this._ctx(slot), plan.spec));
+    _graph(slot, plan, ref) {
+        const key = ref ? plan.key + ":ref" : plan.key;
+        if (!slot.graphs.has(key))
+            slot.graphs.set(key, this.addon.createGraph(this._ctx(slot), ref ? plan.quality.refSpec : plan.spec));
         return slot.graphs.get(key);
+    }
+
+    _segmentPath(jobId, off) {
+        return path.join(this.outDir, "job" + jobId, off + ".y4m");
     }
 
     _update(row, fields) {
@@ -105,32 +136,95 @@ class GpuSegmentScheduler extends EventEmitter {
         return local.map(function (i) { return base + i; });
     }
 
-    async _runSegment(slot, task) {
-        const plan = task.plan;
-        const t0 = Date.now();
-        const g = this._graph(slot, plan);
-        const idx = this._frames(plan, task.chunkOffset, plan.srcFps);
-        const src = await this.source(plan, idx);
-        const outs = plan.spec.outputs;
+    _allocOutputs(outs, n) {
         const dst = [], per = outs.map(function () { return []; });
-        src.forEach(function () {
+        for (let i = 0; i < n; ++i)
             outs.forEach(function (o, k) {
                 const f = allocFrame(o.w, o.h, o.fmt);
                 dst.push(f);
                 per[k].push(f);
             });
-        });
-        const quality = await this.addon.run(g, src, dst, null);
-        if (this.sink) await this.sink(plan, task.rows, per);
-        const ms = Date.now() - t0;
+        return { dst: dst, per: per };
+    }
+
+    async _runSegment(slot, task) {
+        const self = this;
+        const plan = task.plan;
+        const t0 = Date.now();
+        const g = this._graph(slot, plan);
+        const idx = this._frames(plan, task.chunkOffset, plan.srcFps);
+        const src = await this.source(plan, idx);
+        const t1 = Date.now();
+        const outs = plan.spec.outputs;
+        const o = this._allocOutputs(outs, src.length);
+        await this.addon.run(g, src, o.dst, null);
+        const t2 = Date.now();
+        // per-rendition PSNR / SSIM against the reference rendition of the same source frames
+        const quality = outs.map(function () { return null; });
+        if (plan.quality && src.length) {
+            const ref = this._allocOutputs(plan.quality.refSpec.outputs, src.length);
+            await this.addon.run(this._graph(slot, plan, true), src, ref.dst, null);
+            for (let k = 0; k < outs.length; ++k) {
+                if (!plan.quality.rows[k]) continue;
+                const st = await this.addon.quality(this._ctx(slot), outs[k].w, outs[k].h, outs[k].fmt, o.per[k],
+                                                    ref.per[k]);
+                const sum = ladder.summarizeQuality(st, outs[k].w, outs[k].h);
+                if (!(plan.quality.rows[k] & 1)) delete sum.psnr;
+                if (!(plan.quality.rows[k] & 2)) delete sum.ssim;
+                quality[k] = sum;
+            }
+        }
+        const t3 = Date.now();
+        const files = outs.map(function () { return null; }), written = outs.map(function () { return 0; });
+        if (this.sink) {
+            await this.sink(plan, task.rows, o.per);
+        } else if (this.outDir) {
+            task.rows.forEach(function (row, k) {
+                if (!row) return;
+                const p = self._segmentPath(row.mainJob, row.chunkOffset);
+                fs.mkdirSync(path.dirname(p), { recursive: true });
+                const fps = plan.framerate ? ladder.rateOf(plan.framerate) : (plan.srcFps || [25, 1]);
+                written[k] = y4m.writeSegment(p, o.per[k], outs[k].w, outs[k].h, outs[k].fmt, fps);
+                files[k] = p;
+            });
+        }
+        const t4 = Date.now();
         return task.rows.map(function (row, k) {
             const h = crypto.createHash("sha1");
             let bytes = 0;
-            per[k].forEach(function (f) {
+            o.per[k].forEach(function (f) {
                 f.data.forEach(function (b) { if (b) { h.update(b); bytes += b.length; } });
             });
-            return { frames: per[k].length, bytes: bytes, sha1: h.digest("hex"), gpu: slot.dev, ms: ms,
-                     width: outs[k].w, height: outs[k].h, fmt: outs[k].fmt, quality: quality };
+            const r = { frames: o.per[k].length, bytes: bytes, sha1: h.digest("hex"), gpu: slot.dev, ms: t4 - t0,
+                        readMs: t1 - t0, gpuMs: t2 - t1, qualityMs: t3 - t2, writeMs: t4 - t3,
+                        width: outs[k].w, height: outs[k].h, fmt: outs[k].fmt };
+            if (quality[k]) r.quality = quality[k];
+            if (files[k]) {
+                r.file = files[k];
+                r.fileBytes = written[k];
+            }
+            return r;
+        });
+    }
+
+    // every chunk of a job done -> its segments assembled into 1 MiB blocks
+    _assembleJobs(jobs, chunks) {
+        const self = this;
+        if (!this.outDir || this.sink) return;
+        jobs.forEach(function (job) {
+            const mine = chunks.filter(function (c) { return c.mainJob === job.id; });
+            if (!mine.length || mine.some(function (c) { return c.status !== "done"; })) return;
+            mine.sort(function (a, b) { return a.chunkOffset - b.chunkOffset; });
+            const files = mine.map(function (c) { return self._segmentPath(job.id, c.chunkOffset); });
+            try {
+                const a = assemble.assembleFiles(files, path.join(self.outDir, "blocks"));
+                const fields = { assembledData: JSON.stringify(a), finished: true };
+                Object.keys(fields).forEach(function (k) { job[k] = fields[k]; });
+                self.onJobUpdate(job, fields);
+                self.emit("jobUpdate", job, fields);
+            } catch (e) {
+                self.emit("updateError", e, job, null);
+            }
         });
     }
 
@@ -139,6 +233,20 @@ class GpuSegmentScheduler extends EventEmitter {
     // once every chunk is "done" or "failed".
     runJobs(jobs, chunks, sources) {
         const self = this;
+        if (this.outDir && !this.sink) {          // Y4M sources: stream geometry / rate from the file header
+            const self = this;
+            Object.keys(sources).forEach(function (sid) {
+                const s = sources[sid];
+                if (!s.path || self.readers[sid]) return;
+                const r = new y4m.Y4MReader(s.path);
+                self.readers[sid] = r;
+                s.w = s.w || r.hdr.w;
+                s.h = s.h || r.hdr.h;
+                s.fmt = s.fmt || 0;
+                s.fps = s.fps || r.hdr.fps;
+            });
+            if (Object.keys(this.readers).length && !this._userSource) this.source = y4mSource(this.readers);
+        }
         const plans = ladder.planLadders(jobs, sources);
         const queue = [];
         plans.forEach(function (plan, pi) {
@@ -168,7 +276,10 @@ class GpuSegmentScheduler extends EventEmitter {
             }
         }
         return new Promise(function (resolve) {
-            if (!total) return resolve(self._summary(0));
+            if (!total) {
+                self._assembleJobs(jobs, chunks);
+                return resolve(self._summary(0));
+            }
             function pull(slot) {
                 if (slot.busy) return;
                 // prefer a task that did not just fail on this GPU
@@ -218,7 +329,10 @@ class GpuSegmentScheduler extends EventEmitter {
                     self.emit("updateError", e, null, null);
                 }).then(function () {
                     slot.busy = false;
-                    if (finished === total) return resolve(self._summary(total));
+                    if (finished === total) {
+                        self._assembleJobs(jobs, chunks);
+                        return resolve(self._summary(total));
+                    }
                     self.slots.forEach(pull);
                 });
             }
@@ -234,4 +348,4 @@ class GpuSegmentScheduler extends EventEmitter {
 }
 
 module.exports = { GpuSegmentScheduler: GpuSegmentScheduler, allocFrame: allocFrame, planeShapes: planeShapes,
-                   synthSource: synthSource };
+                   synthSource: synthSource, y4mSource: y4mSource };

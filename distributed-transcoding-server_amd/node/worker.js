@@ -3,15 +3,19 @@
 // renditions + updated JobChunks rows out (the drop-in for a CPU worker that
 // spawns ffmpeg-static per segment, index.js:9).
 //
-//   node worker.js <job.json> [--dump DIR]
+//   node worker.js <job.json> [--out DIR | --dump DIR]
 //
 // job.json: {"workerId": 1, "segmentFrames": 600, "gpus": [0, ...] (optional),
-//            "sources": {"<sourceID>": {"w": 3840, "h": 2160, "fmt": 0, "fps": [60, 1]}},
+//            "sources": {"<sourceID>": {"path": "src.y4m"} or {"w": 3840, "h": 2160, "fmt": 0,
+//                                                             "fps": [60, 1]}},
 //            "jobs": [Jobs rows], "chunks": [JobChunks rows]}
-// Prints one JSON object: {"chunks": [updated rows], "summary": {...}}.
+// Prints one JSON object: {"chunks": [updated rows], "jobs": [rows], "summary": {...}}.
+// --out DIR: sources with a `path` are read from their Y4M file, every rendition
+// segment is written as DIR/job<id>/<chunkOffset>.y4m and finished jobs get
+// Jobs.assembledData (1 MiB blocks in DIR/blocks) and finished = true.
 // --dump DIR writes every output frame as DIR/<jobId>_<chunkOffset>_<frame>.raw
-// (packed planes) for offline checks.  Decode/encode stay in host libavcodec
-// and are not part of this process; the source here is libdts's synthetic one.
+// (packed planes) for offline checks.  Without a path the source is libdts's
+// synthetic one.  Compressed decode / encode (libavcodec) are not part of this build.
 const path = require("path");
 const fs = require("fs");
 
@@ -29,6 +33,8 @@ async function main(argv) {
     const cfg = JSON.parse(fs.readFileSync(argv[0], "utf8"));
     const di = argv.indexOf("--dump");
     const dump = di >= 0 ? argv[di + 1] : null;
+    const oi = argv.indexOf("--out");
+    const outDir = oi >= 0 ? argv[oi + 1] : cfg.outDir || null;
     threadPool(cfg.gpus ? cfg.gpus.length : 8);
     const addon = loadAddon();
     const { GpuSegmentScheduler } = require("./scheduler");
@@ -42,9 +48,9 @@ async function main(argv) {
         });
     } : null;
     const sched = new GpuSegmentScheduler({ addon: addon, gpus: cfg.gpus, workerId: cfg.workerId,
-                                            segmentFrames: cfg.segmentFrames, sink: sink });
+                                            segmentFrames: cfg.segmentFrames, sink: sink, outDir: outDir });
     const summary = await sched.runJobs(cfg.jobs, cfg.chunks, cfg.sources);
-    process.stdout.write(JSON.stringify({ chunks: cfg.chunks, summary: summary }) + "\n");
+    process.stdout.write(JSON.stringify({ chunks: cfg.chunks, jobs: cfg.jobs, summary: summary }) + "\n");
 }
 
 if (require.main === module) {

@@ -91,7 +91,7 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_ctx_last_hip_error", "dts_graph_create", "dts_graph_destroy", "dts_graph_info_get",
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
-           "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device"]
+           "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device", "dts_quality_run_host"]
 
 _lib = None
 
@@ -126,6 +126,8 @@ def lib():
     L.dts_quality_run_device.argtypes = [vp, i32, i32, i32, ctypes.POINTER(DevFrames),
                                          ctypes.POINTER(DevFrames), i32, vp, vp]
     L.dts_qstat_finalize.argtypes = [i32, i32, ctypes.POINTER(QRaw), i32, ctypes.POINTER(QStat)]
+    L.dts_quality_run_host.argtypes = [vp, i32, i32, i32, ctypes.POINTER(Frame), ctypes.POINTER(Frame), i32,
+                                       ctypes.POINTER(QStat)]
     L.dts_synth_host.argtypes = [i32, i32, i32, i32, u32, i64, ctypes.POINTER(Frame)]
     L.dts_synth_device.argtypes = [vp, i32, i32, i32, i32, u32, i64, ctypes.POINTER(DevFrames), i32, vp]
     L.dts_frame_layout.argtypes = [i32, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)]
@@ -278,6 +280,15 @@ class Context:
         check(lib().dts_quality_run_device(self.h, w, h, fmt, ctypes.byref(a), ctypes.byref(b), nframes,
                                            ctypes.c_void_p(qraw_ptr), ctypes.c_void_p(stream or 0)),
               "quality_run_device")
+
+    def quality_host(self, w, h, fmt, a_frames, b_frames):
+        """vf_psnr + vf_ssim of host frames a[i] vs b[i] (plane lists) -> [qstat dict]."""
+        n = len(a_frames)
+        a = (Frame * n)(*[frame_struct(f) for f in a_frames])
+        b = (Frame * n)(*[frame_struct(f) for f in b_frames])
+        q = (QStat * n)()
+        check(lib().dts_quality_run_host(self.h, w, h, fmt, a, b, n, q), "quality_run_host")
+        return [q[i].as_dict() for i in range(n)]
 
     def yadif_device(self, w, h, mode, tff, seq, nseq, first, count, dst, stream=None):
         check(lib().dts_yadif_run_device(self.h, w, h, mode, tff, ctypes.byref(seq), nseq, first, count,

@@ -206,6 +206,11 @@ int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes,
 int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt,
                            const dts_dev_frames *a, const dts_dev_frames *b,
                            int nframes, dts_qraw *qraw_dev, void *stream);
+/* The same on host frames (a[i] vs b[i], i < nframes): uploads, runs and returns
+ * the finished per-frame statistics in out[nframes].  Synchronous.  Used by the
+ * Node worker for each rendition against its reference rendition. */
+int dts_quality_run_host(dts_ctx *ctx, int w, int h, int fmt, const dts_frame *a, const dts_frame *b,
+                         int nframes, dts_qstat *out);
 /* vf_yadif (FFmpeg 4.4, 8-bit yuv420p) on a device-resident sequence of nseq
  * frames: outputs are made for frames first .. first+count-1, each with
  * prev = frame i-1 and next = frame i+1 clamped to the sequence (yadif's

@@ -5,8 +5,12 @@
 const assert = require("assert");
 const path = require("path");
 const NODE = path.join(__dirname, "..", "..", "distributed-transcoding-server_amd", "node");
+const fs = require("fs");
+const os = require("os");
 const { GpuSegmentScheduler } = require(path.join(NODE, "scheduler"));
 const ladder = require(path.join(NODE, "ladder"));
+const y4m = require(path.join(NODE, "y4m"));
+const assemble = require(path.join(NODE, "assemble"));
 
 function fakeAddon(opts) {
     opts = opts || {};
@@ -24,6 +28,14 @@ function fakeAddon(opts) {
             let i = 0;
             for (let k = 0; k < nout; k++) { while (i + 1 < n && near(i + 1) <= k) i++; out.push(i); }
             return out;
+        },
+        // stand-in vf_psnr: identical frames -> sse 0, otherwise 1 per byte of the first plane differing
+        quality: function (ctx, w, h, fmt, a, b) {
+            stats.quality = (stats.quality || 0) + 1;
+            return Promise.resolve(a.map(function (fa, i) {
+                const d = fa.data[0][0] === b[i].data[0][0] ? 0 : 1;
+                return { sse: { y: d, u: 0, v: 0 }, psnr: {}, ssim: { y: 1 - d / 2, u: 1, v: 1 }, ssimAll: 1 - d / 4 };
+            }));
         },
         run: function (g, src, dst, q) {
             stats.runs++;
@@ -157,6 +169,120 @@ async function testThrowingUpdateDoesNotHang() {
     js.chunks.forEach(function (c) { assert.strictEqual(c.status, "done"); });
 }
 
+function tmpdir() {
+    return fs.mkdtempSync(path.join(os.tmpdir(), "dts-node-"));
+}
+
+function testY4MRoundTrip() {
+    const d = tmpdir(), p = path.join(d, "a.y4m");
+    const w = 37, h = 23, cw = 19, ch = 12;
+    y4m.writeFile(p, w, h, [30000, 1001], 5, function (i) {
+        const f = { data: [Buffer.alloc(w * h, i), Buffer.alloc(cw * ch, 100 + i), Buffer.alloc(cw * ch, 200 + i)],
+                    pitch: [w, cw, cw] };
+        f.data[0][3] = 7;
+        return f;
+    });
+    const r = new y4m.Y4MReader(p);
+    assert.deepStrictEqual([r.hdr.w, r.hdr.h, r.frames], [w, h, 5]);
+    assert.deepStrictEqual(r.hdr.fps, [30000, 1001]);
+    const f3 = r.read(3);
+    assert.strictEqual(f3.data[0][0], 3);
+    assert.strictEqual(f3.data[0][3], 7);
+    assert.strictEqual(f3.data[1][cw * ch - 1], 103);
+    assert.strictEqual(f3.data[2][0], 203);
+    assert.throws(function () { r.read(5); }, /out of range/);
+    r.close();
+    // nv12 rendition -> planar Y4M record (de-interleaved chroma)
+    const nv = { data: [Buffer.alloc(w * h, 1), Buffer.alloc(ch * 2 * cw), null], pitch: [w, 2 * cw, 0] };
+    for (let i = 0; i < cw * ch; ++i) { nv.data[1][2 * i] = 10; nv.data[1][2 * i + 1] = 20; }
+    const rec = y4m.frameRecord(nv, w, h, 1);
+    assert.strictEqual(rec.length, 6 + y4m.frameBytes(w, h));
+    assert.strictEqual(rec[6 + w * h], 10);
+    assert.strictEqual(rec[6 + w * h + cw * ch], 20);
+    assert.throws(function () { y4m.parseHeader(Buffer.from("YUV4MPEG2 W4 H4 C444\n")); }, /4:2:0/);
+}
+
+function testAssembleBlocks() {
+    const d = tmpdir();
+    const sizes = [700000, 1048576, 5, 1500000];
+    const files = sizes.map(function (n, i) {
+        const p = path.join(d, "s" + i);
+        const b = Buffer.alloc(n);
+        for (let k = 0; k < n; ++k) b[k] = (k * 7 + i) & 255;
+        fs.writeFileSync(p, b);
+        return p;
+    });
+    const a = assemble.assembleFiles(files, path.join(d, "blocks"));
+    const total = sizes.reduce(function (x, y) { return x + y; }, 0);
+    assert.strictEqual(a.size, total);
+    assert.strictEqual(a.chunk.length, Math.ceil(total / 1048576));
+    const whole = Buffer.concat(files.map(function (f) { return fs.readFileSync(f); }));
+    // index.js block arithmetic: any byte range reads back from the blocks
+    [[0, 10], [1048570, 1048600], [total - 3, total + 100], [700000, 1748576]].forEach(function (rg) {
+        const got = assemble.readRange(a, path.join(d, "blocks"), rg[0], rg[1]);
+        assert.ok(got.equals(whole.slice(rg[0], Math.min(rg[1], total - 1) + 1)), "range " + rg);
+    });
+}
+
+function testQualitySummary() {
+    // two frames, luma MSE 1 and 3 -> mean 2; chroma exact -> inf; area-weighted average
+    const w = 4, h = 4;
+    const st = [1, 3].map(function (m) {
+        return { sse: { y: m * 16, u: 0, v: 0 }, ssim: { y: 0.5, u: 1, v: 1 }, ssimAll: 0.75 };
+    });
+    const r = ladder.summarizeQuality(st, w, h);
+    assert.ok(Math.abs(r.psnr.y - 10 * Math.log10(255 * 255 / 2)) < 1e-9);
+    assert.strictEqual(r.psnr.u, Infinity);
+    assert.ok(Math.abs(r.psnr.avg - 10 * Math.log10(255 * 255 / (2 * 16 / 24))) < 1e-9);
+    assert.strictEqual(r.ssim.all, 0.75);
+    assert.deepStrictEqual(ladder.qualityOf({ id: 1, codecSettings: '{"quality": "ssim"}' }), { mode: 2, ref: 0x200 });
+    assert.strictEqual(ladder.qualityOf({ id: 1, codecSettings: "-crf 20" }), null);
+}
+
+async function testY4MJobAssembled() {
+    // a Y4M source, renditions written per segment, quality on one row, every job assembled
+    const d = tmpdir(), src = path.join(d, "src.y4m");
+    const W = 64, H = 36;
+    y4m.writeFile(src, W, H, [60, 1], 14, function (i) {
+        return { data: [Buffer.alloc(W * H, i), Buffer.alloc(32 * 18, 128), Buffer.alloc(32 * 18, 128)], pitch: [W, 32, 32] };
+    });
+    const addon = fakeAddon({ devices: 2 });
+    const jobs = [{ id: 21, sourceID: 3, width: 32, height: 18, framerate: 60, codecSettings: '{"quality": "both"}' },
+                  { id: 22, sourceID: 3, width: 16, height: 10, framerate: 60, codecSettings: null }];
+    const chunks = [];
+    let id = 1;
+    jobs.forEach(function (j) { for (let o = 0; o < 3; o++) chunks.push({ id: id++, mainJob: j.id, chunkOffset: o, status: null }); });
+    const updates = [];
+    const s = new GpuSegmentScheduler({ addon: addon, segmentFrames: 6, outDir: d,
+                                        onJobUpdate: function (j, f) { updates.push([j.id, f.finished]); } });
+    await s.runJobs(jobs, chunks, { 3: { path: src } });
+    chunks.forEach(function (c) {
+        assert.strictEqual(c.status, "done");
+        const r = JSON.parse(c.result);
+        assert.strictEqual(r.frames, c.chunkOffset < 2 ? 6 : 2);             // 14 frames: 6 + 6 + 2
+        assert.ok(r.readMs >= 0 && r.gpuMs >= 0 && r.writeMs >= 0);
+        assert.strictEqual(fs.statSync(r.file).size, r.fileBytes);
+        if (c.mainJob === 21) assert.ok(r.quality && r.quality.psnr && r.quality.ssim);
+        else assert.strictEqual(r.quality, undefined);
+        // the rendition file reads back: first luma byte = the source frame index (stand-in ladder)
+        const rd = new y4m.Y4MReader(r.file);
+        assert.strictEqual(rd.frames, r.frames);
+        assert.strictEqual(rd.read(0).data[0][0], 6 * c.chunkOffset);
+        rd.close();
+    });
+    jobs.forEach(function (j) {
+        assert.strictEqual(j.finished, true);
+        const a = JSON.parse(j.assembledData);
+        const files = chunks.filter(function (c) { return c.mainJob === j.id; })
+            .map(function (c) { return JSON.parse(c.result).file; });
+        const total = files.reduce(function (x, f) { return x + fs.statSync(f).size; }, 0);
+        assert.strictEqual(a.size, total);
+        assert.strictEqual(a.chunk.length, Math.ceil(total / 1048576));
+    });
+    assert.deepStrictEqual(updates.sort(), [[21, true], [22, true]]);
+    assert.ok(addon.stats.quality >= 3);
+}
+
 function testNoDevicesIsLoud() {
     assert.throws(function () { new GpuSegmentScheduler({ addon: fakeAddon({ devices: 0 }) }); }, /no CPU fallback/);
 }
@@ -169,5 +295,9 @@ function testNoDevicesIsLoud() {
     await testGiveUpAfterRetries();
     await testFpsMapAndResume();
     await testThrowingUpdateDoesNotHang();
+    testY4MRoundTrip();
+    testAssembleBlocks();
+    testQualitySummary();
+    await testY4MJobAssembled();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });

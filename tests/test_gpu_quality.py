@@ -137,3 +137,21 @@ def test_quality_nv12_vs_oracle(ctx, w, h):
         ctypes.memmove(ctypes.addressof(r), host[i].tobytes(), ctypes.sizeof(r))
         got = D.qstat_finalize(w, h, [r])[0]
         check_q(got, orc.quality_frame(w, h, fr_a[i], fr_b[i]))
+
+
+@pytest.mark.parametrize("fmt", [D.FMT_YUV420P, D.FMT_NV12])
+def test_quality_host_entry_vs_oracle(ctx, fmt):
+    """dts_quality_run_host (the Node worker's per-rendition quality): host frames of
+    either 8-bit 4:2:0 layout against the oracle on the planar planes."""
+    w, h = 130, 74
+    src = [D.synth_host(2 * w, 2 * h, D.FMT_YUV420P, 0, 9, f) for f in range(3)]
+    a = [orc.scale_frame(f, 2 * w, 2 * h, 0, w, h, fmt, D.SCALE_BICUBIC) for f in src]
+    b = [orc.scale_frame(f, 2 * w, 2 * h, 0, w, h, fmt, D.SCALE_LANCZOS) for f in src]
+    got = ctx.quality_host(w, h, fmt, a, b)
+
+    def planar(p):
+        if fmt != D.FMT_NV12:
+            return p
+        return [p[0], np.ascontiguousarray(p[1][:, 0::2]), np.ascontiguousarray(p[1][:, 1::2])]
+    for i in range(3):
+        check_q(got[i], orc.quality_frame(w, h, planar(a[i]), planar(b[i])))

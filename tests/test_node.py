@@ -112,3 +112,94 @@ a.run(g, [fr(64, 36, 0, 0)], [fr(32, 18, 1, 0)]).then(function () {
     r = subprocess.run([NODE, "-e", script], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout.strip().split("\n")[-1]) == {"thrown": 5, "ok": True}
+
+
+def _write_y4m(path, frames, w, h, fps=(60, 1)):
+    with open(path, "wb") as f:
+        f.write(f"YUV4MPEG2 W{w} H{h} F{fps[0]}:{fps[1]} Ip A1:1 C420jpeg\n".encode())
+        for planes in frames:
+            f.write(b"FRAME\n")
+            for p in planes:
+                f.write(np.ascontiguousarray(p).tobytes())
+
+
+def _read_y4m(path):
+    data = open(path, "rb").read()
+    nl = data.index(b"\n")
+    tok = data[:nl].decode().split()
+    w = int(next(t[1:] for t in tok if t[0] == "W"))
+    h = int(next(t[1:] for t in tok if t[0] == "H"))
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    fb = w * h + 2 * cw * ch
+    out, o = [], nl + 1
+    while o < len(data):
+        assert data[o:o + 6] == b"FRAME\n"
+        raw = np.frombuffer(data[o + 6:o + 6 + fb], np.uint8)
+        out.append([raw[:w * h].reshape(h, w), raw[w * h:w * h + cw * ch].reshape(ch, cw),
+                    raw[w * h + cw * ch:].reshape(ch, cw)])
+        o += 6 + fb
+    return w, h, out
+
+
+def _planar(planes, fmt):
+    if fmt != D.FMT_NV12:
+        return planes
+    return [planes[0], np.ascontiguousarray(planes[1][:, 0::2]), np.ascontiguousarray(planes[1][:, 1::2])]
+
+
+@pytest.mark.gpu
+def test_worker_gpu_y4m_quality_assembled(tmp_path):
+    """A Y4M source through worker.js --out: rendition segments written as Y4M (bit-exact
+    vs the oracle), per-segment PSNR/SSIM of the row that asks for it (vs the lanczos
+    reference rendition, from the oracle's per-frame records), and Jobs.assembledData =
+    the job's segments in 1 MiB blocks whose bytes read back as the segment files."""
+    sw, sh, n, seg = 384, 216, 7, 3
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 11, i) for i in range(n)]
+    src = tmp_path / "src.y4m"
+    _write_y4m(src, frames, sw, sh)
+    jobs = [{"id": 31, "sourceID": 2, "width": 192, "height": 108, "framerate": 60,
+             "codecSettings": json.dumps({"quality": "both"})},
+            {"id": 32, "sourceID": 2, "width": 128, "height": 72, "framerate": 60,
+             "codecSettings": json.dumps({"scale": "lanczos", "format": "yuv420p"})}]
+    chunks = [{"id": k * 3 + off + 1, "mainJob": j["id"], "chunkOffset": off, "status": None}
+              for k, j in enumerate(jobs) for off in range(3)]
+    cfg = {"workerId": 4, "segmentFrames": seg, "gpus": [0], "sources": {"2": {"path": str(src)}},
+           "jobs": jobs, "chunks": chunks}
+    (tmp_path / "job.json").write_text(json.dumps(cfg))
+    out = tmp_path / "out"
+    r = subprocess.run([NODE, os.path.join(ROOT, "distributed-transcoding-server_amd", "node", "worker.js"),
+                        str(tmp_path / "job.json"), "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    spec = {31: (192, 108, D.FMT_NV12, D.SCALE_BICUBIC), 32: (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS)}
+    for c in res["chunks"]:
+        assert c["status"] == "done"
+        rec = json.loads(c["result"])
+        w, h, fmt, m = spec[c["mainJob"]]
+        idx = list(range(c["chunkOffset"] * seg, min(n, (c["chunkOffset"] + 1) * seg)))
+        assert rec["frames"] == len(idx) and os.path.getsize(rec["file"]) == rec["fileBytes"]
+        gw, gh, got = _read_y4m(rec["file"])
+        assert (gw, gh, len(got)) == (w, h, len(idx))
+        recs = []
+        for i, g in zip(idx, got):
+            want = orc.scale_frame(frames[i], sw, sh, D.FMT_YUV420P, w, h, fmt, m)
+            assert all(np.array_equal(a, b) for a, b in zip(g, _planar(want, fmt))), (c["mainJob"], i)
+            if c["mainJob"] == 31:
+                ref = orc.scale_frame(frames[i], sw, sh, D.FMT_YUV420P, w, h, fmt, D.SCALE_LANCZOS)
+                recs.append(orc.quality_frame(w, h, _planar(want, fmt), _planar(ref, fmt)))
+        if c["mainJob"] == 31:
+            q = rec["quality"]
+            mse_y = sum(x["mse"][0] for x in recs) / len(recs)
+            assert q["psnr"]["y"] == pytest.approx(10 * np.log10(255 * 255 / mse_y), rel=1e-9)
+            assert q["ssim"]["all"] == pytest.approx(sum(x["ssim_all"] for x in recs) / len(recs), abs=1e-4)
+        else:
+            assert "quality" not in rec
+    for j in res["jobs"]:
+        assert j["finished"] is True
+        a = json.loads(j["assembledData"])
+        files = [json.loads(c["result"])["file"] for c in sorted(res["chunks"], key=lambda c: c["chunkOffset"])
+                 if c["mainJob"] == j["id"]]
+        whole = b"".join(open(f, "rb").read() for f in files)
+        assert a["size"] == len(whole) and len(a["chunk"]) == -(-len(whole) // 1048576)
+        blocks = b"".join((out / "blocks" / cid).read_bytes() for cid in a["chunk"])
+        assert blocks == whole
