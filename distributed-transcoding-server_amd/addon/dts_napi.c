@@ -167,6 +167,19 @@ static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
     if (get_i32(env, o, "quality", 0, &s->quality) || get_i32(env, o, "qualityOut", 0, &s->quality_out) ||
         get_i32(env, o, "maxBatch", 0, &s->max_batch))
         return -1;
+    /* deint: {mode, tff} -> yadif ahead of the ladder (sources carry a context frame each side) */
+    bool has_di = false;
+    napi_has_named_property(env, o, "deint", &has_di);
+    if (has_di) {
+        napi_value di;
+        napi_valuetype t;
+        if (napi_get_named_property(env, o, "deint", &di) != napi_ok) return -1;
+        napi_typeof(env, di, &t);
+        if (t == napi_object) {
+            s->deint = 1;
+            if (get_i32(env, di, "mode", 0, &s->deint_mode) || get_i32(env, di, "tff", 1, &s->deint_tff)) return -1;
+        }
+    }
     /* tonemap: {mode, param, desat, peak, npl} -> HDR10 -> SDR (vf_tonemap / zscale) */
     bool has_tm = false;
     napi_has_named_property(env, o, "tonemap", &has_tm);
@@ -418,20 +431,22 @@ static napi_value js_run(napi_env env, napi_callback_info info)
         free_job(j);
         return throw_dts(env, DTS_E_INVAL, "run: frames (a plane is missing, or its Buffer / pitch is too small)");
     }
-    if ((uint64_t)nd != (uint64_t)ns * (uint64_t)s->nout) {
+    const uint32_t cf = s->deint ? 2u : 0u;       /* deint: one context frame each side of the segment */
+    if (ns < cf || (uint64_t)nd != (uint64_t)(ns - cf) * (uint64_t)s->nout) {
         free_job(j);
-        return throw_dts(env, DTS_E_INVAL, "run: dst must hold src.length * outputs frames (frame-major)");
+        return throw_dts(env, DTS_E_INVAL, "run: dst must hold (src.length - context) * outputs frames (frame-major)");
     }
-    j->n = (int)ns;
+    j->n = (int)(ns - cf);
     napi_valuetype qt = napi_undefined;
     if (argc >= 4) napi_typeof(env, argv[3], &qt);
     if (qt == napi_object) {
         const int qo = s->quality_out;
-        if (!s->quality || parse_frames(env, argv[3], &j->qref, &nq, &ow[qo], &oh[qo], &of[qo], 1) || nq != ns) {
+        if (!s->quality || parse_frames(env, argv[3], &j->qref, &nq, &ow[qo], &oh[qo], &of[qo], 1) ||
+            nq != (uint32_t)j->n) {
             free_job(j);
             return throw_dts(env, DTS_E_INVAL, "run: qref frames");
         }
-        j->q = (dts_qstat *)calloc(ns ? ns : 1, sizeof(dts_qstat));
+        j->q = (dts_qstat *)calloc(j->n ? (size_t)j->n : 1, sizeof(dts_qstat));
         if (!j->q) {
             free_job(j);
             return throw_dts(env, DTS_E_NOMEM, "run");

@@ -33,6 +33,10 @@ struct QScratch {
     void *p = nullptr;
     size_t bytes = 0;
     hipEvent_t ev = nullptr;
+    // the deinterlaced source frames of a graph with deint on (one batch), ordered the same way
+    void *dp = nullptr;
+    size_t dbytes = 0;
+    hipEvent_t dev = nullptr;
 };
 
 struct dts_ctx {
@@ -424,6 +428,10 @@ int validate_spec(const dts_graph_spec &s)
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
     if (s.quality && !fmt_8bit(s.out[s.quality_out].fmt)) return DTS_E_UNSUPPORTED;   // vf_psnr/vf_ssim: 8-bit
+    if (s.deint) {                                        // yadif ahead of the ladder: 8-bit yuv420p, frame modes
+        if (s.deint != 1 || s.src_fmt != DTS_FMT_YUV420P || s.hdr_to_sdr) return DTS_E_UNSUPPORTED;
+        if ((s.deint_mode != 0 && s.deint_mode != 2) || s.src_w < 16) return DTS_E_UNSUPPORTED;
+    }
     if (s.hdr_to_sdr) {
         if (s.src_fmt != DTS_FMT_P010LE) return DTS_E_INVAL;                        // HDR10 sources are p010
         if (s.tonemap.mode < DTS_TM_NONE || s.tonemap.mode > DTS_TM_MOBIUS) return DTS_E_INVAL;
@@ -611,7 +619,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.3 (gfx950; abi 3)"; }
+const char *dts_version(void) { return "dts-mi355x 0.4 (gfx950; abi 4)"; }
 
 const char *dts_strerror(int err)
 {
@@ -662,7 +670,12 @@ static void qscratch_free(QScratch &q)
         hipEventSynchronize(q.ev);
         hipEventDestroy(q.ev);
     }
+    if (q.dev) {
+        hipEventSynchronize(q.dev);
+        hipEventDestroy(q.dev);
+    }
     if (q.p) hipFree(q.p);
+    if (q.dp) hipFree(q.dp);
     q = QScratch{};
 }
 
@@ -1030,6 +1043,58 @@ static int ensure_qscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
     return DTS_OK;
 }
 
+// one of our batch buffers as caller-style device frames
+static dts_dev_frames dev_frames(uint8_t *base, const DevLayout &lay)
+{
+    dts_dev_frames d{};
+    for (int p = 0; p < 3; ++p) {
+        d.data[p] = lay.rowb[p] ? base + lay.off[p] : nullptr;
+        d.pitch[p] = lay.pitch[p];
+    }
+    d.frame_stride = lay.fstride;
+    return d;
+}
+
+// the deinterlace buffer of a QScratch (same reuse rule as the quality partials)
+static int ensure_dscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
+{
+    if (!q.dev) HIPCHK(ctx, hipEventCreateWithFlags(&q.dev, hipEventDisableTiming));
+    if (q.dbytes >= bytes) return DTS_OK;
+    if (q.dp) {
+        HIPCHK(ctx, hipEventSynchronize(q.dev));
+        hipFree(q.dp);
+        q.dp = nullptr;
+        q.dbytes = 0;
+    }
+    HIPCHK(ctx, hipMalloc(&q.dp, bytes));
+    q.dbytes = bytes;
+    return DTS_OK;
+}
+
+// k_yadif over outputs first .. first+count-1 of a device sequence (vf_yadif.c filter_slice)
+static int yadif_enqueue(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames &seq, int nseq, int first,
+                         int count, const dts_dev_frames &dst, hipStream_t st)
+{
+    const int fields = (mode & 1) ? 2 : 1;
+    YadifParams p{};
+    p.seq = to_dev(seq, DTS_FMT_YUV420P);
+    p.w = w;
+    p.h = h;
+    p.nseq = nseq;
+    p.mode = mode;
+    p.tff = tff ? 1 : 0;
+    p.aligned = planes_ok(seq, w, h, DTS_FMT_YUV420P, 4) && planes_ok(dst, w, h, DTS_FMT_YUV420P, 4);
+    const int chunk = 32768;                              // outputs per launch (grid z)
+    for (int j0 = 0; j0 < count; j0 += chunk) {
+        const int n = std::min(chunk, count - j0);
+        p.first = first + j0;
+        p.dst = to_dev(dst, DTS_FMT_YUV420P);
+        for (int pl = 0; pl < 3; ++pl) p.dst.data[pl] += (uint64_t)((int64_t)j0 * fields * dst.frame_stride);
+        HIPCHK(ctx, launch_yadif(p, n * fields, st));
+    }
+    return DTS_OK;
+}
+
 static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, const dts_dev_frames &a,
                            const dts_dev_frames &b, int n, dts_qraw *qraw, hipStream_t st)
 {
@@ -1199,13 +1264,46 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
     hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
 
-    const DevPlanes dsrc = to_dev(*src, s.src_fmt);
     DevPlanes ddst[DTS_MAX_OUTPUTS];
     int dfmt[DTS_MAX_OUTPUTS];
     for (int k = 0; k < s.nout; ++k) {
         ddst[k] = to_dev(dst[k], s.out[k].fmt);
         dfmt[k] = s.out[k].fmt;
     }
+    if (s.deint) {
+        // yadif into a batch of deinterlaced frames, then the ladder (and quality) from it;
+        // src holds nframes + 2 frames (one context frame each side)
+        const int B = g->batch;
+        int e = ensure_dscratch(ctx, qs, (size_t)B * g->lay_src.fstride);
+        if (e) return e;
+        const dts_dev_frames dbuf = dev_frames(static_cast<uint8_t *>(qs.dp), g->lay_src);
+        for (int c0 = 0; c0 < nframes; c0 += B) {
+            const int m = std::min(B, nframes - c0);
+            HIPCHK(ctx, hipStreamWaitEvent(st, qs.dev, 0));   // the buffer's previous user
+            e = yadif_enqueue(ctx, s.src_w, s.src_h, s.deint_mode, s.deint_tff, *src, nframes + 2, 1 + c0, m, dbuf, st);
+            if (e) return e;
+            DevPlanes dd[DTS_MAX_OUTPUTS];
+            for (int k = 0; k < s.nout; ++k) {
+                dd[k] = ddst[k];
+                for (int pl = 0; pl < 3; ++pl) dd[k].data[pl] += (uint64_t)((int64_t)c0 * dst[k].frame_stride);
+            }
+            e = enqueue_ladder(g, to_dev(dbuf, s.src_fmt), dd, dfmt, m, st);
+            if (e) return e;
+            if (want_q) {
+                const dts_output_spec &o = s.out[s.quality_out];
+                dts_dev_frames qa = dst[s.quality_out], qb = *qref;
+                for (int pl = 0; pl < 3; ++pl) {
+                    if (qa.data[pl]) qa.data[pl] = static_cast<uint8_t *>(qa.data[pl]) + (int64_t)c0 * qa.frame_stride;
+                    if (qb.data[pl]) qb.data[pl] = static_cast<uint8_t *>(qb.data[pl]) + (int64_t)c0 * qb.frame_stride;
+                }
+                e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, qa, qb, m, qraw_dev + c0, st);
+                if (e) return e;
+            }
+            HIPCHK(ctx, hipEventRecord(qs.dev, st));
+        }
+        return DTS_OK;
+    }
+    const DevPlanes dsrc = to_dev(*src, s.src_fmt);
     const int e = g->hdr ? enqueue_hdr(g, dsrc, ddst, nframes, st) : enqueue_ladder(g, dsrc, ddst, dfmt, nframes, st);
     if (e) return e;
     if (want_q) {
@@ -1301,24 +1399,7 @@ int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dt
     if (count == 0) return DTS_OK;
     hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
-    const int fields = (mode & 1) ? 2 : 1;
-    YadifParams p{};
-    p.seq = to_dev(*seq, DTS_FMT_YUV420P);
-    p.w = w;
-    p.h = h;
-    p.nseq = nseq;
-    p.mode = mode;
-    p.tff = tff ? 1 : 0;
-    p.aligned = planes_ok(*seq, w, h, DTS_FMT_YUV420P, 4) && planes_ok(*dst, w, h, DTS_FMT_YUV420P, 4);
-    const int chunk = 32768;                              // outputs per launch (grid z)
-    for (int j0 = 0; j0 < count; j0 += chunk) {
-        const int n = std::min(chunk, count - j0);
-        p.first = first + j0;
-        p.dst = to_dev(*dst, DTS_FMT_YUV420P);
-        for (int pl = 0; pl < 3; ++pl) p.dst.data[pl] += (uint64_t)((int64_t)j0 * fields * dst->frame_stride);
-        HIPCHK(ctx, launch_yadif(p, n * fields, st));
-    }
-    return DTS_OK;
+    return yadif_enqueue(ctx, w, h, mode, tff, *seq, nseq, first, count, *dst, st);
 }
 
 int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out)
@@ -1395,12 +1476,13 @@ static int alloc_host_path(dts_graph *g)
     dts_ctx *ctx = g->ctx;
     const dts_graph_spec &s = g->spec;
     const int B = g->batch;
-    g->pin_in_bytes = (int64_t)B * g->info.src_frame_bytes;
+    const int cf = s.deint ? 2 : 0;                      // deint: one context frame each side
+    g->pin_in_bytes = (int64_t)(B + cf) * g->info.src_frame_bytes;
     if (s.quality) g->pin_in_bytes += (int64_t)B * g->info.out_frame_bytes[s.quality_out];
     g->pin_out_bytes = 0;
     for (int k = 0; k < s.nout; ++k) g->pin_out_bytes += (int64_t)B * g->info.out_frame_bytes[k];
     for (int sl = 0; sl < 2; ++sl) {
-        HIPCHK(ctx, hipMalloc(&g->dev_src[sl], (size_t)B * g->lay_src.fstride));
+        HIPCHK(ctx, hipMalloc(&g->dev_src[sl], (size_t)(B + cf) * g->lay_src.fstride));
         for (int k = 0; k < s.nout; ++k) HIPCHK(ctx, hipMalloc(&g->dev_out[sl][k], (size_t)B * g->lay_out[k].fstride));
         if (s.quality) {
             HIPCHK(ctx, hipMalloc(&g->dev_q[sl], (size_t)B * g->lay_q.fstride));
@@ -1454,16 +1536,6 @@ static hipError_t copy_frames(uint8_t *dev, const DevLayout &lay, uint8_t *host,
     return hipSuccess;
 }
 
-static dts_dev_frames dev_frames(uint8_t *base, const DevLayout &lay)
-{
-    dts_dev_frames d{};
-    for (int p = 0; p < 3; ++p) {
-        d.data[p] = lay.rowb[p] ? base + lay.off[p] : nullptr;
-        d.pitch[p] = lay.pitch[p];
-    }
-    d.frame_stride = lay.fstride;
-    return d;
-}
 
 static int finish_slot(dts_graph *g, int sl)
 {
@@ -1511,11 +1583,12 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             if (e) return e;
             hipStream_t st = ctx->stream[sl];
             uint8_t *hp = g->pin_in[sl];
-            for (int f = 0; f < n; ++f) {
+            const int cf = s.deint ? 2 : 0;              // deint: src[f0 .. f0 + n + 1] (context frames)
+            for (int f = 0; f < n + cf; ++f) {
                 pack_frame(hp + (int64_t)f * g->info.src_frame_bytes, src[f0 + f], s.src_w, s.src_h, s.src_fmt);
             }
-            HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n, true, st));
-            uint8_t *qhp = hp + (int64_t)B * g->info.src_frame_bytes;
+            HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n + cf, true, st));
+            uint8_t *qhp = hp + (int64_t)(B + cf) * g->info.src_frame_bytes;
             if (s.quality) {
                 const dts_output_spec &o = s.out[s.quality_out];
                 for (int f = 0; f < n; ++f)

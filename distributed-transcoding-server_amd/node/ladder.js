@@ -22,7 +22,10 @@ const MAX_OUTPUTS = 4;
 // worker reads an optional JSON object from it with the filtergraph knobs a CPU
 // worker would put on its ffmpeg command line:
 //   {"scale": "bicubic", "format": "nv12", "param": [b, c], "tonemap": {"mode": "hable", ...},
-//    "quality": "psnr" | "ssim" | "both", "qualityRef": "lanczos"}
+//    "quality": "psnr" | "ssim" | "both", "qualityRef": "lanczos",
+//    "deinterlace": "yadif" | {"mode": 0 | 2, "parity": "tff" | "bff"}}
+// deinterlace: `yadif=MODE:PARITY` ahead of the scale (frame-rate modes; vf_yadif.c),
+// run on the GPU in the same graph (dts_graph_spec.deint).
 // quality: `[rendition][reference]psnr` / `ssim` per segment against a reference
 // rendition of the same size -- the source scaled with `qualityRef` (default
 // lanczos) -- reported in JobChunks.result.quality.
@@ -48,6 +51,20 @@ function outputOf(job) {
 }
 
 const QUALITY = { psnr: 1, ssim: 2, both: 3, true: 3 };
+
+// {mode, tff} or null
+function deintOf(job) {
+    const s = parseSettings(job.codecSettings);
+    if (!s.deinterlace) return null;
+    const d = typeof s.deinterlace === "object" ? s.deinterlace : {};
+    if (typeof s.deinterlace === "string" && s.deinterlace.toLowerCase() !== "yadif")
+        throw new Error("job " + job.id + ": unknown deinterlacer " + s.deinterlace);
+    const mode = d.mode === undefined ? 0 : d.mode | 0;
+    if (mode !== 0 && mode !== 2) throw new Error("job " + job.id + ": yadif mode " + mode + " (frame-rate modes 0 / 2 only)");
+    const parity = String(d.parity || "tff").toLowerCase();
+    if (parity !== "tff" && parity !== "bff") throw new Error("job " + job.id + ": yadif parity " + d.parity);
+    return { mode: mode, tff: parity === "tff" ? 1 : 0 };
+}
 
 // {mode: DTS_Q_*, ref: DTS_SCALE_*} or null
 function qualityOf(job) {
@@ -97,12 +114,18 @@ function planLadders(jobs, sources) {
             const spec = { src: { w: src.w, h: src.h, fmt: src.fmt }, outputs: part.map(outputOf), quality: 0,
                            maxBatch: 32 };
             if (tm) spec.tonemap = tm;
+            const di = deintOf(part[0]);
+            part.forEach(function (r) {
+                if (JSON.stringify(deintOf(r)) !== JSON.stringify(di))
+                    throw new Error("jobs " + part[0].id + "/" + r.id + ": one graph needs one deinterlace setting");
+            });
+            if (di) spec.deint = di;
             // per-rendition quality (codecSettings.quality): run by the scheduler after the
             // ladder, each requesting row against its reference rendition
             const q = part.map(qualityOf);
             const quality = q.some(function (x) { return x; }) ? {
                 rows: q.map(function (x) { return x ? x.mode : 0; }),
-                refSpec: { src: spec.src, quality: 0, maxBatch: spec.maxBatch,
+                refSpec: { src: spec.src, quality: 0, maxBatch: spec.maxBatch, deint: spec.deint,
                            outputs: spec.outputs.map(function (o, k) {
                                return { w: o.w, h: o.h, fmt: o.fmt, method: q[k] ? q[k].ref : o.method };
                            }) }
@@ -155,5 +178,6 @@ function summarizeQuality(stats, w, h) {
 }
 
 module.exports = { FMT: FMT, METHOD: METHOD, TONEMAP: TONEMAP, MAX_OUTPUTS: MAX_OUTPUTS, parseSettings: parseSettings,
-                   outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, planLadders: planLadders,
+                   outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, deintOf: deintOf,
+                   planLadders: planLadders,
                    rateOf: rateOf, fpsFrames: fpsFrames, summarizeQuality: summarizeQuality };

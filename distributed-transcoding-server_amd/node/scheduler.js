@@ -147,23 +147,43 @@ class GpuSegmentScheduler extends EventEmitter {
         return { dst: dst, per: per };
     }
 
+    // source frames a stream holds (Y4M file), Infinity for the synthetic source
+    _sourceFrames(plan) {
+        const r = this.readers[plan.sourceID];
+        return r ? r.frames : Infinity;
+    }
+
     async _runSegment(slot, task) {
         const self = this;
         const plan = task.plan;
         const t0 = Date.now();
         const g = this._graph(slot, plan);
-        const idx = this._frames(plan, task.chunkOffset, plan.srcFps);
+        let idx = this._frames(plan, task.chunkOffset, plan.srcFps);
+        let sel = null;
+        if (plan.spec.deint) {
+            // yadif needs each frame's neighbours in the source stream: the graph runs on the
+            // segment's contiguous frames plus one context frame each side (clamped: yadif's
+            // clone at the stream ends); the vf_fps selection is applied to its outputs
+            const base = task.chunkOffset * this.segmentFrames, total = this._sourceFrames(plan);
+            const n = Math.max(0, Math.min(this.segmentFrames, total - base));
+            sel = idx.filter(function (i) { return i < base + n; }).map(function (i) { return i - base; });
+            idx = n ? [Math.max(base - 1, 0)].concat(Array.from({ length: n }, function (_, i) { return base + i; }),
+                                                      [Math.min(base + n, total - 1)]) : [];
+        }
         const src = await this.source(plan, idx);
         const t1 = Date.now();
         const outs = plan.spec.outputs;
-        const o = this._allocOutputs(outs, src.length);
-        await this.addon.run(g, src, o.dst, null);
+        const nout = plan.spec.deint ? Math.max(0, src.length - 2) : src.length;
+        const o = this._allocOutputs(outs, nout);
+        if (nout) await this.addon.run(g, src, o.dst, null);
+        if (sel) o.per = o.per.map(function (fr) { return sel.map(function (j) { return fr[j]; }); });
         const t2 = Date.now();
         // per-rendition PSNR / SSIM against the reference rendition of the same source frames
         const quality = outs.map(function () { return null; });
-        if (plan.quality && src.length) {
-            const ref = this._allocOutputs(plan.quality.refSpec.outputs, src.length);
+        if (plan.quality && nout) {
+            const ref = this._allocOutputs(plan.quality.refSpec.outputs, nout);
             await this.addon.run(this._graph(slot, plan, true), src, ref.dst, null);
+            if (sel) ref.per = ref.per.map(function (fr) { return sel.map(function (j) { return fr[j]; }); });
             for (let k = 0; k < outs.length; ++k) {
                 if (!plan.quality.rows[k]) continue;
                 const st = await this.addon.quality(this._ctx(slot), outs[k].w, outs[k].h, outs[k].fmt, o.per[k],

@@ -49,7 +49,9 @@ class GraphSpec(ctypes.Structure):
     _fields_ = [("src_w", ctypes.c_int32), ("src_h", ctypes.c_int32), ("src_fmt", ctypes.c_int32),
                 ("nout", ctypes.c_int32), ("out", OutputSpec * MAX_OUTPUTS),
                 ("quality", ctypes.c_int32), ("quality_out", ctypes.c_int32), ("max_batch", ctypes.c_int32),
-                ("hdr_to_sdr", ctypes.c_int32), ("tonemap", TonemapSpec)]
+                ("hdr_to_sdr", ctypes.c_int32), ("tonemap", TonemapSpec),
+                ("deint", ctypes.c_int32), ("deint_mode", ctypes.c_int32), ("deint_tff", ctypes.c_int32),
+                ("pad2_", ctypes.c_int32)]
 
 
 class Frame(ctypes.Structure):
@@ -229,9 +231,12 @@ def graph_plan(spec):
     return info
 
 
-def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0, tonemap=None):
+def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0, tonemap=None,
+              deint=None):
     """outputs: list of (w, h, fmt, method[, (p0, p1)]).  tonemap: None, or a dict
-    {mode, param, desat, peak, npl} turning on HDR10 -> SDR (dts_tonemap_spec)."""
+    {mode, param, desat, peak, npl} turning on HDR10 -> SDR (dts_tonemap_spec).
+    deint: None, or (mode, tff) for yadif ahead of the ladder (sources then carry one
+    context frame on each side: dts_graph_spec.deint)."""
     s = GraphSpec()
     s.src_w, s.src_h, s.src_fmt = src_w, src_h, src_fmt
     s.nout = len(outputs)
@@ -247,6 +252,8 @@ def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max
         s.tonemap.desat = tonemap.get("desat", 0.0)
         s.tonemap.peak = tonemap.get("peak", 0.0)
         s.tonemap.npl = tonemap.get("npl", 100.0)
+    if deint is not None:
+        s.deint, s.deint_mode, s.deint_tff = 1, deint[0], deint[1]
     return s
 
 
@@ -320,11 +327,13 @@ class Graph:
             pass
 
     def run_host(self, frames, qref=None):
-        """frames: list of source frames (plane lists).  Returns (outputs, qstats):
-        outputs[f][k] is output k of frame f as a plane list."""
+        """frames: list of source frames (plane lists; with deint, n + 2 of them: one
+        context frame each side).  Returns (outputs, qstats): outputs[f][k] is output
+        k of frame f as a plane list."""
         s = self.spec
-        n = len(frames)
-        src = (Frame * n)(*[frame_struct(f) for f in frames])
+        ns = len(frames)
+        n = ns - 2 if s.deint else ns
+        src = (Frame * ns)(*[frame_struct(f) for f in frames])
         outs = [[alloc_frame(s.out[k].w, s.out[k].h, s.out[k].fmt) for k in range(s.nout)] for _ in range(n)]
         dst = (Frame * (n * s.nout))(*[frame_struct(outs[f][k]) for f in range(n) for k in range(s.nout)])
         qr = (Frame * n)(*[frame_struct(q) for q in qref]) if qref is not None else None

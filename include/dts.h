@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DTS_ABI_VERSION 3
+#define DTS_ABI_VERSION 4
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -118,6 +118,17 @@ typedef struct dts_graph_spec {
      * (float path, +-1 LSB vs the double restatement). */
     int32_t hdr_to_sdr;                 /* 0 = off */
     dts_tonemap_spec tonemap;
+    /* Deinterlace ahead of the ladder (`-vf yadif=MODE:PARITY,scale=...`, vf_yadif.c):
+     * 8-bit yuv420p sources, frame-rate modes 0 (send_frame) and 2 (send_frame_nospatial).
+     * With it on, every source batch carries one context frame on each side: src
+     * holds nframes + 2 frames, outputs are made for src[1 .. nframes] (each with
+     * prev = its predecessor, next = its successor in the batch); at the start / end
+     * of a stream the caller repeats the first / last frame (yadif's clone).
+     * Segments therefore overlap their neighbours by one frame each way. */
+    int32_t deint;                      /* 0 = off, 1 = yadif */
+    int32_t deint_mode;                 /* 0 or 2 */
+    int32_t deint_tff;                  /* 1 = top field first, 0 = bottom */
+    int32_t pad2_;
 } dts_graph_spec;
 
 /* host frame: plane p at data[p] with row pitch pitch[p] bytes.
@@ -187,7 +198,8 @@ int dts_graph_info_get(const dts_graph *g, dts_graph_info *info);
 int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info);
 
 /* Host-memory path (the Node worker's path).  dst holds nframes*nout frames,
- * frame-major (dst[f*nout + k]).  qref/q may be NULL when quality is off.
+ * frame-major (dst[f*nout + k]); src holds nframes (+ 2 with deint: see above).
+ * qref/q may be NULL when quality is off.
  * The caller keeps every buffer alive until dts_graph_wait returns. */
 int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes,
                      const dts_frame *dst, const dts_frame *qref, dts_qstat *q);

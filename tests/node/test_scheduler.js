@@ -40,11 +40,13 @@ function fakeAddon(opts) {
         run: function (g, src, dst, q) {
             stats.runs++;
             stats.byDev[g.ctx.dev] = (stats.byDev[g.ctx.dev] || 0) + 1;
-            assert.strictEqual(dst.length, src.length * g.spec.outputs.length);
+            const cf = g.spec.deint ? 1 : 0;             // deint: one context frame each side
+            stats.srcFirst = src.map(function (f) { return f.data[0][0]; });
+            assert.strictEqual(dst.length, (src.length - 2 * cf) * g.spec.outputs.length);
             return new Promise(function (resolve, reject) {
                 setTimeout(function () {
                     if (opts.fail && opts.fail(g.ctx.dev, stats.runs)) return reject(new Error("dts run: HIP error (-1000)"));
-                    dst.forEach(function (f, i) { f.data[0][0] = src[Math.floor(i / g.spec.outputs.length)].data[0][0]; });
+                    dst.forEach(function (f, i) { f.data[0][0] = src[cf + Math.floor(i / g.spec.outputs.length)].data[0][0]; });
                     resolve(null);
                 }, opts.delay === undefined ? 2 : opts.delay);
             });
@@ -283,6 +285,44 @@ async function testY4MJobAssembled() {
     assert.ok(addon.stats.quality >= 3);
 }
 
+async function testDeinterlaceWithRateChange() {
+    // yadif + 60 -> 30 fps over a 14-frame Y4M source in segments of 6: the graph sees the
+    // contiguous segment plus a context frame each side (clamped at the ends), and the
+    // vf_fps pick (every other frame) is applied to its outputs
+    const d = tmpdir(), src = path.join(d, "src.y4m");
+    y4m.writeFile(src, 32, 18, [60, 1], 14, function (i) {
+        return { data: [Buffer.alloc(32 * 18, i), Buffer.alloc(16 * 9, 128), Buffer.alloc(16 * 9, 128)], pitch: [32, 16, 16] };
+    });
+    const addon = fakeAddon({ devices: 1 });
+    const jobs = [{ id: 41, sourceID: 9, width: 16, height: 10, framerate: 30,
+                    codecSettings: '{"deinterlace": {"mode": 2, "parity": "bff"}}' }];
+    const chunks = [0, 1, 2].map(function (o) { return { id: 50 + o, mainJob: 41, chunkOffset: o, status: null }; });
+    const firsts = [];
+    addon.run = (function (run) {
+        return function (g, s, dst, q) {
+            assert.deepStrictEqual(g.spec.deint, { mode: 2, tff: 0 });
+            firsts.push(s.map(function (f) { return f.data[0][0]; }));
+            return run(g, s, dst, q);
+        };
+    })(addon.run);
+    const s = new GpuSegmentScheduler({ addon: addon, segmentFrames: 6, outDir: d });
+    await s.runJobs(jobs, chunks, { 9: { path: src } });
+    firsts.sort(function (a, b) { return a[1] - b[1]; });
+    assert.deepStrictEqual(firsts, [[0, 0, 1, 2, 3, 4, 5, 6], [5, 6, 7, 8, 9, 10, 11, 12], [11, 12, 13, 13]]);
+    chunks.forEach(function (c) {
+        const r = JSON.parse(c.result);
+        const rd = new y4m.Y4MReader(r.file);
+        const got = Array.from({ length: rd.frames }, function (_, i) { return rd.read(i).data[0][0]; });
+        rd.close();
+        const want = { 0: [0, 2, 4], 1: [6, 8, 10], 2: [12] }[c.chunkOffset];
+        assert.deepStrictEqual(got, want, "chunk " + c.chunkOffset);
+    });
+    assert.throws(function () {
+        ladder.planLadders([{ id: 1, sourceID: 1, width: 8, height: 8, codecSettings: '{"deinterlace": {"mode": 1}}' }],
+                           { 1: { w: 16, h: 16, fmt: 0 } });
+    }, /frame-rate modes/);
+}
+
 function testNoDevicesIsLoud() {
     assert.throws(function () { new GpuSegmentScheduler({ addon: fakeAddon({ devices: 0 }) }); }, /no CPU fallback/);
 }
@@ -299,5 +339,6 @@ function testNoDevicesIsLoud() {
     testAssembleBlocks();
     testQualitySummary();
     await testY4MJobAssembled();
+    await testDeinterlaceWithRateChange();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });

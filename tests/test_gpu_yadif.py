@@ -93,3 +93,30 @@ def test_yadif_subrange_and_validation(ctx):
         ctx.yadif_device(w, h, 0, 1, seq, n, 5, 2, _dev(out_t, w, h))
     with pytest.raises(D.DtsError):
         ctx.yadif_device(8, h, 0, 1, seq, n, 0, 1, _dev(out_t, w, h))
+
+
+@pytest.mark.parametrize("mode,tff", [(0, 1), (2, 0)])
+def test_graph_yadif_then_ladder(ctx, mode, tff):
+    """The graph's deinterlace stage (dts_graph_spec.deint): yadif on the device batch,
+    then the ladder, bit-exact against orc.yadif_frame followed by orc.scale_frame.
+    The host path chunks by max_batch = 2, so chunk edges take their neighbours
+    from the one-frame context the caller supplies around the segment."""
+    import dtsffi as Dm
+    sw, sh = 384, 216
+    rng = np.random.default_rng(mode * 7 + tff)
+    seq = [random_frame(sw, sh, Dm.FMT_YUV420P, rng) for _ in range(7)]
+    outs = [(192, 108, Dm.FMT_NV12, Dm.SCALE_BICUBIC), (128, 72, Dm.FMT_YUV420P, Dm.SCALE_LANCZOS)]
+    g = Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_YUV420P, outs, max_batch=2, deint=(mode, tff)))
+    got, _ = g.run_host(seq[1:7])                    # segment = seq[2..5], context seq[1] and seq[6]
+    assert len(got) == 4
+    for j in range(4):
+        i = 2 + j
+        de = orc.yadif_frame(seq[i - 1], seq[i], seq[i + 1], sw, sh, mode, tff, 0)
+        for k, (w, h, fmt, m) in enumerate(outs):
+            want = orc.scale_frame(de, sw, sh, Dm.FMT_YUV420P, w, h, fmt, m)
+            assert all(np.array_equal(a, b) for a, b in zip(got[j][k], want)), (mode, tff, j, k)
+    g.close()
+    with pytest.raises(Dm.DtsError):                   # frame-rate modes only; 8-bit planar sources only
+        Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_YUV420P, outs, deint=(1, 1)))
+    with pytest.raises(Dm.DtsError):
+        Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_NV12, outs, deint=(0, 1)))

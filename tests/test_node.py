@@ -203,3 +203,41 @@ def test_worker_gpu_y4m_quality_assembled(tmp_path):
         assert a["size"] == len(whole) and len(a["chunk"]) == -(-len(whole) // 1048576)
         blocks = b"".join((out / "blocks" / cid).read_bytes() for cid in a["chunk"])
         assert blocks == whole
+
+
+@pytest.mark.gpu
+def test_worker_gpu_yadif_fps(tmp_path):
+    """codecSettings deinterlace + a 60 -> 30 fps rendition through worker.js on the GPU:
+    every written frame equals orc.yadif_frame (neighbours from the source stream, the
+    first / last frame cloned at the ends) followed by orc.scale_frame, for the frames
+    vf_fps (round=near) keeps."""
+    sw, sh, n, seg = 256, 144, 9, 4
+    rng = np.random.default_rng(5)
+    frames = [[rng.integers(0, 256, s, dtype=np.uint8) for s in ((sh, sw), (sh // 2, sw // 2), (sh // 2, sw // 2))]
+              for _ in range(n)]
+    src = tmp_path / "src.y4m"
+    _write_y4m(src, frames, sw, sh)
+    jobs = [{"id": 61, "sourceID": 1, "width": 128, "height": 72, "framerate": 30,
+             "codecSettings": json.dumps({"deinterlace": {"mode": 0, "parity": "tff"}, "format": "yuv420p"})}]
+    chunks = [{"id": 70 + o, "mainJob": 61, "chunkOffset": o, "status": None} for o in range(3)]
+    cfg = {"workerId": 1, "segmentFrames": seg, "gpus": [0], "sources": {"1": {"path": str(src)}},
+           "jobs": jobs, "chunks": chunks}
+    (tmp_path / "job.json").write_text(json.dumps(cfg))
+    r = subprocess.run([NODE, os.path.join(ROOT, "distributed-transcoding-server_amd", "node", "worker.js"),
+                        str(tmp_path / "job.json"), "--out", str(tmp_path / "out")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    for c in res["chunks"]:
+        assert c["status"] == "done", c
+        rec = json.loads(c["result"])
+        base = c["chunkOffset"] * seg
+        nseg = min(seg, n - base)
+        keep = [i for i in D.fps_map(seg, (60, 1), (30, 1)).tolist() if i < nseg]
+        _, _, got = _read_y4m(rec["file"])
+        assert len(got) == len(keep)
+        for g, j in zip(got, keep):
+            i = base + j
+            de = orc.yadif_frame(frames[max(i - 1, 0)], frames[i], frames[min(i + 1, n - 1)], sw, sh, 0, 1, 0)
+            want = orc.scale_frame(de, sw, sh, D.FMT_YUV420P, 128, 72, D.FMT_YUV420P, D.SCALE_BICUBIC)
+            assert all(np.array_equal(a, b) for a, b in zip(g, want)), (c["chunkOffset"], j)
