@@ -7,16 +7,19 @@
 // p010 intermediate).  Float path: the output must match the double-precision
 // restatement (oracle/vf_tonemap_ref.c) within +-1 LSB.
 //
-// One lane = one 2x2 luma block and its chroma sample: two dword luma loads
-// (row pair), one dword U16V16 load, 4 pixel conversions, 2 x u16 luma stores
-// and the chroma mean.  Lanes of a wave take consecutive blocks, so every
-// load and store of the wave is one contiguous run; a workgroup walks 16 block
-// rows of a 64-block column strip.  The two transfer curves (PQ EOTF, 6 pow
-// per pixel, and the BT.709 OETF, 3 pow per pixel) are 1024-interval tables
-// (built in double on the host, 2 x (kTmLutN + 1) floats) staged in LDS once per
-// workgroup and linearly interpolated: measured against the exact curves,
-// 2e-4 of the 8-bit outputs move by one LSB, inside the +-1 LSB
-// tolerance, and the kernel no longer waits on the transcendental unit.
+// Chroma as vf_zscale has zimg resample it by default (bilinear, chroma location
+// "left" = MPEG-2 4:2:0 siting; oracle/vf_tonemap_ref.c states the filter): the
+// 4:2:0 chroma is interpolated up to every pixel before the bt2020 matrix, and the
+// output Cb/Cr are filtered back down 2:1 (taps 1/4 1/2 1/4 x 1/8 3/8 3/8 1/8).
+// A workgroup owns 64 chroma columns x kTmCRows chroma rows: it stages the chroma
+// samples it needs (+1 each side) in LDS, converts every luma pixel of its tile
+// plus a one-pixel ring (the 2:1 filter's support) keeping the full-resolution
+// Cb/Cr in LDS, writes the tile's luma, then filters its chroma outputs from LDS.
+// The two transfer curves (PQ EOTF, 6 pow per pixel, and the BT.709 OETF, 3 pow
+// per pixel) are 1024-interval tables (built in double on the host, 2 x (kTmLutN
+// + 1) floats) staged in LDS and linearly interpolated: measured against the exact
+// curves, 2e-4 of the 8-bit outputs move by one LSB, inside the +-1 LSB
+// tolerance.
 #include "dts_internal.h"
 
 namespace dts {
@@ -106,35 +109,83 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
 
 } // namespace
 
+constexpr int kTmCRows = 8;                  // chroma rows per workgroup (16 luma rows)
+constexpr int kTmLW = 130, kTmLH = 2 * kTmCRows + 2;   // luma tile + ring: 128 + 2 columns, 16 + 2 rows
+constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged: 64 + 2 columns, 8 + 2 rows
+
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
     __shared__ float2 tl[2 * (kTmLutN + 1)];
-    for (int i = threadIdx.x; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
-    __syncthreads();
-    const int bx = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int f = blockIdx.z;
-    if (bx >= (P.w >> 1)) return;
+    __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
+    __shared__ float cb4[kTmLH][kTmLW], cr4[kTmLH][kTmLW];   // output Cb / Cr at full resolution
+    const int t = threadIdx.x, f = blockIdx.z;
+    const int cw = P.w >> 1, ch = P.h >> 1;
+    const int cx0 = blockIdx.x * 64, cy0 = blockIdx.y * kTmCRows;
+    const int x0 = 2 * cx0, y0 = 2 * cy0;
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
-    const int by_end = min((int)(blockIdx.y + 1) * kTmRows, P.h >> 1);
-    for (int by = blockIdx.y * kTmRows + (threadIdx.x >> 6); by < by_end; by += 4) {
-        const uint64_t ys = P.src.data[0] + sf + (uint64_t)(2 * by) * P.src.pitch[0] + 4 * bx;
-        const uint32_t l0 = *reinterpret_cast<const uint32_t *>(ys);
-        const uint32_t l1 = *reinterpret_cast<const uint32_t *>(ys + P.src.pitch[0]);
-        const uint32_t c =
-            *reinterpret_cast<const uint32_t *>(P.src.data[1] + sf + (uint64_t)by * P.src.pitch[1] + 4 * bx);
-        const float cb = (float)((int)((c & 0xffffu) >> 6) - 512) * (1.f / 896.f);
-        const float cr = (float)((int)(c >> 22) - 512) * (1.f / 896.f);
-        float Y[4], Cb[4], Cr[4];
-        pixel(P, tl, (int)((l0 & 0xffffu) >> 6), cb, cr, Y[0], Cb[0], Cr[0]);
-        pixel(P, tl, (int)(l0 >> 22), cb, cr, Y[1], Cb[1], Cr[1]);
-        pixel(P, tl, (int)((l1 & 0xffffu) >> 6), cb, cr, Y[2], Cb[2], Cr[2]);
-        pixel(P, tl, (int)(l1 >> 22), cb, cr, Y[3], Cb[3], Cr[3]);
-        const uint64_t yd = P.dst.data[0] + df + (uint64_t)(2 * by) * P.dst.pitch[0] + 2 * bx;
-        *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8(16.f + 219.f * Y[0]) | (q8(16.f + 219.f * Y[1]) << 8));
-        *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) =
-            (uint16_t)(q8(16.f + 219.f * Y[2]) | (q8(16.f + 219.f * Y[3]) << 8));
-        const int u = q8(128.f + 224.f * ((Cb[0] + Cb[1] + Cb[2] + Cb[3]) * 0.25f));
-        const int v = q8(128.f + 224.f * ((Cr[0] + Cr[1] + Cr[2] + Cr[3]) * 0.25f));
+    for (int i = t; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
+    for (int i = t; i < kTmCH * kTmCW; i += 256) {
+        const int r = i / kTmCW, c = i - r * kTmCW;
+        const int sy = min(max(cy0 - 1 + r, 0), ch - 1), sx = min(max(cx0 - 1 + c, 0), cw - 1);
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(P.src.data[1] + sf + (uint64_t)sy * P.src.pitch[1] +
+                                                                4 * sx);
+        cin[r][c] = make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f),
+                                (float)((int)(v >> 22) - 512) * (1.f / 896.f));
+    }
+    __syncthreads();
+    // every luma pixel of the tile + ring: row r = luma y0 - 1 + r, unit u < 64 = the
+    // column pair x0 + 2u, x0 + 2u + 1; u = 64 / 65 = the ring columns x0 - 1 / x0 + 128
+    for (int i = t; i < kTmLH * 66; i += 256) {
+        const int r = i / 66, u = i - r * 66;
+        const int y = min(max(y0 - 1 + r, 0), P.h - 1);
+        const int xa = u < 64 ? x0 + 2 * u : (u == 64 ? x0 - 1 : x0 + 128);
+        const int npx = u < 64 ? 2 : 1;
+        // zimg bilinear up, chroma location left: rows k (3/4) and k2 (1/4)
+        const int ky = y >> 1, k = min(ky, ch - 1), k2 = min(max((y & 1) ? ky + 1 : ky - 1, 0), ch - 1);
+        const uint64_t yrow = P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0];
+        float Yv[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (q >= npx) break;
+            const int x = min(max(xa + q, 0), P.w - 1);
+            const int j = x >> 1, j1 = min(min(j + 1, cw - 1), cx0 + 64);   // (x even: j1 unused, fx = 0)
+            const int lj = j - (cx0 - 1), lj1 = j1 - (cx0 - 1), lk = k - (cy0 - 1), lk2 = k2 - (cy0 - 1);
+            const float fx = (x & 1) ? 0.5f : 0.f;
+            const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
+            const float cb = 0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x));
+            const float cr = 0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y));
+            const int y10 = (int)(*reinterpret_cast<const uint16_t *>(yrow + 2 * x) >> 6);
+            float Cb, Cr;
+            pixel(P, tl, y10, cb, cr, Yv[q], Cb, Cr);
+            const int lx = (xa + q) - (x0 - 1);
+            cb4[r][lx] = Cb;
+            cr4[r][lx] = Cr;
+        }
+        // luma of the tile's own pixels (w, h even: a column pair is inside or outside together)
+        if (u < 64 && r >= 1 && r <= 2 * kTmCRows && y0 - 1 + r < P.h && xa < P.w) {
+            const uint64_t yd = P.dst.data[0] + df + (uint64_t)(y0 - 1 + r) * P.dst.pitch[0] + xa;
+            *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8(16.f + 219.f * Yv[0]) | (q8(16.f + 219.f * Yv[1]) << 8));
+        }
+    }
+    __syncthreads();
+    // chroma 2:1 (location left): columns 2 bx - 1 .. 2 bx + 1, rows 2 by - 1 .. 2 by + 2
+    constexpr float wx[3] = {0.25f, 0.5f, 0.25f}, wy[4] = {0.125f, 0.375f, 0.375f, 0.125f};
+    for (int i = t; i < 64 * kTmCRows; i += 256) {
+        const int ry = i >> 6, rx = i & 63;
+        const int bx = cx0 + rx, by = cy0 + ry;
+        if (bx >= cw || by >= ch) continue;
+        float sb = 0.f, sr = 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int ly = 2 * ry + a;                   // luma row 2 by - 1 + a, ring row 0 = y0 - 1
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const int lx = 2 * rx + b;               // luma column 2 bx - 1 + b, ring column 0 = x0 - 1
+                sb += wy[a] * wx[b] * cb4[ly][lx];
+                sr += wy[a] * wx[b] * cr4[ly][lx];
+            }
+        }
+        const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
         if (P.dst_fmt == DTS_FMT_NV12) {
             *reinterpret_cast<uint16_t *>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx) =
                 (uint16_t)(u | (v << 8));
@@ -147,7 +198,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s)
 {
-    const dim3 grid((unsigned)((p.w / 2 + 63) / 64), (unsigned)((p.h / 2 + kTmRows - 1) / kTmRows), (unsigned)p.nframes);
+    const dim3 grid((unsigned)((p.w / 2 + 63) / 64), (unsigned)((p.h / 2 + kTmCRows - 1) / kTmCRows), (unsigned)p.nframes);
     hipLaunchKernelGGL(k_tonemap, grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }

@@ -11,8 +11,18 @@
  *
  * zscale is zimg, which is third-party even to FFmpeg and absent here, so the
  * zimg steps are restated from the published standards they implement:
- *   - bt2020nc limited-range Y'CbCr -> R'G'B' (ITU-R BT.2020 Kr/Kb),
- *     chroma of each 2x2 luma block replicated (zimg filter_c=point);
+ *   - the 4:2:0 chroma resampled as vf_zscale configures zimg by default
+ *     (FFmpeg 4.4 vf_zscale.c: filter = filterc = "bilinear"; chroma location
+ *     taken from the frame, "left" = MPEG-2 4:2:0 siting: horizontally
+ *     co-sited with the even luma columns, vertically between the two luma
+ *     rows): up to 4:4:4 before the matrix by the triangle filter of radius 1
+ *     (odd luma columns = mean of the two chroma neighbours; luma rows take
+ *     0.75 / 0.25 of the nearer / farther chroma row), and back to 4:2:0 after
+ *     the output matrix by the same filter stretched 2:1 (horizontal taps
+ *     1/4 1/2 1/4 centred on the even column, vertical 1/8 3/8 3/8 1/8 around
+ *     the row pair); samples beyond the plane edge repeat the edge sample
+ *     (for radius-1 bilinear taps, zimg's edge mirroring gives the same);
+ *   - bt2020nc limited-range Y'CbCr -> R'G'B' (ITU-R BT.2020 Kr/Kb);
  *   - SMPTE ST 2084 (PQ) EOTF, scaled so NPL cd/m^2 -> 1.0;
  *   - bt2020 -> bt709 primaries in linear light (3x3 from the xy primaries and
  *     D65 white);
@@ -20,12 +30,13 @@
  *     restated from memory, including its peak fallback (10.0 for linear
  *     input without HDR side data) and param defaults (init());
  *   - BT.709 OETF (zimg's rec_709_oetf constants), bt709 limited-range
- *     Y'CbCr, chroma = mean of the 2x2 block (zimg bilinear 2:1, centred).
+ *     Y'CbCr (chroma 2:1 as above), rounded to 8 bits (zscale dither=none).
  * Parity status: unpinned (no zimg/ffmpeg here); the GPU must match this
  * restatement within +-1 LSB (float vs double).
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "oracle.h"
 
@@ -146,81 +157,119 @@ static int q8(double v)
 
 static int rd16(const uint8_t *p) { return (p[0] | (p[1] << 8)) >> 6; }
 
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* zimg bilinear, chroma location left: the 4:2:0 chroma value (Cb' or Cr', centred,
+ * c = 0 Cb / 1 Cr) at luma pixel (x, y) */
+static double chroma_up(const uint8_t *plane, int64_t pitch, int cw, int ch, int c, int x, int y)
+{
+    const int j = x >> 1, j1 = clampi(j + 1, 0, cw - 1);
+    const double fx = (x & 1) ? 0.5 : 0.0;
+    const int k = clampi(y >> 1, 0, ch - 1), k2 = clampi((y & 1) ? (y >> 1) + 1 : (y >> 1) - 1, 0, ch - 1);
+    double v[2];
+    int i;
+    for (i = 0; i < 2; i++) {
+        const uint8_t *row = plane + (int64_t)(i ? k2 : k) * pitch + 2 * c;
+        const double a = (rd16(row + 4 * j) - 512) / 896.0, b = (rd16(row + 4 * j1) - 512) / 896.0;
+        v[i] = (1.0 - fx) * a + fx * b;
+    }
+    return 0.75 * v[0] + 0.25 * v[1];
+}
+
 int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_t src_pitch[3],
                          int dstFmt, uint8_t *const dst[3], const int64_t dst_pitch[3],
                          int mode, double param, double desat, double peak, double npl)
 {
     const double kr2 = 0.2627, kb2 = 0.0593, kg2 = 1.0 - kr2 - kb2;
     const double kr7 = 0.2126, kb7 = 0.0722, kg7 = 1.0 - kr7 - kb7;
-    double M[3][3], scale, hpeak;
-    int bx, by;
+    static const double wx[3] = {0.25, 0.5, 0.25}, wy[4] = {0.125, 0.375, 0.375, 0.125};
+    double M[3][3], scale, hpeak, *cb4, *cr4;
+    int x, y, bx, by;
+    const int cw = w / 2, ch = h / 2;
     if (w < 2 || h < 2 || (w & 1) || (h & 1)) return -22;
     if (dstFmt != ORC_FMT_YUV420P && dstFmt != ORC_FMT_NV12) return -22;
     if (mode < TM_NONE || mode > TM_MOBIUS) return -22;
+    cb4 = (double *)malloc(sizeof(double) * (size_t)w * h);
+    cr4 = (double *)malloc(sizeof(double) * (size_t)w * h);
+    if (!cb4 || !cr4) {
+        free(cb4);
+        free(cr4);
+        return -12;
+    }
     orc_bt2020_to_bt709(M);
     if (npl <= 0.0) npl = 100.0;
     if (peak <= 0.0) peak = 10.0;
     param = orc_tonemap_param(mode, param);
     scale = 10000.0 / npl;
     hpeak = hable(peak);
-    for (by = 0; by < h / 2; by++)
-        for (bx = 0; bx < w / 2; bx++) {
-            const uint8_t *c = src[1] + (int64_t)by * src_pitch[1] + 4 * bx;
-            const double cb = (rd16(c) - 512) / 896.0, cr = (rd16(c + 2) - 512) / 896.0;
+    for (y = 0; y < h; y++)
+        for (x = 0; x < w; x++) {
+            const double cb = chroma_up(src[1], src_pitch[1], cw, ch, 0, x, y);
+            const double cr = chroma_up(src[1], src_pitch[1], cw, ch, 1, x, y);
+            const double yy = (rd16(src[0] + (int64_t)y * src_pitch[0] + 2 * x) - 64) / 876.0;
+            double rp = yy + 2.0 * (1.0 - kr2) * cr, bp = yy + 2.0 * (1.0 - kb2) * cb;
+            double gp = (yy - kr2 * rp - kb2 * bp) / kg2;
+            double r0 = pq_eotf(clamp01(rp)) * scale, g0 = pq_eotf(clamp01(gp)) * scale,
+                   b0 = pq_eotf(clamp01(bp)) * scale;
+            double r = M[0][0] * r0 + M[0][1] * g0 + M[0][2] * b0;
+            double g = M[1][0] * r0 + M[1][1] * g0 + M[1][2] * b0;
+            double b = M[2][0] * r0 + M[2][1] * g0 + M[2][2] * b0;
+            double sig, sig0, Y;
+            /* vf_tonemap.c tonemap() */
+            if (desat > 0.0) {
+                double luma = kr7 * r + kg7 * g + kb7 * b;
+                double ob = fmax(luma - desat, 1e-6) / fmax(luma, 1e-6);
+                r = r * (1.0 - ob) + luma * ob;
+                g = g * (1.0 - ob) + luma * ob;
+                b = b * (1.0 - ob) + luma * ob;
+            }
+            sig = fmax(fmax(fmax(r, g), b), 1e-6);
+            sig0 = sig;
+            switch (mode) {
+            case TM_LINEAR: sig = sig * param / peak; break;
+            case TM_GAMMA:
+                sig = sig > 0.05 ? pow(sig / peak, 1.0 / param) : sig * pow(0.05 / peak, 1.0 / param) / 0.05;
+                break;
+            case TM_CLIP: sig = fmin(fmax(sig * param, 0.0), 1.0); break;
+            case TM_REINHARD: sig = sig / (sig + param) * (peak + param) / peak; break;
+            case TM_HABLE: sig = hable(sig) / hpeak; break;
+            case TM_MOBIUS: sig = mobius(sig, param, peak); break;
+            default: break;
+            }
+            r *= sig / sig0;
+            g *= sig / sig0;
+            b *= sig / sig0;
+            r = rec709_oetf(clamp01(r));
+            g = rec709_oetf(clamp01(g));
+            b = rec709_oetf(clamp01(b));
+            Y = kr7 * r + kg7 * g + kb7 * b;
+            cb4[(size_t)y * w + x] = (b - Y) / (2.0 * (1.0 - kb7));
+            cr4[(size_t)y * w + x] = (r - Y) / (2.0 * (1.0 - kr7));
+            dst[0][(int64_t)y * dst_pitch[0] + x] = (uint8_t)q8(16.0 + 219.0 * Y);
+        }
+    /* 4:4:4 -> 4:2:0, chroma location left: taps 1/4 1/2 1/4 around column 2 bx,
+     * 1/8 3/8 3/8 1/8 over rows 2 by - 1 .. 2 by + 2, edge samples repeated */
+    for (by = 0; by < ch; by++)
+        for (bx = 0; bx < cw; bx++) {
             double sb = 0.0, sr = 0.0;
-            int d;
-            for (d = 0; d < 4; d++) {
-                const int x = 2 * bx + (d & 1), y = 2 * by + (d >> 1);
-                const double yy = (rd16(src[0] + (int64_t)y * src_pitch[0] + 2 * x) - 64) / 876.0;
-                double rp = yy + 2.0 * (1.0 - kr2) * cr, bp = yy + 2.0 * (1.0 - kb2) * cb;
-                double gp = (yy - kr2 * rp - kb2 * bp) / kg2;
-                double r0 = pq_eotf(clamp01(rp)) * scale, g0 = pq_eotf(clamp01(gp)) * scale,
-                       b0 = pq_eotf(clamp01(bp)) * scale;
-                double r = M[0][0] * r0 + M[0][1] * g0 + M[0][2] * b0;
-                double g = M[1][0] * r0 + M[1][1] * g0 + M[1][2] * b0;
-                double b = M[2][0] * r0 + M[2][1] * g0 + M[2][2] * b0;
-                double sig, sig0, Y, Cb, Cr;
-                /* vf_tonemap.c tonemap() */
-                if (desat > 0.0) {
-                    double luma = kr7 * r + kg7 * g + kb7 * b;
-                    double ob = fmax(luma - desat, 1e-6) / fmax(luma, 1e-6);
-                    r = r * (1.0 - ob) + luma * ob;
-                    g = g * (1.0 - ob) + luma * ob;
-                    b = b * (1.0 - ob) + luma * ob;
+            int i, t;
+            for (i = 0; i < 4; i++) {
+                const int yy = clampi(2 * by - 1 + i, 0, h - 1);
+                for (t = 0; t < 3; t++) {
+                    const int xx = clampi(2 * bx - 1 + t, 0, w - 1);
+                    sb += wy[i] * wx[t] * cb4[(size_t)yy * w + xx];
+                    sr += wy[i] * wx[t] * cr4[(size_t)yy * w + xx];
                 }
-                sig = fmax(fmax(fmax(r, g), b), 1e-6);
-                sig0 = sig;
-                switch (mode) {
-                case TM_LINEAR: sig = sig * param / peak; break;
-                case TM_GAMMA:
-                    sig = sig > 0.05 ? pow(sig / peak, 1.0 / param) : sig * pow(0.05 / peak, 1.0 / param) / 0.05;
-                    break;
-                case TM_CLIP: sig = fmin(fmax(sig * param, 0.0), 1.0); break;
-                case TM_REINHARD: sig = sig / (sig + param) * (peak + param) / peak; break;
-                case TM_HABLE: sig = hable(sig) / hpeak; break;
-                case TM_MOBIUS: sig = mobius(sig, param, peak); break;
-                default: break;
-                }
-                r *= sig / sig0;
-                g *= sig / sig0;
-                b *= sig / sig0;
-                r = rec709_oetf(clamp01(r));
-                g = rec709_oetf(clamp01(g));
-                b = rec709_oetf(clamp01(b));
-                Y = kr7 * r + kg7 * g + kb7 * b;
-                Cb = (b - Y) / (2.0 * (1.0 - kb7));
-                Cr = (r - Y) / (2.0 * (1.0 - kr7));
-                dst[0][(int64_t)y * dst_pitch[0] + x] = (uint8_t)q8(16.0 + 219.0 * Y);
-                sb += Cb;
-                sr += Cr;
             }
             if (dstFmt == ORC_FMT_NV12) {
-                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx] = (uint8_t)q8(128.0 + 224.0 * sb * 0.25);
-                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx + 1] = (uint8_t)q8(128.0 + 224.0 * sr * 0.25);
+                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx] = (uint8_t)q8(128.0 + 224.0 * sb);
+                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx + 1] = (uint8_t)q8(128.0 + 224.0 * sr);
             } else {
-                dst[1][(int64_t)by * dst_pitch[1] + bx] = (uint8_t)q8(128.0 + 224.0 * sb * 0.25);
-                dst[2][(int64_t)by * dst_pitch[2] + bx] = (uint8_t)q8(128.0 + 224.0 * sr * 0.25);
+                dst[1][(int64_t)by * dst_pitch[1] + bx] = (uint8_t)q8(128.0 + 224.0 * sb);
+                dst[2][(int64_t)by * dst_pitch[2] + bx] = (uint8_t)q8(128.0 + 224.0 * sr);
             }
         }
+    free(cb4);
+    free(cr4);
     return 0;
 }
