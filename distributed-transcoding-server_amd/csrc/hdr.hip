@@ -109,7 +109,8 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
 
 } // namespace
 
-constexpr int kTmCRows = 8;                  // chroma rows per workgroup (16 luma rows)
+constexpr int kTmCRows = 8;                  // chroma rows per tile (16 luma rows)
+constexpr int kTmTiles = 8;                  // tiles per workgroup, walked top to bottom (one table load)
 constexpr int kTmLW = 130, kTmLH = 2 * kTmCRows + 2;   // luma tile + ring: 128 + 2 columns, 16 + 2 rows
 constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged: 64 + 2 columns, 8 + 2 rows
 
@@ -120,10 +121,14 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     __shared__ float cb4[kTmLH][kTmLW], cr4[kTmLH][kTmLW];   // output Cb / Cr at full resolution
     const int t = threadIdx.x, f = blockIdx.z;
     const int cw = P.w >> 1, ch = P.h >> 1;
-    const int cx0 = blockIdx.x * 64, cy0 = blockIdx.y * kTmCRows;
-    const int x0 = 2 * cx0, y0 = 2 * cy0;
+    const int cx0 = blockIdx.x * 64;
+    const int x0 = 2 * cx0;
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
     for (int i = t; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
+    for (int tile = 0; tile < kTmTiles; ++tile) {
+    const int cy0 = (blockIdx.y * kTmTiles + tile) * kTmCRows, y0 = 2 * cy0;
+    if (cy0 >= ch) break;
+    if (tile) __syncthreads();                      // the previous tile's chroma pass is done with cin / cb4
     for (int i = t; i < kTmCH * kTmCW; i += 256) {
         const int r = i / kTmCW, c = i - r * kTmCW;
         const int sy = min(max(cy0 - 1 + r, 0), ch - 1), sx = min(max(cx0 - 1 + c, 0), cw - 1);
@@ -133,39 +138,56 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
                                 (float)((int)(v >> 22) - 512) * (1.f / 896.f));
     }
     __syncthreads();
-    // every luma pixel of the tile + ring: row r = luma y0 - 1 + r, unit u < 64 = the
-    // column pair x0 + 2u, x0 + 2u + 1; u = 64 / 65 = the ring columns x0 - 1 / x0 + 128
-    for (int i = t; i < kTmLH * 66; i += 256) {
-        const int r = i / 66, u = i - r * 66;
-        const int y = min(max(y0 - 1 + r, 0), P.h - 1);
-        const int xa = u < 64 ? x0 + 2 * u : (u == 64 ? x0 - 1 : x0 + 128);
-        const int npx = u < 64 ? 2 : 1;
-        // zimg bilinear up, chroma location left: rows k (3/4) and k2 (1/4)
+    // one luma pixel (clamped into the picture): zimg bilinear up (chroma location left:
+    // columns j, j + 1 at weights 1 - fx, fx; rows k, k2 at 3/4, 1/4) + the conversion
+    auto pix = [&](int xr, int yr, float &Yv, float &Cb, float &Cr) {
+        const int x = min(max(xr, 0), P.w - 1), y = min(max(yr, 0), P.h - 1);
         const int ky = y >> 1, k = min(ky, ch - 1), k2 = min(max((y & 1) ? ky + 1 : ky - 1, 0), ch - 1);
-        const uint64_t yrow = P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0];
-        float Yv[2];
+        const int j = x >> 1, j1 = min(min(j + 1, cw - 1), cx0 + 64);   // (x even: j1 unused, fx = 0)
+        const int lj = j - (cx0 - 1), lj1 = j1 - (cx0 - 1), lk = k - (cy0 - 1), lk2 = k2 - (cy0 - 1);
+        const float fx = (x & 1) ? 0.5f : 0.f;
+        const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
+        const float cb = 0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x));
+        const float cr = 0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y));
+        const int y10 = (int)(*reinterpret_cast<const uint16_t *>(P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0] +
+                                                                  2 * x) >> 6);
+        pixel(P, tl, y10, cb, cr, Yv, Cb, Cr);
+    };
+    // the tile's 2x2 blocks (luma written here) ...
+    for (int i = t; i < 64 * kTmCRows; i += 256) {
+        const int byl = i >> 6, bxl = i & 63;
+        float Yv[4], Cb[4], Cr[4];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            if (q >= npx) break;
-            const int x = min(max(xa + q, 0), P.w - 1);
-            const int j = x >> 1, j1 = min(min(j + 1, cw - 1), cx0 + 64);   // (x even: j1 unused, fx = 0)
-            const int lj = j - (cx0 - 1), lj1 = j1 - (cx0 - 1), lk = k - (cy0 - 1), lk2 = k2 - (cy0 - 1);
-            const float fx = (x & 1) ? 0.5f : 0.f;
-            const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
-            const float cb = 0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x));
-            const float cr = 0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y));
-            const int y10 = (int)(*reinterpret_cast<const uint16_t *>(yrow + 2 * x) >> 6);
-            float Cb, Cr;
-            pixel(P, tl, y10, cb, cr, Yv[q], Cb, Cr);
-            const int lx = (xa + q) - (x0 - 1);
-            cb4[r][lx] = Cb;
-            cr4[r][lx] = Cr;
+        for (int q = 0; q < 4; ++q) pix(x0 + 2 * bxl + (q & 1), y0 + 2 * byl + (q >> 1), Yv[q], Cb[q], Cr[q]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            cb4[1 + 2 * byl + (q >> 1)][1 + 2 * bxl + (q & 1)] = Cb[q];
+            cr4[1 + 2 * byl + (q >> 1)][1 + 2 * bxl + (q & 1)] = Cr[q];
         }
-        // luma of the tile's own pixels (w, h even: a column pair is inside or outside together)
-        if (u < 64 && r >= 1 && r <= 2 * kTmCRows && y0 - 1 + r < P.h && xa < P.w) {
-            const uint64_t yd = P.dst.data[0] + df + (uint64_t)(y0 - 1 + r) * P.dst.pitch[0] + xa;
+        const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
+        if (xa < P.w && ya < P.h) {                         // w, h even: the whole block is inside
+            const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
             *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8(16.f + 219.f * Yv[0]) | (q8(16.f + 219.f * Yv[1]) << 8));
+            *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) =
+                (uint16_t)(q8(16.f + 219.f * Yv[2]) | (q8(16.f + 219.f * Yv[3]) << 8));
         }
+    }
+    // ... and the one-pixel ring (chroma only): rows y0 - 1 and y0 + 16 (130 pixels
+    // each), columns x0 - 1 and x0 + 128 of the 16 rows between
+    for (int i = t; i < 2 * kTmLW + 2 * 2 * kTmCRows; i += 256) {
+        int lx, ly;
+        if (i < 2 * kTmLW) {
+            ly = i < kTmLW ? 0 : kTmLH - 1;
+            lx = i < kTmLW ? i : i - kTmLW;
+        } else {
+            const int k = i - 2 * kTmLW;
+            ly = 1 + (k >> 1);
+            lx = (k & 1) ? kTmLW - 1 : 0;
+        }
+        float Yv, Cb, Cr;
+        pix(x0 - 1 + lx, y0 - 1 + ly, Yv, Cb, Cr);
+        cb4[ly][lx] = Cb;
+        cr4[ly][lx] = Cr;
     }
     __syncthreads();
     // chroma 2:1 (location left): columns 2 bx - 1 .. 2 bx + 1, rows 2 by - 1 .. 2 by + 2
@@ -194,11 +216,13 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             *reinterpret_cast<uint8_t *>(P.dst.data[2] + df + (uint64_t)by * P.dst.pitch[2] + bx) = (uint8_t)v;
         }
     }
+    }
 }
 
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s)
 {
-    const dim3 grid((unsigned)((p.w / 2 + 63) / 64), (unsigned)((p.h / 2 + kTmCRows - 1) / kTmCRows), (unsigned)p.nframes);
+    const int rows = kTmCRows * kTmTiles;
+    const dim3 grid((unsigned)((p.w / 2 + 63) / 64), (unsigned)((p.h / 2 + rows - 1) / rows), (unsigned)p.nframes);
     hipLaunchKernelGGL(k_tonemap, grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }
