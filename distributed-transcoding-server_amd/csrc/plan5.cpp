@@ -392,9 +392,6 @@ bool plan5_kind(const Plan5In &in, Plan5Kind &out)
         pk.FA = lds;                                       // fragment buffers (V(b) in buffer b % kL5FragBufs)
         pk.FB = 2048 * std::max(FM, 1);
         lds += kL5FragBufs * pk.FB;
-        if (std::getenv("DTS_PLAN_DEBUG"))
-            std::fprintf(stderr, "plan5 %s SW %d FM %d SB %d lds %d RR %d %d %d\n", in.chroma ? "chroma" : "luma", SW, FM,
-                         pk.SB, lds, RR[0], nr > 1 ? RR[1] : 0, nr > 2 ? RR[2] : 0);
         // rings: (rendition, plane), two column-major byte planes each
         pk.nrings = nr * nplanes;
         for (int r = 0; r < nr; ++r)
