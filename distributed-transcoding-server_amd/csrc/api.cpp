@@ -173,6 +173,14 @@ struct dts_graph {
     Job5 *dev_jobs5 = nullptr;
     Kind5 *dev_kinds5 = nullptr;
     int njobs5 = 0, lds5 = 0, grid5 = 0;
+    // v6 ladder (ladder6.hip): planar 8-bit sources; v5 stays planned for frames whose
+    // planes are not 4-byte aligned
+    bool v6 = false;
+    void *dev_tables6 = nullptr;
+    const Unit6 *dev_units6 = nullptr;
+    const uint32_t *dev_frag6 = nullptr;
+    const int32_t *dev_fire6 = nullptr;
+    int nunits6 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -412,6 +420,8 @@ struct GraphPlan {
     Plan5Kind p5[2];                      // luma, chroma
     std::vector<Job5> jobs5;
     int lds5 = 0;
+    bool v6 = false;                      // ... and on k_ladder6 where frames are 4-byte aligned
+    Plan6 p6;
     dts_graph_info info{};
 };
 
@@ -455,13 +465,22 @@ bool v5_enabled()
     return !(f && (f[0] == '3' || f[0] == '4'));
 }
 
-// k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs
+// DTS_LADDER=5 / 4 / 3 keep the graph off the v6 kernel
+bool v6_enabled()
+{
+    const char *f = std::getenv("DTS_LADDER");
+    return !(f && (f[0] == '3' || f[0] == '4' || f[0] == '5'));
+}
+
+// k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
+// and k_ladder6 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
 {
     if (!v5_enabled() || s.hdr_to_sdr) return false;
     if (s.src_fmt != DTS_FMT_YUV420P && s.src_fmt != DTS_FMT_NV12) return false;
+    Plan5In ins[2];
     for (int kind = 0; kind < 2; ++kind) {
-        Plan5In in;
+        Plan5In &in = ins[kind];
         in.chroma = kind == 1;
         in.nv12_chroma = kind == 1 && s.src_fmt == DTS_FMT_NV12;
         in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
@@ -480,6 +499,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     std::stable_sort(gp.jobs5.begin(), gp.jobs5.end(), [&](const Job5 &a, const Job5 &b) { return srcx(a) < srcx(b); });
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
+    gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
     return true;
 }
 
@@ -604,10 +624,10 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     }
     if (s.quality) algo += in.out_frame_bytes[s.quality_out];
     in.algo_bytes_per_frame = algo;
-    in.njobs = (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
+    in.njobs = gp.v6 ? (int)gp.p6.units.size() : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
     in.lds_bytes = std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
     in.ladder_v4_mask = (int32_t)gp.v4_mask;
-    in.ladder_v5 = gp.v5 ? 1 : 0;
+    in.ladder_v5 = gp.v6 ? 2 : (gp.v5 ? 1 : 0);
     for (int kind = 0; kind < 2; ++kind) {
         in.v5_strip_width[kind] = gp.v5 ? gp.p5[kind].strip_width : 0;
         in.v5_strips[kind] = gp.v5 ? (int32_t)gp.p5[kind].strips.size() : 0;
@@ -874,6 +894,25 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
     return DTS_OK;
 }
 
+// v6 tables -> one device blob (units, fragment pairs, fire tables)
+static int upload_v6(dts_graph *g, const GraphPlan &gp)
+{
+    dts_ctx *ctx = g->ctx;
+    std::vector<uint8_t> blob;
+    const size_t u_off = push_blob(blob, gp.p6.units);
+    const size_t f_off = push_blob(blob, gp.p6.frag);
+    const size_t r_off = push_blob(blob, gp.p6.fire);
+    HIPCHK(ctx, hipMalloc(&g->dev_tables6, blob.size()));
+    HIPCHK(ctx, hipMemcpy(g->dev_tables6, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables6);
+    g->dev_units6 = reinterpret_cast<const Unit6 *>(base + u_off);
+    g->dev_frag6 = reinterpret_cast<const uint32_t *>(base + f_off);
+    g->dev_fire6 = reinterpret_cast<const int32_t *>(base + r_off);
+    g->nunits6 = (int)gp.p6.units.size();
+    g->v6 = true;
+    return DTS_OK;
+}
+
 int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
 {
     if (!ctx || !spec || !out) return DTS_E_INVAL;
@@ -901,6 +940,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         e = gp.v5 ? DTS_OK : upload_v3(g, gp.kts);
         if (!e && gp.v4_mask) e = upload_v4(g, gp);
         if (!e && gp.v5) e = upload_v5(g, gp);
+        if (!e && gp.v6) e = upload_v6(g, gp);
         if (!e && hipMalloc(&g->dev_queue, kQueueSlots * kQueueWidth * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
             e = DTS_E_HIP;
@@ -983,6 +1023,7 @@ void dts_graph_destroy(dts_graph *g)
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_tables5) hipFree(g->dev_tables5);
+    if (g->dev_tables6) hipFree(g->dev_tables6);
     if (g->dev_queue) hipFree(g->dev_queue);
     qscratch_free(g->qs);
     for (auto &q : g->hqs) qscratch_free(q);
@@ -1128,6 +1169,15 @@ static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, co
     return DTS_OK;
 }
 
+// k_ladder6 reads and writes planes with 4-byte accesses: every plane base and pitch
+// 4-byte aligned (else the graph runs on k_ladder5)
+static bool planes_aligned6(const DevPlanes &p)
+{
+    for (int pl = 0; pl < 3; ++pl)
+        if ((p.data[pl] | (uint64_t)p.pitch[pl]) & 3u) return false;
+    return (p.fstride & 3) == 0;
+}
+
 // The ladder launches (v4 kinds, then v3 kinds) for nframes frames of src into dst[k]
 // (format dst_fmt[k]); persistent grids over nframes x njobs items, items per launch < 2^30.
 static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, const int *dst_fmt, int nframes,
@@ -1153,7 +1203,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    const int njobs_max = std::max(1, std::max(std::max(p.njobs, g->njobs4), g->njobs5));
+    const int njobs_max = std::max(1, std::max(std::max(p.njobs, g->njobs4), std::max(g->njobs5, g->nunits6)));
     const int max_frames = std::max(1, (1 << 30) / njobs_max);
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
         const int n = std::min(max_frames, nframes - f0);
@@ -1163,6 +1213,22 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
+        bool aligned6 = g->v6 && planes_aligned6(pp.src);
+        for (int k = 0; k < s.nout && aligned6; ++k) aligned6 = planes_aligned6(pp.dst[k]);
+        if (aligned6) {
+            Ladder6Params q{};
+            q.src = pp.src;
+            for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
+            q.nunits = g->nunits6;
+            q.nframes = n;
+            q.units = g->dev_units6;
+            q.frag = g->dev_frag6;
+            q.fire = g->dev_fire6;
+            const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->nunits6;
+            if (grid > INT32_MAX) return DTS_E_RANGE;
+            HIPCHK(ctx, launch_ladder6(q, (int)grid, st));
+            continue;
+        }
         if (g->v5) {
             Ladder5Params q{};
             q.src = pp.src;

@@ -241,6 +241,54 @@ hipError_t launch_ladder5(const Ladder5Params &p, int src_kind, int lds_bytes, i
 int ladder5_blocks_per_cu(int src_kind, int lds_bytes);
 
 // ---------------------------------------------------------------------------
+// v6 ladder (ladder6.hip, plan6.cpp): one wave per (frame, plane kind,
+// rendition, column group), walking the plane top to bottom; the H outputs stay
+// in VGPRs (the H MFMA's C layout is the V MFMA's A layout), so there is no LDS,
+// no barrier and no ring traffic.
+// ---------------------------------------------------------------------------
+constexpr int kL6Gran = 16;         // source rows per granule (the H MFMA's M)
+constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, V K blocks), ladder6.hip
+
+// variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns
+// per H tile, VKB K blocks of 64 source rows (4 VKB granules held) per V row block, and
+// CT 16-column tiles per plane: 4 MFMA tiles when HKB = VKB = 1, else 2
+constexpr int l6_variant(int np, int hkb, int vkb) { return (np == 2 ? 4 : 0) + 2 * (hkb - 1) + (vkb - 1); }
+constexpr int l6_np(int v) { return v >= 4 ? 2 : 1; }
+constexpr int l6_hkb(int v) { return ((v >> 1) & 1) + 1; }
+constexpr int l6_vkb(int v) { return (v & 1) + 1; }
+constexpr int l6_ct(int v) { return ((v & 3) == 0 ? 4 : 2) / l6_np(v); }
+
+struct Unit6 {                      // one wave's share of a frame
+    int32_t variant;                // ladder6.hip kVar6[variant]
+    int32_t kind;                   // 0 luma, 1 chroma (U and V planes in one unit)
+    int32_t rung;
+    int32_t col0;                   // first output column (multiple of 16)
+    int32_t ncols;                  // output columns this unit stores (<= 16 CT)
+    int32_t ngran;                  // source granules (srcH / 16, rounded up)
+    int32_t srcH, dstH;
+    int32_t nrb;                    // row blocks (16 output rows) of the rendition
+    int32_t fmt;                    // the rendition's output format
+    uint32_t hfrag;                 // H fragment pair of tile c, K block kb: hfrag + c * HKB + kb
+    uint32_t vfrag;                 // V fragment pair of row block j, K block kb: vfrag + j * VKB + kb
+    int32_t fire;                   // the rendition's fire table: row block j runs after granule fire[j]
+    int32_t dstW;
+    int32_t x0[4];                  // first source column of each column tile's H K blocks (multiple of 4,
+                                    // except a right-edge tile ending at the plane's last column)
+    int32_t pad_[2];
+};
+
+struct Ladder6Params {
+    DevPlanes src;
+    DevPlanes dst[kMaxRungs];
+    int32_t nunits, nframes, pad_[2];
+    const Unit6 *units;
+    const uint32_t *frag;           // fragment pairs (taps >> 8, taps & 255 as signed bytes), 512 dwords each
+    const int32_t *fire;
+};
+
+hipError_t launch_ladder6(const Ladder6Params &p, int grid, hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
 // ---------------------------------------------------------------------------
 constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x

@@ -105,4 +105,17 @@ struct Plan5Kind {
 // false: the geometry / format does not fit k_ladder5 (the kind then runs on v4 / v3)
 bool plan5_kind(const Plan5In &in, Plan5Kind &out);
 
+// v6 ladder plan (plan6.cpp, ladder6.hip): the work units of one frame (both
+// plane kinds, every rendition), their B fragments and the V fire tables.
+struct Plan6 {
+    std::vector<Unit6> units;
+    std::vector<uint32_t> frag;      // fragment pairs, 512 dwords each
+    std::vector<int32_t> fire;
+};
+
+// kinds[0] luma, kinds[1] chroma (Plan5In: same inputs as v5).  false: the graph
+// does not fit k_ladder6 (nv12 source, planes narrower than 64 or 128 columns,
+// windows wider than two K blocks ...): it then runs on k_ladder5.
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out);
+
 } // namespace dts

@@ -1,0 +1,257 @@
+// plan6.cpp -- host planning of the v6 ladder (ladder6.hip, dts_internal.h
+// "v6 ladder"): per frame, one work unit per (plane kind, rendition, group of
+// 16-column tiles); per tile the H K blocks (64 source columns each) and their
+// B fragments; per rendition the V row blocks (16 output rows), the granule
+// after which each runs and its B fragments.  The taps are the libswscale
+// ones (filters.cpp sws_build_filter = FFmpeg 4.4 utils.c initFilter and
+// pack_v), re-laid for v_mfma_i32_16x16x64_i8; nothing here changes a tap.
+//
+// K order.  The MFMA multiplies lane (m, g)'s A byte j with lane (n, g)'s B
+// byte j and sums over (g, j) (tools/probe_mfma_i8.hip), so any K labelling
+// both operands share is exact:
+//  * H: lane (row m, group g) loads 16 consecutive source bytes at x0 + 64 kb
+//    + 16 g; B byte j of lane (output n, g) is the tap of column x0 + 64 kb +
+//    16 g + j;
+//  * V: the H C registers of 4 VKB granules are the A operand as they stand
+//    (lane (column, g) holds rows 4g..4g+3 of each granule); K block kb's
+//    dword d is ring slot 4 kb + d, which holds granule q - ((q - s) mod R)
+//    when the block runs after granule q.  B byte 4d + i of lane (output row n,
+//    g) is the tap of source row 16 granule + 4 g + i.
+#include <algorithm>
+#include <cstring>
+
+#include "filters.h"
+
+namespace dts {
+
+namespace {
+
+void extent6(const SwsFilter &f, int i, int &a, int &z)
+{
+    a = 1 << 30;
+    z = -1;
+    for (int j = 0; j < f.size; ++j)
+        if (f.coeff[(size_t)i * f.size + j]) {
+            a = std::min(a, f.pos[i] + j);
+            z = std::max(z, f.pos[i] + j);
+        }
+}
+
+int htap6(const SwsFilter &f, int i, int src)
+{
+    const int j = src - f.pos[i];
+    return (j >= 0 && j < f.size) ? f.coeff[(size_t)i * f.size + j] : 0;
+}
+
+int vtap6(const VTable &v, int y, int row)
+{
+    const int d = row - v.pos[y];
+    if (d < 0 || d >= 2 * v.nv) return 0;
+    const uint32_t w = v.coef[(size_t)y * v.nv + d / 2];
+    return (int16_t)(d & 1 ? w >> 16 : w & 0xffff);
+}
+
+// one fragment pair from tapf(lane, j) (j = byte of the lane's 16): c = 256 hi + lo,
+// hi and lo signed bytes; false if a tap does not split
+template <class F>
+bool put6(std::vector<uint32_t> &bf, uint32_t frag, F tapf)
+{
+    uint8_t *hi = reinterpret_cast<uint8_t *>(bf.data() + (size_t)frag * 512);
+    uint8_t *lo = hi + 1024;
+    for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 16; ++j) {
+            const int c = tapf(lane, j);
+            const int l = (int8_t)(c & 0xff), h = (c - l) >> 8;
+            if (h < -128 || h > 127) return false;
+            hi[lane * 16 + j] = (uint8_t)h;
+            lo[lane * 16 + j] = (uint8_t)l;
+        }
+    return true;
+}
+
+struct Rend6 {                      // one (plane kind, rendition)
+    int hkb = 0, vkb = 0;
+    std::vector<int> x0;            // per 16-column tile
+    std::vector<int> fire;          // per row block
+};
+
+// H K blocks and per-tile x0; false if a tile's taps span more than 2 K blocks
+bool plan_h6(const SwsFilter &f, int srcW, int dstW, Rend6 &r)
+{
+    const int ntiles = (dstW + 15) / 16;
+    for (int hkb = 1; hkb <= 2; ++hkb) {
+        if (srcW < 64 * hkb) return false;
+        const int xmax = srcW - 64 * hkb;                  // (a right-edge tile may start unaligned)
+        bool ok = true;
+        r.x0.assign(ntiles, 0);
+        for (int t = 0; t < ntiles && ok; ++t) {
+            int a = 1 << 30, z = -1;
+            for (int o = 16 * t; o < std::min(16 * t + 16, dstW); ++o) {
+                int ai, zi;
+                extent6(f, o, ai, zi);
+                if (zi < 0) continue;
+                a = std::min(a, ai);
+                z = std::max(z, zi);
+            }
+            if (z < 0) continue;                           // all-zero taps (never for a normalised filter)
+            const int x0 = std::min(a & ~3, xmax);
+            r.x0[t] = x0;
+            ok = z < x0 + 64 * hkb;
+        }
+        if (ok) {
+            r.hkb = hkb;
+            return true;
+        }
+    }
+    return false;
+}
+
+// V: the granule after which each row block runs, and the ring depth
+bool plan_v6(const VTable &v, int srcH, int dstH, Rend6 &r)
+{
+    const int ngran = (srcH + kL6Gran - 1) / kL6Gran;
+    const int nrb = (dstH + 15) / 16;
+    std::vector<int> a(nrb), z(nrb);
+    for (int j = 0; j < nrb; ++j) {
+        a[j] = 1 << 30;
+        z[j] = -1;
+        for (int y = 16 * j; y < std::min(16 * j + 16, dstH); ++y)
+            for (int d = 0; d < 2 * v.nv; ++d)
+                if (vtap6(v, y, v.pos[y] + d)) {
+                    a[j] = std::min(a[j], v.pos[y] + d);
+                    z[j] = std::max(z[j], v.pos[y] + d);
+                }
+        if (z[j] < 0 || z[j] >= srcH || a[j] < 0) return false;
+    }
+    r.fire.assign(nrb, 0);
+    for (int j = 0; j < nrb; ++j) {
+        r.fire[j] = std::min(z[j] / kL6Gran, ngran - 1);
+        if (j && r.fire[j] < r.fire[j - 1]) return false;   // the kernel runs row blocks in order
+    }
+    for (int vkb = 1; vkb <= 2; ++vkb) {
+        const int R = 4 * vkb;
+        bool ok = true;
+        for (int j = 0; j < nrb && ok; ++j) ok = a[j] >= kL6Gran * (r.fire[j] - R + 1);
+        if (ok) {
+            r.vkb = vkb;
+            return true;
+        }
+    }
+    return false;
+}
+
+} // namespace
+
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
+{
+    out = Plan6{};
+    struct Cost { Unit6 u; int64_t cost; };
+    std::vector<Cost> units;
+    uint32_t nfrag = 0;
+    struct Pending { int kind, rung; Rend6 r; uint32_t hfrag, vfrag; int fire; int ct; };
+    std::vector<Pending> todo;
+    for (int kind = 0; kind < 2; ++kind) {
+        const Plan5In &in = kinds[kind];
+        if (in.nv12_chroma) return false;                  // planar sources only (nv12: k_ladder5)
+        if ((int)in.rungs.size() < 1 || (int)in.rungs.size() > DTS_MAX_OUTPUTS) return false;
+        for (int k = 0; k < (int)in.rungs.size(); ++k) {
+            const Plan5Rung &R = in.rungs[k];
+            if (R.fmt != DTS_FMT_YUV420P && R.fmt != DTS_FMT_NV12) return false;
+            const SwsFilter &f = *R.fh;
+            for (int i = 0; i < R.dstW; ++i) {             // H bias = 128 * 16384
+                int sum = 0;
+                for (int j = 0; j < f.size; ++j) sum += f.coeff[(size_t)i * f.size + j];
+                if (sum != 1 << 14) return false;
+            }
+            for (int y = 0; y < R.dstH; ++y) {             // V bias = 128 * 4096
+                int sum = 0;
+                for (int d = 0; d < 2 * R.v->nv; ++d) sum += vtap6(*R.v, y, R.v->pos[y] + d);
+                if (sum != 1 << 12) return false;
+            }
+            Pending p;
+            p.kind = kind;
+            p.rung = k;
+            if (!plan_h6(f, in.srcW, R.dstW, p.r) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
+            const int np = in.chroma ? 2 : 1;
+            p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb));
+            const int ntiles = (R.dstW + 15) / 16;
+            const int ntp = (ntiles + p.ct - 1) / p.ct * p.ct;  // tiles padded to whole units
+            p.r.x0.resize(ntp, 0);
+            p.hfrag = nfrag;
+            nfrag += (uint32_t)(ntp * p.r.hkb);
+            p.vfrag = nfrag;
+            nfrag += (uint32_t)(p.r.fire.size() * p.r.vkb);
+            p.fire = (int)out.fire.size();
+            out.fire.insert(out.fire.end(), p.r.fire.begin(), p.r.fire.end());
+            todo.push_back(std::move(p));
+        }
+    }
+    out.frag.assign((size_t)nfrag * 512, 0);
+    for (const Pending &p : todo) {
+        const Plan5In &in = kinds[p.kind];
+        const Plan5Rung &R = in.rungs[p.rung];
+        const SwsFilter &f = *R.fh;
+        const VTable &v = *R.v;
+        const int np = in.chroma ? 2 : 1;
+        const int var = l6_variant(np, p.r.hkb, p.r.vkb);
+        const int ntp = (int)p.r.x0.size();
+        for (int t = 0; t < ntp; ++t)
+            for (int kb = 0; kb < p.r.hkb; ++kb) {
+                const int base = p.r.x0[t] + 64 * kb;
+                if (!put6(out.frag, p.hfrag + (uint32_t)(t * p.r.hkb + kb), [&](int lane, int j) {
+                        const int o = 16 * t + (lane & 15);
+                        return o < R.dstW ? htap6(f, o, base + 16 * (lane >> 4) + j) : 0;
+                    }))
+                    return false;
+            }
+        const int R4 = 4 * p.r.vkb;
+        for (int jb = 0; jb < (int)p.r.fire.size(); ++jb) {
+            const int q = p.r.fire[jb];
+            std::vector<int> got(16, 0);
+            for (int kb = 0; kb < p.r.vkb; ++kb) {
+                if (!put6(out.frag, p.vfrag + (uint32_t)(jb * p.r.vkb + kb), [&](int lane, int jj) {
+                        const int s = 4 * kb + jj / 4;
+                        const int gran = q - ((q - s) % R4 + R4) % R4;
+                        const int row = kL6Gran * gran + 4 * (lane >> 4) + (jj & 3);
+                        const int y = 16 * jb + (lane & 15);
+                        const int c = (gran >= 0 && row < in.srcH && y < R.dstH) ? vtap6(v, y, row) : 0;
+                        got[lane & 15] += c;
+                        return c;
+                    }))
+                    return false;
+            }
+            for (int n = 0; n < 16; ++n)                   // every tap of the block landed in a slot
+                if (16 * jb + n < R.dstH && got[n] != 1 << 12) return false;
+        }
+        const int ngran = (in.srcH + kL6Gran - 1) / kL6Gran;
+        const int nrb = (int)p.r.fire.size();
+        for (int u = 0; u * p.ct < ntp; ++u) {
+            Unit6 w{};
+            w.variant = var;
+            w.kind = p.kind;
+            w.rung = p.rung;
+            w.col0 = 16 * p.ct * u;
+            w.ncols = std::min(16 * p.ct, R.dstW - w.col0);
+            w.ngran = ngran;
+            w.srcH = in.srcH;
+            w.dstH = R.dstH;
+            w.dstW = R.dstW;
+            w.nrb = nrb;
+            w.fmt = R.fmt;
+            w.hfrag = p.hfrag + (uint32_t)(u * p.ct * p.r.hkb);
+            w.vfrag = p.vfrag;
+            w.fire = p.fire;
+            for (int c = 0; c < 4; ++c) w.x0[c] = c < p.ct ? p.r.x0[(size_t)u * p.ct + c] : 0;
+            // MFMAs per unit: H ngran x tiles x HKB x 2, V row blocks x tiles x VKB x 4
+            const int tiles = p.ct * np;
+            const int64_t cost = (int64_t)ngran * tiles * p.r.hkb * 2 + (int64_t)nrb * tiles * p.r.vkb * 4;
+            units.push_back({w, cost});
+        }
+    }
+    // heaviest units first: the dispatcher starts them first, which shortens a frame's tail
+    std::stable_sort(units.begin(), units.end(), [](const Cost &a, const Cost &b) { return a.cost > b.cost; });
+    for (const Cost &c : units) out.units.push_back(c.u);
+    return !out.units.empty();
+}
+
+} // namespace dts

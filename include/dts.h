@@ -177,7 +177,10 @@ typedef struct dts_graph_info {
                                            ladder kernel (the rest on v3; DTS_LADDER=3 forces v3) */
     int32_t h_pairs4[DTS_MAX_OUTPUTS][2]; /* v4 H tap pairs per output (luma, chroma), 0 = v3 */
     int32_t ladder_v5;                  /* 1: the whole graph runs on the v5 ladder kernel (H on the
-                                           matrix cores; DTS_LADDER=4 / 3 force v4 / v3) */
+                                           matrix cores); 2: on the v6 kernel (H and V on the matrix
+                                           cores, H outputs in registers; v5 for frames whose planes
+                                           are not 4-byte aligned).  DTS_LADDER=5 / 4 / 3 force
+                                           v5 / v4 / v3 */
     int32_t v5_strip_width[2];          /* v5 source columns per strip (luma, chroma) */
     int32_t v5_strips[2];               /* v5 strips per plane kind */
 } dts_graph_info;

@@ -126,8 +126,9 @@ def test_plan_bench_ladder_runs_on_v4(fmt, monkeypatch):
 def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
     """8-bit sources with 8-bit outputs (cfg1, cfg2, cfg4 and upscales) plan the whole
     graph onto the v5 (matrix-core) ladder: every strip's H entries fit the waves and
-    its LDS fits one workgroup per CU.  p010 sources and HDR graphs stay on v4 / v3."""
-    monkeypatch.delenv("DTS_LADDER", raising=False)
+    its LDS fits one workgroup per CU.  p010 sources and HDR graphs stay on v4 / v3.
+    Planar sources go on to v6 (ladder_v5 == 2), nv12 sources stay on v5."""
+    monkeypatch.setenv("DTS_LADDER", "5")
     for sw, sh, outs in [(3840, 2160, LADDER4K), (7680, 4320, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)]),
                          (1920, 1080, [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]),
                          (640, 360, [(1280, 720, D.FMT_NV12, D.SCALE_BICUBIC), (320, 180, D.FMT_NV12, D.SCALE_AREA)])]:
@@ -135,8 +136,25 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
         assert info.ladder_v5 == 1 and info.ladder_v4_mask == 0
         assert info.lds_bytes <= 160 * 1024 and min(info.v5_strips) >= 1
     assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, LADDER4K)).ladder_v5 == 0
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    want = 2 if fmt == D.FMT_YUV420P else 1
+    assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == want
+    assert D.graph_plan(D.make_spec(7680, 4320, fmt, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)])).ladder_v5 == want
     monkeypatch.setenv("DTS_LADDER", "4")
     assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == 0
+
+
+def test_plan_v6_units(monkeypatch):
+    """cfg2 on v6: one work unit per (plane kind, rendition, column group) of a frame;
+    a tile whose taps span more than two 64-column K blocks keeps the graph on v5."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
+    assert info.ladder_v5 == 2
+    # luma: 1080p 30 x 64 columns, 720p 40 x 32 (two V K blocks), 480p 27 x 32 (two H and V K blocks);
+    # chroma (U and V per unit): 1080p 30 x 32, 720p 40 x 16, 480p 27 x 16
+    assert info.njobs == 30 + 40 + 27 + 30 + 40 + 27
+    # 8K -> 480p bicubic: 36 taps, 16 outputs span 180 source columns: v5 cannot either
+    assert D.graph_plan(D.make_spec(7680, 4320, D.FMT_YUV420P, [(854, 480, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 < 2
 
 
 def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
