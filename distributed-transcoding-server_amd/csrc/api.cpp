@@ -180,7 +180,7 @@ struct dts_graph {
     const Unit6 *dev_units6 = nullptr;
     const uint32_t *dev_frag6 = nullptr;
     const int32_t *dev_fire6 = nullptr;
-    int nunits6 = 0;
+    int nunits6 = 0, lds6 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -625,7 +625,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     if (s.quality) algo += in.out_frame_bytes[s.quality_out];
     in.algo_bytes_per_frame = algo;
     in.njobs = gp.v6 ? (int)gp.p6.units.size() : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
-    in.lds_bytes = std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
+    in.lds_bytes = gp.v6 ? gp.p6.lds_bytes : std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
     in.ladder_v4_mask = (int32_t)gp.v4_mask;
     in.ladder_v5 = gp.v6 ? 2 : (gp.v5 ? 1 : 0);
     for (int kind = 0; kind < 2; ++kind) {
@@ -909,6 +909,7 @@ static int upload_v6(dts_graph *g, const GraphPlan &gp)
     g->dev_frag6 = reinterpret_cast<const uint32_t *>(base + f_off);
     g->dev_fire6 = reinterpret_cast<const int32_t *>(base + r_off);
     g->nunits6 = (int)gp.p6.units.size();
+    g->lds6 = gp.p6.lds_bytes;
     g->v6 = true;
     return DTS_OK;
 }
@@ -1226,7 +1227,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.fire = g->dev_fire6;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->nunits6;
             if (grid > INT32_MAX) return DTS_E_RANGE;
-            HIPCHK(ctx, launch_ladder6(q, (int)grid, st));
+            HIPCHK(ctx, launch_ladder6(q, (int)grid, g->lds6, st));
             continue;
         }
         if (g->v5) {

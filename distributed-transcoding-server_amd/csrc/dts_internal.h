@@ -247,6 +247,7 @@ int ladder5_blocks_per_cu(int src_kind, int lds_bytes);
 // no barrier and no ring traffic.
 // ---------------------------------------------------------------------------
 constexpr int kL6Gran = 16;         // source rows per granule (the H MFMA's M)
+constexpr int kL6Stages = 2;        // source granules in flight per wave (LDS stages; ladder6.hip DTS_L6_NS <= this)
 constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, V K blocks), ladder6.hip
 
 // variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns
@@ -274,7 +275,8 @@ struct Unit6 {                      // one wave's share of a frame
     int32_t dstW;
     int32_t x0[4];                  // first source column of each column tile's H K blocks (multiple of 4,
                                     // except a right-edge tile ending at the plane's last column)
-    int32_t pad_[2];
+    int32_t fs;                     // V fragment slots in LDS: most row blocks firing within kL6Stages granules
+    int32_t pad_;
 };
 
 struct Ladder6Params {
@@ -286,7 +288,9 @@ struct Ladder6Params {
     const int32_t *fire;
 };
 
-hipError_t launch_ladder6(const Ladder6Params &p, int grid, hipStream_t s);
+hipError_t launch_ladder6(const Ladder6Params &p, int grid, int lds_bytes, hipStream_t s);
+// LDS per wave of a unit: its source stages and its V fragment slots
+int ladder6_lds_bytes(const Unit6 &u);
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

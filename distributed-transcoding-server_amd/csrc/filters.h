@@ -111,6 +111,7 @@ struct Plan6 {
     std::vector<Unit6> units;
     std::vector<uint32_t> frag;      // fragment pairs, 512 dwords each
     std::vector<int32_t> fire;
+    int lds_bytes = 0;               // dynamic LDS of the launch (the largest unit's)
 };
 
 // kinds[0] luma, kinds[1] chroma (Plan5In: same inputs as v5).  false: the graph

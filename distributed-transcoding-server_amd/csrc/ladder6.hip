@@ -30,6 +30,17 @@
 //    consecutive bytes of its row (nv12: U and V interleaved by v_perm).
 #include "dts_internal.h"
 
+#ifndef DTS_L6_NS
+#define DTS_L6_NS 2         // LDS stages per wave: source granules in flight (DMA'd NS granules ahead)
+#endif
+#ifndef DTS_L6_ABLATE
+#define DTS_L6_ABLATE 0     // diagnostic builds only: 1 skip the source loads, 2 skip the V blocks,
+                            // 4 skip the V stores
+#endif
+#ifndef DTS_L6_WPE
+#define DTS_L6_WPE 0        // > 0: ask the compiler for at least this many waves per SIMD
+#endif
+
 namespace dts {
 
 namespace {
@@ -152,6 +163,11 @@ __device__ __forceinline__ void vblock(const Unit6 &U, int j, const v4i (&rh)[Wa
     uint32_t w[W::T];
 #pragma unroll
     for (int t = 0; t < W::T; ++t) w[t] = vcombine6(hh[t], hl[t], ll[t]);
+    if (DTS_L6_ABLATE & 4) {
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) asm volatile("" ::"v"(w[t]));
+        return;
+    }
     const int y = 16 * j + m;
     if (y >= U.dstH) return;
     if (W::NP == 1) {                                      // luma
@@ -191,6 +207,33 @@ __device__ __forceinline__ void vblock(const Unit6 &U, int j, const v4i (&rh)[Wa
                 put_row6<4>(rowp, at, U.dstW - at, o);
             }
         }
+    }
+}
+
+// s_waitcnt vmcnt(N) through the builtin, so the compiler's own wait insertion sees it
+// (it does not order the LDS-DMA writes with the ds_reads of the same LDS)
+template <int N>
+__device__ __forceinline__ void vm_wait6()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// ring slot s <- this granule's (hi, lo) dwords of every tile (s wave-uniform)
+template <int S, int R, int T>
+__device__ __forceinline__ void ring_put(v4i (&rh)[R / 4][T], v4i (&rl)[R / 4][T], int s, const uint32_t (&hi)[T],
+                                         const uint32_t (&lo)[T])
+{
+    if constexpr (S < R) {
+        if (s == S) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                rh[S / 4][t][S % 4] = (int)hi[t];
+                rl[S / 4][t][S % 4] = (int)lo[t];
+            }
+            return;
+        }
+        ring_put<S + 1, R, T>(rh, rl, s, hi, lo);
     }
 }
 
@@ -235,20 +278,12 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
             bh[c][kb] = *GP6(g_cv4i, o);
             bl[c][kb] = *GP6(g_cv4i, o + 1024);
         }
-    uint32_t xo[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) xo[c] = (uint32_t)U.x0[c] + 16u * (uint32_t)g;
-    // V: the next row block, its fire granule and B operands
+    // V: the next row block to run and its fire granule; the next one whose fragments are
+    // to be DMA'd and its fire granule
     k_u32 *fire = GP6(k_u32, P.fire + U.fire);
-    int j = 0;
-    int fg = U.nrb > 0 ? (int)fire[0] : 0x7fffffff;
+    int j = 0, jf = 0;
+    int fg = U.nrb > 0 ? (int)fire[0] : 0x7fffffff, fgf = fg;
     v4i vh[VKB], vl[VKB];
-#pragma unroll
-    for (int kb = 0; kb < VKB; ++kb) {
-        const uint64_t o = fr + (uint64_t)(U.vfrag + (uint32_t)kb) * 2048u;
-        vh[kb] = *GP6(g_cv4i, o);
-        vl[kb] = *GP6(g_cv4i, o + 1024);
-    }
     const v4i zero = {0, 0, 0, 0}, hbias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
     // the ring: slot s of tile t is dword s % 4 of rh[s / 4][t] (hi bytes) and rl (lo bytes)
     v4i rh[VKB][T], rl[VKB][T];
@@ -256,34 +291,76 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
     for (int kb = 0; kb < VKB; ++kb)
 #pragma unroll
         for (int t = 0; t < T; ++t) rh[kb][t] = rl[kb][t] = zero;
-    // the walk covers whole ring periods: granules past the plane (rows clamped to its
-    // last row) are computed and never used, so the unrolled body has no exits
-    const int ngran = (U.ngran + R - 1) / R * R, srcH1 = U.srcH - 1;
-    // A operands of the next granule (one granule of prefetch)
-    v4i an[T][HKB];
-    auto aload = [&](int q) {
-        const uint32_t row = (uint32_t)min(kL6Gran * q + m, srcH1);
+    const int ngran = U.ngran, srcH1 = U.srcH - 1;
+    // A operands: the 16 rows x 64 bytes of every (plane, tile, K block) reach this wave's
+    // LDS by LDS-DMA, NS granules ahead (stage q % NS).  DMA lane l loads row l >> 2, chunk
+    // (l & 3) ^ ((l >> 4) & 3) of the 64 bytes: four lanes cover one row's 64 contiguous
+    // bytes (one cache access instead of four), and the A read of lane (m, g) -- row m,
+    // chunk g -- is a conflict-free ds_read_b128 at 16 (4 m + (g ^ ((m >> 2) & 3))).
+    constexpr int NS = DTS_L6_NS, ND = T * HKB;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
+    const int dr = lane >> 2, dch = (lane & 3) ^ ((dr >> 2) & 3);
+    uint32_t dcol[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) dcol[c] = (uint32_t)U.x0[c] + 16u * (uint32_t)dch;
+    const uint32_t roff = 16u * (uint32_t)(4 * m + (g ^ ((m >> 2) & 3)));
+    // V fragment slots after the stages: row block j's fragments in slot j % fs, DMA'd right
+    // after the source of its fire granule, so the source wait covers them too
+    uint8_t *fb = lds6 + NS * ND * 1024;
+    const int FS = U.fs;
+    int fsi = 0, fsu = 0;
+    auto frags = [&](int upto) {
+        while (fgf <= upto) {
+            uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
+            const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
+#pragma unroll
+            for (int h = 0; h < 2 * VKB; ++h)
+                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
+                                                 (__attribute__((address_space(3))) void *)(dst + 1024 * h), 16, 0, 0);
+            fsi = fsi + 1 == FS ? 0 : fsi + 1;
+            ++jf;
+            fgf = jf < U.nrb ? (int)fire[jf] : 0x7fffffff;
+        }
+    };
+    auto dma = [&](int q) {
+        if (DTS_L6_ABLATE & 1) {
+            frags(q);
+            return;
+        }
+        const uint32_t row = (uint32_t)min(kL6Gran * q + dr, srcH1);
+        uint8_t *st = lds6 + (uint32_t)(q % NS) * (uint32_t)(ND * 1024);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             const uint64_t rp = sb[p] + (uint64_t)(row * sp[p]);
 #pragma unroll
             for (int c = 0; c < CT; ++c)
 #pragma unroll
-                for (int kb = 0; kb < HKB; ++kb) an[p * CT + c][kb] = *GP6(g_cv4i, rp + xo[c] + 64u * kb);
+                for (int kb = 0; kb < HKB; ++kb)
+                    __builtin_amdgcn_global_load_lds(
+                        (const void *)(uintptr_t)(rp + dcol[c] + 64u * kb),
+                        (__attribute__((address_space(3))) void *)(st + 1024 * ((p * CT + c) * HKB + kb)), 16, 0, 0);
         }
+        frags(q);
     };
-    aload(0);
-    for (int q0 = 0; q0 < ngran; q0 += R) {
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int q = q0 + s;
+    for (int i = 0; i < NS - 1; ++i) dma(i);
+    int s = 0;                                             // ring slot of granule q
+    for (int q = 0; q < ngran; ++q) {
+        {
+            // granule q + NS - 1 into the stage granule q - 1 was read from (its ds_reads
+            // completed before its MFMAs); past the plane: clamped rows, unused, which keeps
+            // the count uniform
+            dma(q + NS - 1);
+            // granule q's DMAs have landed: only the (NS - 1) ND DMAs issued after them may
+            // be outstanding (younger V stores / fragment loads only make this wait longer)
+            vm_wait6<(NS - 1) * ND>();
+            const uint8_t *st = lds6 + (uint32_t)(q % NS) * (uint32_t)(ND * 1024) + roff;
             v4i a[T][HKB];
 #pragma unroll
             for (int t = 0; t < T; ++t)
 #pragma unroll
-                for (int kb = 0; kb < HKB; ++kb) a[t][kb] = an[t][kb] ^ (int)0x80808080u;
-            aload(q + 1);                                  // (past the end: clamped rows, unused)
-            // H of granule q -> ring slot s
+                for (int kb = 0; kb < HKB; ++kb)
+                    a[t][kb] = *reinterpret_cast<const v4i *>(st + 1024 * (t * HKB + kb)) ^ (int)0x80808080u;
             v4i ah[T], al[T];
 #pragma unroll
             for (int t = 0; t < T; ++t) {
@@ -297,34 +374,49 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
                     ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
                     al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
                 }
+            uint32_t hi[T], lo[T];
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
                 const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
-                rh[s / 4][t][s % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                rl[s / 4][t][s % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                hi[t] = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                lo[t] = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
             }
-            // the row blocks whose window this granule completes
-            while (fg == q) {
-                vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g);
-                ++j;
-                if (j < U.nrb) {
-                    fg = (int)fire[j];
+            ring_put<0, R, T>(rh, rl, s, hi, lo);
+            s = s + 1 == R ? 0 : s + 1;
+        }
+        while (fg == q) {
+            {
+                const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
 #pragma unroll
-                    for (int kb = 0; kb < VKB; ++kb) {
-                        const uint64_t o = fr + (uint64_t)(U.vfrag + (uint32_t)(j * VKB + kb)) * 2048u;
-                        vh[kb] = *GP6(g_cv4i, o);
-                        vl[kb] = *GP6(g_cv4i, o + 1024);
-                    }
-                } else {
-                    fg = 0x7fffffff;
+                for (int kb = 0; kb < VKB; ++kb) {
+                    vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
+                    vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
                 }
+                fsu = fsu + 1 == FS ? 0 : fsu + 1;
             }
+            if (!(DTS_L6_ABLATE & 2)) {
+                vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g);
+            } else {
+#pragma unroll
+                for (int kb = 0; kb < VKB; ++kb)
+#pragma unroll
+                    for (int t = 0; t < T; ++t) asm volatile("" ::"v"(rh[kb][t]), "v"(rl[kb][t]), "v"(vh[kb]), "v"(vl[kb]));
+            }
+            ++j;
+            fg = j < U.nrb ? (int)fire[j] : 0x7fffffff;
         }
     }
+    // the DMAs past the plane still write this workgroup's LDS: drain them before the
+    // wave (and its LDS allocation) ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(64) void k_ladder6(Ladder6Params P)
+__global__ __launch_bounds__(64)
+#if DTS_L6_WPE > 0
+__attribute__((amdgpu_waves_per_eu(DTS_L6_WPE)))
+#endif
+void k_ladder6(Ladder6Params P)
 {
     // workgroup b: XCD b % 8; frame 8 (k / nunits) + b % 8, unit k % nunits (k = b / 8)
     const int b = (int)blockIdx.x, k = b >> 3;
@@ -346,9 +438,17 @@ __global__ __launch_bounds__(64) void k_ladder6(Ladder6Params P)
 
 } // namespace
 
-hipError_t launch_ladder6(const Ladder6Params &p, int grid, hipStream_t s)
+static_assert(DTS_L6_NS <= kL6Stages, "the planner sizes the fragment slots for kL6Stages granules");
+
+int ladder6_lds_bytes(const Unit6 &u)
 {
-    hipLaunchKernelGGL(k_ladder6, dim3(grid), dim3(64), 0, s, p);
+    const int v = u.variant;
+    return DTS_L6_NS * l6_ct(v) * l6_np(v) * l6_hkb(v) * 1024 + u.fs * l6_vkb(v) * 2048;
+}
+
+hipError_t launch_ladder6(const Ladder6Params &p, int grid, int lds_bytes, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ladder6, dim3(grid), dim3(64), lds_bytes, s, p);
     return hipGetLastError();
 }
 

@@ -225,6 +225,13 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
         }
         const int ngran = (in.srcH + kL6Gran - 1) / kL6Gran;
         const int nrb = (int)p.r.fire.size();
+        // V fragment slots: the fragments of the row blocks firing in granules q .. q + kL6Stages - 1
+        // are in LDS together (each is DMA'd with the source of its fire granule)
+        int fs = 1;
+        for (int a = 0, z = 0; a < nrb; ++a) {
+            while (z < nrb && p.r.fire[z] < p.r.fire[a] + kL6Stages) ++z;
+            fs = std::max(fs, z - a);
+        }
         for (int u = 0; u * p.ct < ntp; ++u) {
             Unit6 w{};
             w.variant = var;
@@ -242,6 +249,8 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
             w.vfrag = p.vfrag;
             w.fire = p.fire;
             for (int c = 0; c < 4; ++c) w.x0[c] = c < p.ct ? p.r.x0[(size_t)u * p.ct + c] : 0;
+            w.fs = fs;
+            out.lds_bytes = std::max(out.lds_bytes, ladder6_lds_bytes(w));
             // MFMAs per unit: H ngran x tiles x HKB x 2, V row blocks x tiles x VKB x 4
             const int tiles = p.ct * np;
             const int64_t cost = (int64_t)ngran * tiles * p.r.hkb * 2 + (int64_t)nrb * tiles * p.r.vkb * 4;
