@@ -24,6 +24,9 @@ using namespace dts;
 #ifdef DTS_L5_STAMP
 namespace dts { int ladder5_stamps(unsigned long long *out, bool reset); }
 #endif
+#ifdef DTS_L6_STAMP
+namespace dts { int ladder6_stamps(unsigned long long *out, bool reset); }
+#endif
 
 // Quality partials (per-tile SSE / SSIM sums) of one k_quality -> k_qreduce
 // pair.  `ev` marks the last launch that used the buffer: the next user waits
@@ -1777,6 +1780,11 @@ int dts_synth_device(dts_ctx *ctx, int w, int h, int fmt, int pattern, uint32_t 
 #ifdef DTS_L5_STAMP
 // diagnostic builds only (tools/build_stamp5.sh): per-phase cycle sums of k_ladder5
 int dts_debug_ladder5_stamps(unsigned long long *out, int reset) { return dts::ladder5_stamps(out, reset != 0); }
+#endif
+
+#ifdef DTS_L6_STAMP
+// diagnostic builds only (tools/build_stamp6.sh): per-variant, per-phase cycle sums of k_ladder6
+int dts_debug_ladder6_stamps(unsigned long long *out, int reset) { return dts::ladder6_stamps(out, reset != 0); }
 #endif
 
 // vf_fps.c (FFmpeg 4.4) frame selection, round=near, constant-rate input

@@ -247,7 +247,7 @@ int ladder5_blocks_per_cu(int src_kind, int lds_bytes);
 // no barrier and no ring traffic.
 // ---------------------------------------------------------------------------
 constexpr int kL6Gran = 16;         // source rows per granule (the H MFMA's M)
-constexpr int kL6Stages = 2;        // source granules in flight per wave (LDS stages; ladder6.hip DTS_L6_NS <= this)
+constexpr int kL6Stages = 4;        // source granules in flight per wave (LDS stages; ladder6.hip DTS_L6_NS <= this)
 constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, V K blocks), ladder6.hip
 
 // variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns

@@ -34,14 +34,35 @@
 #define DTS_L6_NS 2         // LDS stages per wave: source granules in flight (DMA'd NS granules ahead)
 #endif
 #ifndef DTS_L6_ABLATE
-#define DTS_L6_ABLATE 0     // diagnostic builds only: 1 skip the source loads, 2 skip the V blocks,
+#define DTS_L6_ABLATE 0     // diagnostic builds only: 1 skip the source loads, 2 skip the V blocks, 8 load
+                            // one (tile, K block) of source per granule and feed it to every tile,
                             // 4 skip the V stores
+#endif
+#ifndef DTS_L6_LDSPAD
+#define DTS_L6_LDSPAD 0     // diagnostic builds only: extra LDS per wave (fewer waves per CU)
 #endif
 #ifndef DTS_L6_WPE
 #define DTS_L6_WPE 0        // > 0: ask the compiler for at least this many waves per SIMD
 #endif
 
+#ifndef DTS_L6_STAMP
+#define DTS_L6_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp6.py)
+#endif
+
 namespace dts {
+
+#if DTS_L6_STAMP
+// [variant][phase]: cycles summed over every wave; [variant][6]: granules, [variant][7]: waves
+__device__ unsigned long long g_l6_stamp[kL6Variants][8];
+#define L6_STAMP(k)                                                        \
+    do {                                                                   \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
+        st_acc[k] += t_ - st_last;                                         \
+        st_last = t_;                                                      \
+    } while (0)
+#else
+#define L6_STAMP(k) (void)0
+#endif
 
 namespace {
 
@@ -73,17 +94,6 @@ __device__ __forceinline__ uint32_t pack_h6(int hi, int lo, int hi2, int lo2)
 {
     const int a = ((hi << 8) + lo) >> 7, b = ((hi2 << 8) + lo2) >> 7;
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(a, b));
-}
-
-// av_clip_uint8((65536 hh + 256 (hl + lh) + ll + bias) >> 19) of 4 columns, packed
-__device__ __forceinline__ uint32_t vcombine6(const v4i &hh, const v4i &hl, const v4i &ll)
-{
-    int v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (((hh[i] << 8) + hl[i]) << 8) + ll[i];
-    const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(v[0], v[1], 19);
-    const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(v[2], v[3], 19);
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 // NB bytes (4, 8, 16) at byte `at` of an output row with `room` bytes left from `at`
@@ -128,6 +138,40 @@ __device__ __forceinline__ void transpose2(uint32_t a, uint32_t b, uint32_t (&o)
     o[1] = x[1];
 }
 
+// Stores of one row block: lane (m, g) holds NB bytes of output row y0 + m at byte
+// at0 + NB g.  Through a 1-KB LDS scratch they move to lane 4 m + g, so four consecutive
+// lanes hold one row's 4 NB contiguous bytes (one cache access per row segment instead
+// of one per lane), then the store of rows < dstH, bytes < rowbytes.
+template <int NB>
+__device__ __forceinline__ void put6(uint8_t *scr, uint64_t base, uint32_t pitch, int y0, int dstH, int at0,
+                                     int rowbytes, const uint32_t (&w)[NB / 4], int m, int g, int lane)
+{
+    // the exchange needs every lane: the stores of a previous call (some lanes skip
+    // them) are done before this write (a convergent point)
+    __builtin_amdgcn_wave_barrier();
+    uint32_t v[NB / 4];
+    if (NB == 16) {
+        *reinterpret_cast<u32x4 *>(scr + 16 * (4 * m + g)) = (u32x4){w[0], w[1 % (NB / 4)], w[2 % (NB / 4)], w[3 % (NB / 4)]};
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(scr + 16 * lane);
+        v[0] = x.x;
+        v[1 % (NB / 4)] = x.y;
+        v[2 % (NB / 4)] = x.z;
+        v[3 % (NB / 4)] = x.w;
+    } else if (NB == 8) {
+        *reinterpret_cast<u32x2 *>(scr + 8 * (4 * m + g)) = (u32x2){w[0], w[1 % (NB / 4)]};
+        const u32x2 x = *reinterpret_cast<const u32x2 *>(scr + 8 * lane);
+        v[0] = x.x;
+        v[1 % (NB / 4)] = x.y;
+    } else {
+        *reinterpret_cast<uint32_t *>(scr + 4 * (4 * m + g)) = w[0];
+        v[0] = *reinterpret_cast<const uint32_t *>(scr + 4 * lane);
+    }
+    const int y = y0 + (lane >> 2);
+    const int at = at0 + NB * (lane & 3);
+    if (y < dstH) put_row6<NB>(base + (uint64_t)y * pitch, at, rowbytes - at, v);
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int VAR>
 struct Walk6 {
     static constexpr int CT = l6_ct(VAR), NP = l6_np(VAR), HKB = l6_hkb(VAR), VKB = l6_vkb(VAR);
@@ -136,78 +180,103 @@ struct Walk6 {
 
 // one row block: V over the whole ring, then the stores of output row 16 j + m
 template <int VAR>
-__device__ __forceinline__ void vblock(const Unit6 &U, int j, const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+__device__ __forceinline__ int vblock(const Unit6 &U, int j, const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
                                        const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
                                        const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
-                                       const uint64_t (&ob)[2], const uint32_t (&op)[2], int m, int g)
+                                       const uint64_t (&ob)[2], const uint32_t (&op)[2], int m, int g,
+                                       uint8_t *scr)
 {
     using W = Walk6<VAR>;
-    const v4i zero = {0, 0, 0, 0}, vbias = {kL5VBias, kL5VBias, kL5VBias, kL5VBias};
-    v4i hh[W::T], hl[W::T], ll[W::T];
+    // 65536 hh + 256 (hl + lh) + ll + bias as three chained accumulations: the hh chain
+    // starts at bias >> 16 (the bias is 12 << 16), each next chain starts at the previous
+    // one << 8 -- two shifts per value instead of a three-term combine
+    static_assert(kL5VBias == 12 << 16, "V bias folded into the hh chain");
+    const v4i vb = {12, 12, 12, 12};
+    v4i acc[W::T];
 #pragma unroll
-    for (int t = 0; t < W::T; ++t) {
-        hh[t] = zero;
-        hl[t] = zero;
-        ll[t] = vbias;
-    }
+    for (int t = 0; t < W::T; ++t) acc[t] = vb;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vh[kb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] <<= 8;
 #pragma unroll
     for (int kb = 0; kb < W::VKB; ++kb)
 #pragma unroll
         for (int t = 0; t < W::T; ++t) {
-            const v4i ah = rh[kb][t], al = rl[kb][t];
-            hh[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, vh[kb], hh[t], 0, 0, 0);
-            hl[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, vl[kb], hl[t], 0, 0, 0);
-            ll[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, vl[kb], ll[t], 0, 0, 0);
-            hl[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, vh[kb], hl[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vl[kb], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vh[kb], acc[t], 0, 0, 0);
         }
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] <<= 8;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vl[kb], acc[t], 0, 0, 0);
     uint32_t w[W::T];
 #pragma unroll
-    for (int t = 0; t < W::T; ++t) w[t] = vcombine6(hh[t], hl[t], ll[t]);
+    for (int t = 0; t < W::T; ++t) {
+        // av_clip_uint8(val >> 19) of 4 columns, packed
+        const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][0], acc[t][1], 19);
+        const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][2], acc[t][3], 19);
+        w[t] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+    }
     if (DTS_L6_ABLATE & 4) {
 #pragma unroll
         for (int t = 0; t < W::T; ++t) asm volatile("" ::"v"(w[t]));
-        return;
+        return 0;
     }
-    const int y = 16 * j + m;
-    if (y >= U.dstH) return;
+    const int y0 = 16 * j, lane = 16 * g + m;
     if (W::NP == 1) {                                      // luma
-        const uint64_t rowp = ob[0] + (uint64_t)y * op[0];
         if (W::CT == 4) {
             uint32_t o[4];
             transpose4(w[0], w[1 % W::T], w[2 % W::T], w[3 % W::T], o);
-            const int at = U.col0 + 16 * g;
-            put_row6<16>(rowp, at, U.dstW - at, o);
+            put6<16>(scr, ob[0], op[0], y0, U.dstH, U.col0, U.dstW, o, m, g, lane);
         } else {
             uint32_t o[2];
             transpose2(w[0], w[1 % W::T], o);
-            const int at = U.col0 + 8 * g;
-            put_row6<8>(rowp, at, U.dstW - at, o);
+            put6<8>(scr, ob[0], op[0], y0, U.dstH, U.col0, U.dstW, o, m, g, lane);
         }
     } else if (U.fmt == DTS_FMT_NV12) {                    // chroma, U V interleaved
-        const uint64_t rowp = ob[0] + (uint64_t)y * op[0];
 #pragma unroll
         for (int c = 0; c < W::CT; ++c) {
             const uint32_t u = w[c], v = w[W::CT + c];
             const uint32_t o[2] = {__builtin_amdgcn_perm(v, u, 0x05010400u), __builtin_amdgcn_perm(v, u, 0x07030602u)};
-            const int at = 2 * U.col0 + 32 * c + 8 * g;
-            put_row6<8>(rowp, at, 2 * U.dstW - at, o);
+            put6<8>(scr, ob[0], op[0], y0, U.dstH, 2 * U.col0 + 32 * c, 2 * U.dstW, o, m, g, lane);
         }
     } else {                                               // chroma, U and V planes
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            const uint64_t rowp = ob[p] + (uint64_t)y * op[p];
             if (W::CT == 2) {
                 uint32_t o[2];
                 transpose2(w[2 * p], w[(2 * p + 1) % W::T], o);
-                const int at = U.col0 + 8 * g;
-                put_row6<8>(rowp, at, U.dstW - at, o);
+                put6<8>(scr, ob[p], op[p], y0, U.dstH, U.col0, U.dstW, o, m, g, lane);
             } else {
                 const uint32_t o[1] = {w[p % W::T]};
-                const int at = U.col0 + 4 * g;
-                put_row6<4>(rowp, at, U.dstW - at, o);
+                put6<4>(scr, ob[p], op[p], y0, U.dstH, U.col0, U.dstW, o, m, g, lane);
             }
         }
     }
+    // store instructions issued (one per put6; edge units' byte stores are not counted,
+    // which only makes the next source wait longer)
+    return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? W::CT : 2);
+}
+
+// s_waitcnt vmcnt(min(n, LO + 15)) for a run-time n >= LO (a switch of 16 immediates):
+// waiting for fewer outstanding instructions than were issued is never too short
+template <int LO>
+__device__ __forceinline__ void vm_wait_n6(int n)
+{
+    static_assert(LO >= 0 && LO + 15 < 64, "vmcnt is 6 bits");
+#define DTS_W6(k) \
+    case k: __builtin_amdgcn_s_waitcnt(((LO + k) & 15) | (7 << 4) | (15 << 8) | (((LO + k) >> 4) << 14)); break;
+    switch (min(max(n - LO, 0), 15)) {
+        DTS_W6(0) DTS_W6(1) DTS_W6(2) DTS_W6(3) DTS_W6(4) DTS_W6(5) DTS_W6(6) DTS_W6(7)
+        DTS_W6(8) DTS_W6(9) DTS_W6(10) DTS_W6(11) DTS_W6(12) DTS_W6(13) DTS_W6(14)
+    default: DTS_W6(15)
+    }
+#undef DTS_W6
 }
 
 // s_waitcnt vmcnt(N) through the builtin, so the compiler's own wait insertion sees it
@@ -217,24 +286,6 @@ __device__ __forceinline__ void vm_wait6()
 {
     static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-// ring slot s <- this granule's (hi, lo) dwords of every tile (s wave-uniform)
-template <int S, int R, int T>
-__device__ __forceinline__ void ring_put(v4i (&rh)[R / 4][T], v4i (&rl)[R / 4][T], int s, const uint32_t (&hi)[T],
-                                         const uint32_t (&lo)[T])
-{
-    if constexpr (S < R) {
-        if (s == S) {
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                rh[S / 4][t][S % 4] = (int)hi[t];
-                rl[S / 4][t][S % 4] = (int)lo[t];
-            }
-            return;
-        }
-        ring_put<S + 1, R, T>(rh, rl, s, hi, lo);
-    }
 }
 
 template <int VAR>
@@ -292,6 +343,10 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
 #pragma unroll
         for (int t = 0; t < T; ++t) rh[kb][t] = rl[kb][t] = zero;
     const int ngran = U.ngran, srcH1 = U.srcH - 1;
+#if DTS_L6_STAMP
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
     // A operands: the 16 rows x 64 bytes of every (plane, tile, K block) reach this wave's
     // LDS by LDS-DMA, NS granules ahead (stage q % NS).  DMA lane l loads row l >> 2, chunk
     // (l & 3) ^ ((l >> 4) & 3) of the 64 bytes: four lanes cover one row's 64 contiguous
@@ -309,8 +364,11 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
     uint8_t *fb = lds6 + NS * ND * 1024;
     const int FS = U.fs;
     int fsi = 0, fsu = 0;
+    int ops = 0;                                           // VMEM instructions issued so far
+    int oend[NS];                                          // ops after the batch of granule q (slot q % NS)
     auto frags = [&](int upto) {
         while (fgf <= upto) {
+            ops += 2 * VKB;
             uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
             const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
 #pragma unroll
@@ -322,11 +380,10 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
             fgf = jf < U.nrb ? (int)fire[jf] : 0x7fffffff;
         }
     };
+    // one batch: the fragments of the row blocks firing at granule q, then granule q's source
     auto dma = [&](int q) {
-        if (DTS_L6_ABLATE & 1) {
-            frags(q);
-            return;
-        }
+        frags(q);
+        if (DTS_L6_ABLATE & 1) return;
         const uint32_t row = (uint32_t)min(kL6Gran * q + dr, srcH1);
         uint8_t *st = lds6 + (uint32_t)(q % NS) * (uint32_t)(ND * 1024);
 #pragma unroll
@@ -336,80 +393,107 @@ __device__ __forceinline__ void walk6(const Ladder6Params &P, const Unit6 &U, in
             for (int c = 0; c < CT; ++c)
 #pragma unroll
                 for (int kb = 0; kb < HKB; ++kb)
-                    __builtin_amdgcn_global_load_lds(
-                        (const void *)(uintptr_t)(rp + dcol[c] + 64u * kb),
-                        (__attribute__((address_space(3))) void *)(st + 1024 * ((p * CT + c) * HKB + kb)), 16, 0, 0);
+                    if (!(DTS_L6_ABLATE & 8) || (p * CT + c) * HKB + kb == 0)
+                    {
+                        __builtin_amdgcn_global_load_lds(
+                            (const void *)(uintptr_t)(rp + dcol[c] + 64u * kb),
+                            (__attribute__((address_space(3))) void *)(st + 1024 * ((p * CT + c) * HKB + kb)), 16, 0, 0);
+                        ++ops;
+                    }
         }
-        frags(q);
     };
 #pragma unroll
-    for (int i = 0; i < NS - 1; ++i) dma(i);
-    int s = 0;                                             // ring slot of granule q
-    for (int q = 0; q < ngran; ++q) {
-        {
+    for (int i = 0; i < NS - 1; ++i) {
+        dma(i);
+        oend[i] = ops;
+    }
+    // the walk is unrolled by the ring length, so ring slot q % R and stage q % NS are
+    // fixed registers / offsets in each copy; granules past the plane (to a whole ring
+    // period) are computed and never used
+    static_assert(R % NS == 0, "the stages cycle within a ring period");
+    const int ngp = (ngran + R - 1) / R * R;
+    for (int q0 = 0; q0 < ngp; q0 += R) {
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const int q = q0 + s;
             // granule q + NS - 1 into the stage granule q - 1 was read from (its ds_reads
             // completed before its MFMAs); past the plane: clamped rows, unused, which keeps
             // the count uniform
+            L6_STAMP(4);
             dma(q + NS - 1);
-            // granule q's DMAs have landed: only the (NS - 1) ND DMAs issued after them may
-            // be outstanding (younger V stores / fragment loads only make this wait longer)
-            vm_wait6<(NS - 1) * ND>();
-            const uint8_t *st = lds6 + (uint32_t)(q % NS) * (uint32_t)(ND * 1024) + roff;
-            v4i a[T][HKB];
+            oend[(s + NS - 1) % NS] = ops;
+            L6_STAMP(0);
+            // granule q's batch (its source and the fragments of the row blocks firing at
+            // q) has landed: every VMEM instruction issued after it may still be in flight
+            vm_wait_n6<(NS - 1) * ((DTS_L6_ABLATE & (1 | 8)) ? (DTS_L6_ABLATE & 1 ? 0 : 1) : ND)>(ops - oend[s % NS]);
+            L6_STAMP(1);
+            {
+                const uint8_t *st = lds6 + (s % NS) * (ND * 1024) + roff;
+                v4i a[T][HKB];
 #pragma unroll
-            for (int t = 0; t < T; ++t)
+                for (int t = 0; t < T; ++t)
 #pragma unroll
-                for (int kb = 0; kb < HKB; ++kb)
-                    a[t][kb] = *reinterpret_cast<const v4i *>(st + 1024 * (t * HKB + kb)) ^ (int)0x80808080u;
-            v4i ah[T], al[T];
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                ah[t] = zero;
-                al[t] = hbias;
-            }
-#pragma unroll
-            for (int kb = 0; kb < HKB; ++kb)
+                    for (int kb = 0; kb < HKB; ++kb)
+                        a[t][kb] = *reinterpret_cast<const v4i *>(st + ((DTS_L6_ABLATE & 8) ? 0 : 1024 * (t * HKB + kb))) ^
+                                   (int)0x80808080u;
+                v4i ah[T], al[T];
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
-                    ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
-                    al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+                    ah[t] = zero;
+                    al[t] = hbias;
                 }
-            uint32_t hi[T], lo[T];
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
-                const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
-                hi[t] = __builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                lo[t] = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u;
-            }
-            ring_put<0, R, T>(rh, rl, s, hi, lo);
-            s = s + 1 == R ? 0 : s + 1;
-        }
-        while (fg == q) {
-            {
-                const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
+                for (int kb = 0; kb < HKB; ++kb)
 #pragma unroll
-                for (int kb = 0; kb < VKB; ++kb) {
-                    vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
-                    vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
+                    for (int t = 0; t < T; ++t) {
+                        ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
+                        al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
+                    const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
+                    rh[s / 4][t][s % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                    rl[s / 4][t][s % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                 }
-                fsu = fsu + 1 == FS ? 0 : fsu + 1;
             }
-            if (!(DTS_L6_ABLATE & 2)) {
-                vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g);
-            } else {
+            L6_STAMP(2);
+            while (fg == q) {
+                {
+                    const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
 #pragma unroll
-                for (int kb = 0; kb < VKB; ++kb)
+                    for (int kb = 0; kb < VKB; ++kb) {
+                        vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
+                        vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
+                    }
+                    fsu = fsu + 1 == FS ? 0 : fsu + 1;
+                }
+                if (!(DTS_L6_ABLATE & 2)) {
+                    ops += vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g, fb + FS * VKB * 2048);
+                } else {
 #pragma unroll
-                    for (int t = 0; t < T; ++t) asm volatile("" ::"v"(rh[kb][t]), "v"(rl[kb][t]), "v"(vh[kb]), "v"(vl[kb]));
+                    for (int kb = 0; kb < VKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t)
+                            asm volatile("" ::"v"(rh[kb][t]), "v"(rl[kb][t]), "v"(vh[kb]), "v"(vl[kb]));
+                }
+                ++j;
+                fg = j < U.nrb ? (int)fire[j] : 0x7fffffff;
+                L6_STAMP(3);
             }
-            ++j;
-            fg = j < U.nrb ? (int)fire[j] : 0x7fffffff;
         }
     }
     // the DMAs past the plane still write this workgroup's LDS: drain them before the
     // wave (and its LDS allocation) ends
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if DTS_L6_STAMP
+    L6_STAMP(5);
+    if (lane == 0) {
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_l6_stamp[VAR][k], st_acc[k]);
+        atomicAdd(&g_l6_stamp[VAR][6], (unsigned long long)ngp);
+        atomicAdd(&g_l6_stamp[VAR][7], 1ull);
+    }
+#endif
 }
 
 __global__ __launch_bounds__(64)
@@ -438,12 +522,25 @@ void k_ladder6(Ladder6Params P)
 
 } // namespace
 
+#if DTS_L6_STAMP
+int ladder6_stamps(unsigned long long *out, bool reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l6_stamp), sizeof(g_l6_stamp)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[kL6Variants * 8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_l6_stamp), z, sizeof z) != hipSuccess) return -1;
+    }
+    return kL6Variants * 8;
+}
+#endif
+
 static_assert(DTS_L6_NS <= kL6Stages, "the planner sizes the fragment slots for kL6Stages granules");
 
 int ladder6_lds_bytes(const Unit6 &u)
 {
     const int v = u.variant;
-    return DTS_L6_NS * l6_ct(v) * l6_np(v) * l6_hkb(v) * 1024 + u.fs * l6_vkb(v) * 2048;
+    return DTS_L6_NS * l6_ct(v) * l6_np(v) * l6_hkb(v) * 1024 + u.fs * l6_vkb(v) * 2048 + 1024 +   // + store scratch
+           DTS_L6_LDSPAD;
 }
 
 hipError_t launch_ladder6(const Ladder6Params &p, int grid, int lds_bytes, hipStream_t s)
