@@ -184,6 +184,15 @@ struct dts_graph {
     const uint32_t *dev_frag6 = nullptr;
     const int32_t *dev_fire6 = nullptr;
     int nunits6 = 0, lds6 = 0;
+    // v7 ladder (ladder7.hip): the v6 waves in strip groups; k_ladder6 / k_ladder5 run
+    // frames whose planes are not 16-byte aligned
+    bool v7 = false;
+    void *dev_tables7 = nullptr;
+    const Group7 *dev_groups7 = nullptr;
+    const Unit7 *dev_units7 = nullptr;
+    const uint32_t *dev_frag7 = nullptr;
+    const int32_t *dev_fire7 = nullptr;
+    int ngroups7 = 0, lds7 = 0, waves7 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -425,6 +434,8 @@ struct GraphPlan {
     int lds5 = 0;
     bool v6 = false;                      // ... and on k_ladder6 where frames are 4-byte aligned
     Plan6 p6;
+    bool v7 = false;                      // ... and on k_ladder7 where frames are 16-byte aligned
+    Plan7 p7;
     dts_graph_info info{};
 };
 
@@ -475,6 +486,21 @@ bool v6_enabled()
     return !(f && (f[0] == '3' || f[0] == '4' || f[0] == '5'));
 }
 
+// DTS_LADDER=6 / 5 / 4 / 3 keep the graph off the v7 kernel
+bool v7_enabled()
+{
+    const char *f = std::getenv("DTS_LADDER");
+    return !(f && (f[0] == '3' || f[0] == '4' || f[0] == '5' || f[0] == '6'));
+}
+
+// waves per k_ladder7 group (DTS_L7_W, 1..16; default 8: two groups of 8 waves per CU)
+int l7_waves()
+{
+    const char *f = std::getenv("DTS_L7_W");
+    const int w = f ? std::atoi(f) : 8;
+    return std::min(std::max(w, 1), kL7MaxWaves);
+}
+
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
 // and k_ladder6 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
@@ -503,6 +529,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
+    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), gp.p7);
     return true;
 }
 
@@ -627,10 +654,11 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     }
     if (s.quality) algo += in.out_frame_bytes[s.quality_out];
     in.algo_bytes_per_frame = algo;
-    in.njobs = gp.v6 ? (int)gp.p6.units.size() : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
-    in.lds_bytes = gp.v6 ? gp.p6.lds_bytes : std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
+    in.njobs = gp.v7 ? (int)gp.p7.groups.size()
+                     : gp.v6 ? (int)gp.p6.units.size() : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
+    in.lds_bytes = gp.v7 ? gp.p7.lds_bytes : gp.v6 ? gp.p6.lds_bytes : std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
     in.ladder_v4_mask = (int32_t)gp.v4_mask;
-    in.ladder_v5 = gp.v6 ? 2 : (gp.v5 ? 1 : 0);
+    in.ladder_v5 = gp.v7 ? 3 : gp.v6 ? 2 : (gp.v5 ? 1 : 0);
     for (int kind = 0; kind < 2; ++kind) {
         in.v5_strip_width[kind] = gp.v5 ? gp.p5[kind].strip_width : 0;
         in.v5_strips[kind] = gp.v5 ? (int32_t)gp.p5[kind].strips.size() : 0;
@@ -917,6 +945,29 @@ static int upload_v6(dts_graph *g, const GraphPlan &gp)
     return DTS_OK;
 }
 
+// v7 tables -> one device blob (groups, units, fragment pairs, fire tables)
+static int upload_v7(dts_graph *g, const GraphPlan &gp)
+{
+    dts_ctx *ctx = g->ctx;
+    std::vector<uint8_t> blob;
+    const size_t g_off = push_blob(blob, gp.p7.groups);
+    const size_t u_off = push_blob(blob, gp.p7.units);
+    const size_t f_off = push_blob(blob, gp.p7.frag);
+    const size_t r_off = push_blob(blob, gp.p7.fire);
+    HIPCHK(ctx, hipMalloc(&g->dev_tables7, blob.size()));
+    HIPCHK(ctx, hipMemcpy(g->dev_tables7, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables7);
+    g->dev_groups7 = reinterpret_cast<const Group7 *>(base + g_off);
+    g->dev_units7 = reinterpret_cast<const Unit7 *>(base + u_off);
+    g->dev_frag7 = reinterpret_cast<const uint32_t *>(base + f_off);
+    g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
+    g->ngroups7 = (int)gp.p7.groups.size();
+    g->lds7 = gp.p7.lds_bytes;
+    g->waves7 = gp.p7.waves;
+    g->v7 = true;
+    return DTS_OK;
+}
+
 int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
 {
     if (!ctx || !spec || !out) return DTS_E_INVAL;
@@ -945,6 +996,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         if (!e && gp.v4_mask) e = upload_v4(g, gp);
         if (!e && gp.v5) e = upload_v5(g, gp);
         if (!e && gp.v6) e = upload_v6(g, gp);
+        if (!e && gp.v7) e = upload_v7(g, gp);
         if (!e && hipMalloc(&g->dev_queue, kQueueSlots * kQueueWidth * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
             e = DTS_E_HIP;
@@ -1028,6 +1080,7 @@ void dts_graph_destroy(dts_graph *g)
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_tables5) hipFree(g->dev_tables5);
     if (g->dev_tables6) hipFree(g->dev_tables6);
+    if (g->dev_tables7) hipFree(g->dev_tables7);
     if (g->dev_queue) hipFree(g->dev_queue);
     qscratch_free(g->qs);
     for (auto &q : g->hqs) qscratch_free(q);
@@ -1182,6 +1235,15 @@ static bool planes_aligned6(const DevPlanes &p)
     return (p.fstride & 3) == 0;
 }
 
+// k_ladder7 stages source rows with 16-byte LDS-DMA lanes: every plane base and pitch
+// 16-byte aligned (else k_ladder6 / k_ladder5)
+static bool planes_aligned7(const DevPlanes &p)
+{
+    for (int pl = 0; pl < 3; ++pl)
+        if ((p.data[pl] | (uint64_t)p.pitch[pl]) & 15u) return false;
+    return (p.fstride & 15) == 0;
+}
+
 // The ladder launches (v4 kinds, then v3 kinds) for nframes frames of src into dst[k]
 // (format dst_fmt[k]); persistent grids over nframes x njobs items, items per launch < 2^30.
 static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, const int *dst_fmt, int nframes,
@@ -1217,6 +1279,22 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
+        const bool aligned7 = g->v7 && planes_aligned7(pp.src);
+        if (aligned7) {
+            Ladder7Params q{};
+            q.src = pp.src;
+            for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
+            q.ngroups = g->ngroups7;
+            q.nframes = n;
+            q.groups = g->dev_groups7;
+            q.units = g->dev_units7;
+            q.frag = g->dev_frag7;
+            q.fire = g->dev_fire7;
+            const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
+            if (grid > INT32_MAX) return DTS_E_RANGE;
+            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, st));
+            continue;
+        }
         bool aligned6 = g->v6 && planes_aligned6(pp.src);
         for (int k = 0; k < s.nout && aligned6; ++k) aligned6 = planes_aligned6(pp.dst[k]);
         if (aligned6) {

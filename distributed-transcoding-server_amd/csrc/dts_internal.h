@@ -293,6 +293,52 @@ hipError_t launch_ladder6(const Ladder6Params &p, int grid, int lds_bytes, hipSt
 int ladder6_lds_bytes(const Unit6 &u);
 
 // ---------------------------------------------------------------------------
+// v7 ladder (ladder7.hip, plan6.cpp plan7_graph): the v6 waves (same variants,
+// same H -> V register pipeline), grouped into workgroups that cover one source
+// column strip of one plane kind for every rendition.  Per granule the group
+// stages the strip's 16 source rows into LDS once (LDS-DMA pieces dealt over its
+// waves, one barrier per granule) and every wave reads its A operands from there:
+// the source crosses L2 -> CU about once per frame instead of once per rendition
+// and column tile.
+// ---------------------------------------------------------------------------
+constexpr int kL7Stages = 3;        // source granules staged per group (in flight + being read)
+constexpr int kL7MaxWaves = 16;     // waves per group (workgroup of <= 1024 threads)
+
+struct Unit7 {                      // one wave of a group
+    int32_t variant;                // as Unit6
+    int32_t kind, rung, col0, ncols, ngran, srcH, dstH, nrb, fmt;
+    uint32_t hfrag, vfrag;
+    int32_t fire, dstW;
+    int32_t xo[4];                  // byte offset of each tile's H K window in the staged strip (x0 - X0, multiple of 16)
+    int32_t fs;                     // V fragment slots of the rendition in this group
+    int32_t flds;                   // LDS offset of the rendition's fragment slots
+    int32_t lead;                   // 1: this wave DMAs the rendition's V fragments for the group
+    int32_t pad_;
+};
+
+struct Group7 {                     // one workgroup's strip of one frame
+    int32_t kind;                   // 0 luma, 1 chroma (U and V)
+    int32_t X0;                     // first staged source column (multiple of 16)
+    int32_t npc;                    // staged pieces per plane and granule (64 columns each)
+    int32_t nwaves;                 // units (the other waves of the workgroup only stage)
+    int32_t u0;                     // first unit
+    int32_t ngran, srcH;
+    int32_t scr;                    // LDS offset of the per-wave store exchange (1 KB per wave)
+};
+
+struct Ladder7Params {
+    DevPlanes src;
+    DevPlanes dst[kMaxRungs];
+    int32_t ngroups, nframes, pad_[2];
+    const Group7 *groups;
+    const Unit7 *units;
+    const uint32_t *frag;           // as Ladder6Params
+    const int32_t *fire;
+};
+
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
 // ---------------------------------------------------------------------------
 constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x

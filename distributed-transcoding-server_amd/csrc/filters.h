@@ -117,6 +117,20 @@ struct Plan6 {
 // kinds[0] luma, kinds[1] chroma (Plan5In: same inputs as v5).  false: the graph
 // does not fit k_ladder6 (nv12 source, planes narrower than 64 or 128 columns,
 // windows wider than two K blocks ...): it then runs on k_ladder5.
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out);
+// align: the H K windows start on multiples of align source columns (4 for k_ladder6;
+// 16 for k_ladder7, whose A operands are 16-B LDS reads); sort: heaviest units first.
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align = 4, bool sort = true);
+
+// v7 ladder plan: the v6 units (align 16) in groups of at most wmax waves over one
+// source strip (Group7, Unit7).  false: the graph does not fit k_ladder7 (plane widths
+// not multiples of 16, strips wider than the plane ...): k_ladder6 / k_ladder5 run it.
+struct Plan7 {
+    std::vector<Group7> groups;
+    std::vector<Unit7> units;
+    std::vector<uint32_t> frag;
+    std::vector<int32_t> fire;
+    int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
+};
+bool plan7_graph(const Plan5In kinds[2], int wmax, Plan7 &out);
 
 } // namespace dts

@@ -1,0 +1,333 @@
+// ladder7.hip -- k_ladder7, the v7 ladder kernel: 8-bit 4:2:0 planar sources to
+// 8-bit renditions on v_mfma_i32_16x16x64_i8, the source staged once per strip.
+//
+// Same arithmetic and the same per-wave pipeline as k_ladder6 (ladder6.hip header;
+// libswscale hScale8To15_c -> yuv2planeX_8_c / yuv2nv12cX_c under
+// SWS_BITEXACT|SWS_ACCURATE_RND, FFmpeg 4.4): a wave owns CT 16-column tiles of
+// one rendition of one plane kind and walks them top to bottom in granules of 16
+// source rows; H per granule and tile on the matrix cores, the H results kept in a
+// register ring that is the V MFMA's A operand, V per 16-row block right after the
+// granule that completes its window, coalesced row stores.
+//
+// What changes is where the A operands come from.  k_ladder6 stages, per wave,
+// the 16 rows x 64 columns of every (tile, K block) it needs: every rendition and
+// every column tile fetches its own copy of the source, ~5x the plane per frame
+// through L2, and the LDS-DMA issue of those copies was ~45 % of a wave's cycles
+// (profiles/r02b_*; tools/stamp6.py).  Here a workgroup is a group of waves of
+// every rendition whose K windows lie in one source strip [X0, X0 + 64 npc) of the
+// plane(s) (plan6.cpp plan7_graph); per granule the group DMAs the strip's 16 rows
+// into LDS once -- npc 1-KB pieces per plane, dealt round robin over all its waves
+// -- and every wave reads its A operands there:
+//
+//  * LDS image of a piece: 16 rows x 64 bytes, lane-linear as the DMA writes it.
+//    DMA lane l loads row l >> 2, 16-B chunk (l & 3) ^ sw(row), sw(r) = 2 ((r >> 3) & 1):
+//    four consecutive lanes cover one row's 64 contiguous bytes.  The A read of lane
+//    (m, g) -- row m, chunk c = xo / 16 + g of the strip -- is the ds_read_b128 at
+//    piece (c >> 2), 16 (4 m + ((c & 3) ^ sw(m))), conflict-free for every xo (each
+//    16-lane group of a ds_read_b128 meets the four chunk positions of each row
+//    quad exactly once);
+//  * kL7Stages granule stages: at granule q a wave waits for its own pieces of q
+//    (counted vmcnt), the group barriers, then issues its pieces of q + 2 into the
+//    stage granule q - 1 was read from (every wave is past those reads) and runs
+//    H(q) and the row blocks firing at q;
+//  * V fragments: the first wave of each rendition in the group DMAs them with its
+//    pieces of the fire granule into the rendition's LDS slots; the barrier of that
+//    granule publishes them to the other waves of the rendition;
+//  * waves beyond the group's units (the workgroup has the widest group's size)
+//    only stage pieces and keep the barrier count.
+#include "dts_internal.h"
+#include "ladder_mfma.h"
+
+namespace dts {
+
+namespace {
+
+constexpr int NS7 = kL7Stages;
+
+// s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0: waiting for fewer outstanding
+// operations than were issued after the batch is never too short
+__device__ __forceinline__ void vm_wait_rt7(int n)
+{
+#define DTS_W7(k) \
+    case k: __builtin_amdgcn_s_waitcnt((k) | (7 << 4) | (15 << 8)); break;
+    switch (min(max(n, 0), 15)) {
+        DTS_W7(0) DTS_W7(1) DTS_W7(2) DTS_W7(3) DTS_W7(4) DTS_W7(5) DTS_W7(6) DTS_W7(7)
+        DTS_W7(8) DTS_W7(9) DTS_W7(10) DTS_W7(11) DTS_W7(12) DTS_W7(13) DTS_W7(14)
+    default: DTS_W7(15)
+    }
+#undef DTS_W7
+}
+
+// every wave's pieces of the granule have landed (each wave waited for its own) and
+// every wave is past its reads of the previous granule
+__device__ __forceinline__ void group_barrier7() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// The group's staging: this wave's share of the pieces of every granule, the counted
+// wait and the barrier.  ops counts this wave's VMEM instructions (pieces, V fragment
+// DMAs, stores); e[i] = ops after the batch of granule q + i (i < NS7 - 1).
+struct Stage7 {
+    uint64_t sb[2];                 // plane bases of this frame (chroma: U, V)
+    uint32_t sp[2];                 // plane pitches
+    int np, npc, npieces, w, nw, srcH1, ngran, stage_bytes;
+    uint32_t lcol;                  // this lane's byte in a piece row: X0 + 16 chunk
+    int dr;                         // this lane's row in a piece
+    int ops, e[NS7 - 1];
+
+    __device__ __forceinline__ void init(const Group7 &G, const DevPlanes &S, int f, int wave, int waves, int lane)
+    {
+        np = G.kind ? 2 : 1;
+        for (int p = 0; p < 2; ++p) {
+            sb[p] = (G.kind ? S.data[1 + p] : S.data[0]) + (uint64_t)f * (uint64_t)S.fstride;
+            sp[p] = (uint32_t)(G.kind ? S.pitch[1 + p] : S.pitch[0]);
+        }
+        npc = G.npc;
+        npieces = np * npc;
+        w = wave;
+        nw = waves;
+        srcH1 = G.srcH - 1;
+        ngran = G.ngran;
+        stage_bytes = npieces * 1024;
+        dr = lane >> 2;
+        lcol = (uint32_t)G.X0 + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
+        ops = 0;
+    }
+    // this wave's pieces of granule q into stage st (nothing past the plane)
+    __device__ __forceinline__ void pieces(uint8_t *lds, int q, int st)
+    {
+        if (q >= ngran) return;
+        const uint32_t row = (uint32_t)min(kL6Gran * q + dr, srcH1);
+        uint8_t *dst = lds + st * stage_bytes;
+        for (int k = w; k < npieces; k += nw) {
+            const int p = k >= npc ? 1 : 0, i = k - p * npc;
+            const uint64_t src = (p ? sb[1] : sb[0]) + (uint64_t)(row * (p ? sp[1] : sp[0])) + lcol + 64u * (uint32_t)i;
+            __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)src,
+                                             (__attribute__((address_space(3))) void *)(dst + 1024 * k), 16, 0, 0);
+            ++ops;
+        }
+    }
+    // granule q's batch has landed for this wave: everything issued after it may still fly
+    __device__ __forceinline__ void wait_batch() { vm_wait_rt7(ops - e[0]); }
+    // after the batch of granule q + NS7 - 1 was issued
+    __device__ __forceinline__ void shift()
+    {
+#pragma unroll
+        for (int i = 0; i + 1 < NS7 - 1; ++i) e[i] = e[i + 1];
+        e[NS7 - 2] = ops;
+    }
+};
+
+// a wave with no unit: stage its pieces, keep the group's barrier count
+__device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
+{
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
+    Stage7 Z;
+    Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < NS7 - 1; ++i) {
+        Z.pieces(lds7, i, i);
+        Z.e[i] = Z.ops;
+    }
+    int sq = 0;
+    for (int q = 0; q < G.ngran; ++q) {
+        Z.wait_batch();
+        group_barrier7();
+        const int sn = sq == 0 ? NS7 - 1 : sq - 1;
+        Z.pieces(lds7, q + NS7 - 1, sn);
+        Z.shift();
+        sq = sq + 1 == NS7 ? 0 : sq + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int VAR>
+__device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
+                                      int f, int wave, int waves)
+{
+    using W = Walk6<VAR>;
+    constexpr int CT = W::CT, HKB = W::HKB, VKB = W::VKB, T = W::T, R = W::R;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
+    const int lane = (int)threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    Stage7 Z;
+    Z.init(G, S, f, wave, waves, lane);
+    // output planes: luma plane 0; nv12 chroma plane 1; yuv420p chroma planes 1 and 2
+    uint64_t ob[2];
+    uint32_t op[2];
+    {
+        const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
+        const DevPlanes D = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, dst)) + U.rung);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            ob[p] = (U.kind ? D.data[1 + p] : D.data[0]) + (uint64_t)f * (uint64_t)D.fstride;
+            op[p] = (uint32_t)(U.kind ? D.pitch[1 + p] : D.pitch[0]);
+        }
+    }
+    const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
+    // H B operands of the walk
+    v4i bh[CT][HKB], bl[CT][HKB];
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int kb = 0; kb < HKB; ++kb) {
+            const uint64_t o = fr + (uint64_t)(U.hfrag + (uint32_t)(c * HKB + kb)) * 2048u;
+            bh[c][kb] = *GP6(g_cv4i, o);
+            bl[c][kb] = *GP6(g_cv4i, o + 1024);
+        }
+    // A read offsets in a stage: tile t = (plane t / CT, column tile t % CT), K block kb
+    uint32_t aoff[T][HKB];
+    {
+        const uint32_t sw = 2u * (uint32_t)((m >> 3) & 1);
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int kb = 0; kb < HKB; ++kb) {
+                const uint32_t c = (uint32_t)U.xo[t % CT] / 16u + 4u * (uint32_t)kb + (uint32_t)g;
+                aoff[t][kb] = (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u + 16u * (4u * (uint32_t)m + ((c & 3u) ^ sw));
+            }
+    }
+    // V: the next row block to run and its fire granule; the next one whose fragments
+    // this wave DMAs (lead wave of the rendition) and its fire granule
+    k_u32 *fire = GP6(k_u32, P.fire + U.fire);
+    int j = 0, jf = 0;
+    int fg = U.nrb > 0 ? (int)fire[0] : 0x7fffffff, fgf = U.lead ? fg : 0x7fffffff;
+    v4i vh[VKB], vl[VKB];
+    const v4i zero = {0, 0, 0, 0}, hbias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
+    // the ring: slot s of tile t is dword s % 4 of rh[s / 4][t] (hi bytes) and rl (lo bytes)
+    v4i rh[VKB][T], rl[VKB][T];
+#pragma unroll
+    for (int kb = 0; kb < VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < T; ++t) rh[kb][t] = rl[kb][t] = zero;
+    uint8_t *fb = lds7 + U.flds;
+    uint8_t *scr = lds7 + G.scr + 1024 * wave;
+    const int FS = U.fs;
+    int fsi = 0, fsu = 0;
+    // the V fragments of the row blocks firing at granule <= upto (lead wave only)
+    auto frags = [&](int upto) {
+        while (fgf <= upto) {
+            Z.ops += 2 * VKB;
+            uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
+            const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
+#pragma unroll
+            for (int h = 0; h < 2 * VKB; ++h)
+                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
+                                                 (__attribute__((address_space(3))) void *)(dst + 1024 * h), 16, 0, 0);
+            fsi = fsi + 1 == FS ? 0 : fsi + 1;
+            ++jf;
+            fgf = jf < U.nrb ? (int)fire[jf] : 0x7fffffff;
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < NS7 - 1; ++i) {
+        frags(i);
+        Z.pieces(lds7, i, i);
+        Z.e[i] = Z.ops;
+    }
+    // unrolled by the ring length (8 covers both), so ring slot q % R is a fixed register
+    // in each copy; stage q % NS7 is a run-time offset
+    static_assert(8 % R == 0, "ring periods divide the unroll");
+    const int ngran = G.ngran;
+    int sq = 0;
+    for (int q0 = 0; q0 < ngran; q0 += 8) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int q = q0 + s;
+            if (q >= ngran) break;
+            Z.wait_batch();
+            group_barrier7();
+            {
+                const int sn = sq == 0 ? NS7 - 1 : sq - 1;
+                frags(q + NS7 - 1);
+                Z.pieces(lds7, q + NS7 - 1, sn);
+                Z.shift();
+            }
+            {
+                const uint8_t *st = lds7 + sq * Z.stage_bytes;
+                v4i a[T][HKB];
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int kb = 0; kb < HKB; ++kb)
+                        a[t][kb] = *reinterpret_cast<const v4i *>(st + aoff[t][kb]) ^ (int)0x80808080u;
+                v4i ah[T], al[T];
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    ah[t] = zero;
+                    al[t] = hbias;
+                }
+#pragma unroll
+                for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
+                        al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+                    }
+                const int rs = s % R;
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
+                    const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
+                    rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                    rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                }
+            }
+            while (fg == q) {
+                {
+                    const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
+#pragma unroll
+                    for (int kb = 0; kb < VKB; ++kb) {
+                        vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
+                        vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
+                    }
+                    fsu = fsu + 1 == FS ? 0 : fsu + 1;
+                }
+                Z.ops += vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g, scr);
+                ++j;
+                fg = j < U.nrb ? (int)fire[j] : 0x7fffffff;
+            }
+            sq = sq + 1 == NS7 ? 0 : sq + 1;
+        }
+    }
+    // the pieces and fragments past the plane were not issued; drain the rest before the
+    // workgroup's LDS goes away
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(64 * kL7MaxWaves)
+void k_ladder7(Ladder7Params P)
+{
+    // workgroup b: XCD b % 8; frame 8 (k / ngroups) + b % 8, group k % ngroups (k = b / 8)
+    const int b = (int)blockIdx.x, k = b >> 3;
+    const int fq = k / P.ngroups;
+    const int f = 8 * fq + (b & 7);
+    if (f >= P.nframes) return;
+    const Group7 G = kld6(P.groups + (k - fq * P.ngroups));
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), waves = (int)blockDim.x >> 6;
+    const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
+    const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
+    if (wave >= G.nwaves) {
+        idle7(G, S, f, wave, waves);
+        return;
+    }
+    const Unit7 U = kld6(P.units + G.u0 + wave);
+    switch (U.variant) {
+    case 0: walk7<0>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6>(P, G, U, S, f, wave, waves); break;
+    default: walk7<7>(P, G, U, S, f, wave, waves); break;
+    }
+}
+
+} // namespace
+
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, hipStream_t s)
+{
+    if (waves < 1 || waves > kL7MaxWaves) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ladder7, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
+    return hipGetLastError();
+}
+
+} // namespace dts

@@ -75,13 +75,15 @@ struct Rend6 {                      // one (plane kind, rendition)
     std::vector<int> fire;          // per row block
 };
 
-// H K blocks and per-tile x0; false if a tile's taps span more than 2 K blocks
-bool plan_h6(const SwsFilter &f, int srcW, int dstW, Rend6 &r)
+// H K blocks and per-tile x0 (a multiple of align); false if a tile's taps span more
+// than 2 K blocks
+bool plan_h6(const SwsFilter &f, int srcW, int dstW, Rend6 &r, int align)
 {
     const int ntiles = (dstW + 15) / 16;
+    if (align > 4 && srcW % align) return false;          // (align 4: a right-edge tile may start unaligned)
     for (int hkb = 1; hkb <= 2; ++hkb) {
         if (srcW < 64 * hkb) return false;
-        const int xmax = srcW - 64 * hkb;                  // (a right-edge tile may start unaligned)
+        const int xmax = srcW - 64 * hkb;
         bool ok = true;
         r.x0.assign(ntiles, 0);
         for (int t = 0; t < ntiles && ok; ++t) {
@@ -94,7 +96,7 @@ bool plan_h6(const SwsFilter &f, int srcW, int dstW, Rend6 &r)
                 z = std::max(z, zi);
             }
             if (z < 0) continue;                           // all-zero taps (never for a normalised filter)
-            const int x0 = std::min(a & ~3, xmax);
+            const int x0 = std::min(a & ~(align - 1), xmax);
             r.x0[t] = x0;
             ok = z < x0 + 64 * hkb;
         }
@@ -142,7 +144,7 @@ bool plan_v6(const VTable &v, int srcH, int dstH, Rend6 &r)
 
 } // namespace
 
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
 {
     out = Plan6{};
     struct Cost { Unit6 u; int64_t cost; };
@@ -171,7 +173,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
             Pending p;
             p.kind = kind;
             p.rung = k;
-            if (!plan_h6(f, in.srcW, R.dstW, p.r) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
+            if (!plan_h6(f, in.srcW, R.dstW, p.r, align) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
             const int np = in.chroma ? 2 : 1;
             p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb));
             const int ntiles = (R.dstW + 15) / 16;
@@ -258,9 +260,97 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out)
         }
     }
     // heaviest units first: the dispatcher starts them first, which shortens a frame's tail
-    std::stable_sort(units.begin(), units.end(), [](const Cost &a, const Cost &b) { return a.cost > b.cost; });
+    if (sort)
+        std::stable_sort(units.begin(), units.end(), [](const Cost &a, const Cost &b) { return a.cost > b.cost; });
     for (const Cost &c : units) out.units.push_back(c.u);
     return !out.units.empty();
+}
+
+// v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
+// position into workgroups of at most wmax waves; each group stages the columns
+// [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
+bool plan7_graph(const Plan5In kinds[2], int wmax, Plan7 &out)
+{
+    out = Plan7{};
+    if (wmax < 1 || wmax > kL7MaxWaves) return false;
+    Plan6 p6;
+    if (!plan6_graph(kinds, p6, 16, false)) return false;
+    out.frag = std::move(p6.frag);
+    out.fire = std::move(p6.fire);
+    for (int kind = 0; kind < 2; ++kind) {
+        const int srcW = kinds[kind].srcW, np = kinds[kind].chroma ? 2 : 1;
+        std::vector<Unit6> us;
+        for (const Unit6 &u : p6.units)
+            if (u.kind == kind) us.push_back(u);
+        if (us.empty()) return false;
+        // window start of a unit (its first tile's x0) orders the plane's units left to right
+        std::stable_sort(us.begin(), us.end(), [](const Unit6 &a, const Unit6 &b) { return a.x0[0] < b.x0[0]; });
+        const int n = (int)us.size(), ng = (n + wmax - 1) / wmax;
+        for (int gi = 0, u = 0; gi < ng; ++gi) {
+            const int cnt = n / ng + (gi < n % ng ? 1 : 0);   // groups as even as possible
+            Group7 g{};
+            g.kind = kind;
+            g.nwaves = cnt;
+            g.u0 = (int)out.units.size();
+            g.ngran = us[u].ngran;
+            g.srcH = us[u].srcH;
+            int a = 1 << 30, z = 0;
+            for (int i = u; i < u + cnt; ++i) {
+                const Unit6 &w = us[i];
+                const int hkb = l6_hkb(w.variant), ct = l6_ct(w.variant);
+                for (int c = 0; c < ct; ++c)
+                    if (16 * c < w.ncols) {                // tiles past the unit's columns have no taps
+                        a = std::min(a, w.x0[c]);
+                        z = std::max(z, w.x0[c] + 64 * hkb);
+                    }
+            }
+            g.npc = (z - a + 63) / 64;
+            g.X0 = std::min(a, srcW - 64 * g.npc);
+            if (g.X0 < 0 || g.X0 % 16) return false;
+            // per rendition: the first wave of the group DMAs its V fragments; slots in LDS
+            int lds = kL7Stages * np * g.npc * 1024;
+            int flds[DTS_MAX_OUTPUTS], lead[DTS_MAX_OUTPUTS];
+            for (int r = 0; r < DTS_MAX_OUTPUTS; ++r) flds[r] = lead[r] = -1;
+            for (int i = u; i < u + cnt; ++i) {
+                const Unit6 &w = us[i];
+                Unit7 v{};
+                v.variant = w.variant;
+                v.kind = w.kind;
+                v.rung = w.rung;
+                v.col0 = w.col0;
+                v.ncols = w.ncols;
+                v.ngran = w.ngran;
+                v.srcH = w.srcH;
+                v.dstH = w.dstH;
+                v.nrb = w.nrb;
+                v.fmt = w.fmt;
+                v.hfrag = w.hfrag;
+                v.vfrag = w.vfrag;
+                v.fire = w.fire;
+                v.dstW = w.dstW;
+                const int ct = l6_ct(w.variant);
+                for (int c = 0; c < 4; ++c)
+                    v.xo[c] = (c < ct && 16 * c < w.ncols) ? w.x0[c] - g.X0 : w.x0[0] - g.X0;
+                v.fs = w.fs;
+                if (lead[w.rung] < 0) {
+                    lead[w.rung] = i;
+                    flds[w.rung] = lds;
+                    lds += w.fs * l6_vkb(w.variant) * 2048;
+                    v.lead = 1;
+                }
+                v.flds = flds[w.rung];
+                if (w.ngran != g.ngran) return false;
+                out.units.push_back(v);
+            }
+            g.scr = lds;
+            out.groups.push_back(g);
+            u += cnt;
+        }
+    }
+    // the widest group sets the workgroup size; every group's LDS fits that many waves
+    for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
+    for (const Group7 &g : out.groups) out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
+    return out.lds_bytes <= 160 * 1024;
 }
 
 } // namespace dts

@@ -127,7 +127,7 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
     """8-bit sources with 8-bit outputs (cfg1, cfg2, cfg4 and upscales) plan the whole
     graph onto the v5 (matrix-core) ladder: every strip's H entries fit the waves and
     its LDS fits one workgroup per CU.  p010 sources and HDR graphs stay on v4 / v3.
-    Planar sources go on to v6 (ladder_v5 == 2), nv12 sources stay on v5."""
+    Planar sources go on to v7 (ladder_v5 == 3), nv12 sources stay on v5."""
     monkeypatch.setenv("DTS_LADDER", "5")
     for sw, sh, outs in [(3840, 2160, LADDER4K), (7680, 4320, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)]),
                          (1920, 1080, [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]),
@@ -137,7 +137,7 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
         assert info.lds_bytes <= 160 * 1024 and min(info.v5_strips) >= 1
     assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, LADDER4K)).ladder_v5 == 0
     monkeypatch.delenv("DTS_LADDER", raising=False)
-    want = 2 if fmt == D.FMT_YUV420P else 1
+    want = 3 if fmt == D.FMT_YUV420P else 1
     assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == want
     assert D.graph_plan(D.make_spec(7680, 4320, fmt, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)])).ladder_v5 == want
     monkeypatch.setenv("DTS_LADDER", "4")
@@ -147,7 +147,7 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
 def test_plan_v6_units(monkeypatch):
     """cfg2 on v6: one work unit per (plane kind, rendition, column group) of a frame;
     a tile whose taps span more than two 64-column K blocks keeps the graph on v5."""
-    monkeypatch.delenv("DTS_LADDER", raising=False)
+    monkeypatch.setenv("DTS_LADDER", "6")
     info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
     assert info.ladder_v5 == 2
     # luma: 1080p 30 x 64 columns, 720p 40 x 32 (two V K blocks), 480p 27 x 32 (two H and V K blocks);
@@ -167,3 +167,18 @@ def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
                                     [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)])).ladder_v4_mask == 0x3
     with pytest.raises(D.DtsError):
         D.graph_plan(D.make_spec(2, 2, D.FMT_YUV420P, LADDER4K))
+
+
+def test_plan_v7_groups(monkeypatch):
+    """cfg2 on v7: the v6 units (K windows on 16-column boundaries) in strip groups of
+    at most DTS_L7_W waves; planes whose widths are not multiples of 16 stay on v6."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    for w, ngroups in [(8, 13 + 13), (16, 7 + 7), (4, 25 + 25)]:
+        monkeypatch.setenv("DTS_L7_W", str(w))
+        info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
+        assert info.ladder_v5 == 3
+        assert info.njobs == ngroups                      # 97 luma and 97 chroma units
+        assert info.lds_bytes <= 160 * 1024
+    monkeypatch.delenv("DTS_L7_W", raising=False)
+    assert D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 2
+    assert D.graph_plan(D.make_spec(384, 216, D.FMT_YUV420P, [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 == 3
