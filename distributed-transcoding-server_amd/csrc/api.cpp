@@ -27,6 +27,9 @@ namespace dts { int ladder5_stamps(unsigned long long *out, bool reset); }
 #ifdef DTS_L6_STAMP
 namespace dts { int ladder6_stamps(unsigned long long *out, bool reset); }
 #endif
+#ifdef DTS_L7_STAMP
+namespace dts { int ladder7_stamps(unsigned long long *out, bool reset); }
+#endif
 
 // Quality partials (per-tile SSE / SSIM sums) of one k_quality -> k_qreduce
 // pair.  `ev` marks the last launch that used the buffer: the next user waits
@@ -501,6 +504,14 @@ int l7_waves()
     return std::min(std::max(w, 1), kL7MaxWaves);
 }
 
+// source stages per k_ladder7 group (DTS_L7_NS: diagnostic kernel builds compiled with
+// another DTS_L7_NS; the default build's kernel stages kL7Stages granules)
+int l7_stages()
+{
+    const char *f = std::getenv("DTS_L7_NS");
+    return f ? std::atoi(f) : kL7Stages;
+}
+
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
 // and k_ladder6 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
@@ -529,7 +540,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), gp.p7);
+    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), gp.p7);
     return true;
 }
 
@@ -1863,6 +1874,10 @@ int dts_debug_ladder5_stamps(unsigned long long *out, int reset) { return dts::l
 #ifdef DTS_L6_STAMP
 // diagnostic builds only (tools/build_stamp6.sh): per-variant, per-phase cycle sums of k_ladder6
 int dts_debug_ladder6_stamps(unsigned long long *out, int reset) { return dts::ladder6_stamps(out, reset != 0); }
+#endif
+#ifdef DTS_L7_STAMP
+// diagnostic builds only (tools/build_stamp7.sh): per-variant, per-phase cycle sums of k_ladder7
+extern "C" int dts_debug_ladder7_stamps(unsigned long long *out, int reset) { return dts::ladder7_stamps(out, reset != 0); }
 #endif
 
 // vf_fps.c (FFmpeg 4.4) frame selection, round=near, constant-rate input

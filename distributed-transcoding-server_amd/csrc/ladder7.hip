@@ -38,11 +38,52 @@
 #include "dts_internal.h"
 #include "ladder_mfma.h"
 
+#ifndef DTS_L7_ABLATE
+#define DTS_L7_ABLATE 0     // diagnostic builds only (wrong results): 1 no group barrier, 2 no A xor
+#endif
+#ifndef DTS_L7_DEFER
+#define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
+#endif
+#ifndef DTS_L7_NS
+#define DTS_L7_NS kL7Stages
+#endif
+#ifndef DTS_L7_STAMP
+#define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
+#endif
+
 namespace dts {
+
+#if DTS_L7_STAMP
+// [variant (8 = staging-only waves)][phase]: cycles summed over every wave; [v][6]: granules, [v][7]: waves
+__device__ unsigned long long g_l7_stamp[kL6Variants + 1][8];
+#define L7_STAMP(k)                                                        \
+    do {                                                                   \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
+        st_acc[k] += t_ - st_last;                                         \
+        st_last = t_;                                                      \
+    } while (0)
+#define L7_STAMP_INIT                                                      \
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};                     \
+    unsigned long long st_last = __builtin_amdgcn_s_memtime()
+#define L7_STAMP_DONE(v, ng)                                               \
+    do {                                                                   \
+        L7_STAMP(5);                                                       \
+        if ((threadIdx.x & 63) == 0) {                                     \
+            for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&g_l7_stamp[v][k_], st_acc[k_]); \
+            atomicAdd(&g_l7_stamp[v][6], (unsigned long long)(ng));       \
+            atomicAdd(&g_l7_stamp[v][7], 1ull);                            \
+        }                                                                  \
+    } while (0)
+#else
+#define L7_STAMP(k) (void)0
+#define L7_STAMP_INIT (void)0
+#define L7_STAMP_DONE(v, ng) (void)0
+#endif
 
 namespace {
 
-constexpr int NS7 = kL7Stages;
+constexpr int NS7 = DTS_L7_NS;
+static_assert(NS7 >= 2 && NS7 + DTS_L7_DEFER <= kL6Stages, "the planner sizes V fragment slots for kL6Stages granules");
 
 // s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0: waiting for fewer outstanding
 // operations than were issued after the batch is never too short
@@ -60,7 +101,13 @@ __device__ __forceinline__ void vm_wait_rt7(int n)
 
 // every wave's pieces of the granule have landed (each wave waited for its own) and
 // every wave is past its reads of the previous granule
-__device__ __forceinline__ void group_barrier7() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void group_barrier7()
+{
+    if (DTS_L7_ABLATE & 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // The group's staging: this wave's share of the pieces of every granule, the counted
 // wait and the barrier.  ops counts this wave's VMEM instructions (pieces, V fragment
@@ -128,15 +175,20 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
         Z.e[i] = Z.ops;
     }
     int sq = 0;
+    L7_STAMP_INIT;
     for (int q = 0; q < G.ngran; ++q) {
         Z.wait_batch();
+        L7_STAMP(0);
         group_barrier7();
+        L7_STAMP(1);
         const int sn = sq == 0 ? NS7 - 1 : sq - 1;
         Z.pieces(lds7, q + NS7 - 1, sn);
         Z.shift();
         sq = sq + 1 == NS7 ? 0 : sq + 1;
+        L7_STAMP(2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    L7_STAMP_DONE(kL6Variants, G.ngran);
 }
 
 template <int VAR>
@@ -184,12 +236,30 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 aoff[t][kb] = (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u + 16u * (4u * (uint32_t)m + ((c & 3u) ^ sw));
             }
     }
-    // V: the next row block to run and its fire granule; the next one whose fragments
-    // this wave DMAs (lead wave of the rendition) and its fire granule
+    // V: the next row block to run and its fire granule (fg; fg1 the one after, loaded a
+    // block ahead so no compare waits on a scalar load); the next one whose fragments
+    // this wave DMAs (lead wave of the rendition) and its fire granule (fgf, fgf1)
+    // The fire table rides in one VGPR (lane l: fire[l] | fire[64 + l] << 16) and is read
+    // with v_readlane: a scalar load per row block would expose its latency at the next
+    // LDS wait (SMEM and LDS share lgkmcnt).  Row blocks past 128 read memory.
     k_u32 *fire = GP6(k_u32, P.fire + U.fire);
+    const int nrb = U.nrb;
+    uint32_t vtab;
+    {
+        const int32_t *fp = P.fire + U.fire;
+        const uint32_t lo = lane < nrb ? (uint32_t)fp[lane] : 0xffffu;
+        const uint32_t hi = lane + 64 < nrb ? (uint32_t)fp[lane + 64] : 0xffffu;
+        vtab = lo | (hi << 16);
+    }
+    auto firev = [&](int i) -> int {
+        if (i >= nrb) return 0x7fffffff;
+        if (i >= 128) return (int)fire[i];
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)vtab, i & 63);
+        return (int)((i & 64 ? x >> 16 : x) & 0xffffu);
+    };
     int j = 0, jf = 0;
-    int fg = U.nrb > 0 ? (int)fire[0] : 0x7fffffff, fgf = U.lead ? fg : 0x7fffffff;
-    v4i vh[VKB], vl[VKB];
+    int fg = firev(0), fg1 = firev(1);
+    int fgf = U.lead ? fg : 0x7fffffff, fgf1 = U.lead ? fg1 : 0x7fffffff;
     const v4i zero = {0, 0, 0, 0}, hbias = {kL5Bias, kL5Bias, kL5Bias, kL5Bias};
     // the ring: slot s of tile t is dword s % 4 of rh[s / 4][t] (hi bytes) and rl (lo bytes)
     v4i rh[VKB][T], rl[VKB][T];
@@ -213,7 +283,25 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                                                  (__attribute__((address_space(3))) void *)(dst + 1024 * h), 16, 0, 0);
             fsi = fsi + 1 == FS ? 0 : fsi + 1;
             ++jf;
-            fgf = jf < U.nrb ? (int)fire[jf] : 0x7fffffff;
+            fgf = fgf1;
+            fgf1 = firev(jf + 1);
+        }
+    };
+    // the row blocks firing at granule qq (their window's last granule is in the ring)
+    auto vfire = [&](int qq) {
+        while (fg == qq) {
+            v4i vh[VKB], vl[VKB];
+            const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
+#pragma unroll
+            for (int kb = 0; kb < VKB; ++kb) {
+                vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
+                vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
+            }
+            fsu = fsu + 1 == FS ? 0 : fsu + 1;
+            Z.ops += vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g, scr);
+            ++j;
+            fg = fg1;
+            fg1 = firev(j + 1);
         }
     };
 #pragma unroll
@@ -223,31 +311,41 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         Z.e[i] = Z.ops;
     }
     // unrolled by the ring length (8 covers both), so ring slot q % R is a fixed register
-    // in each copy; stage q % NS7 is a run-time offset
+    // in each copy; stage q % NS7 is a run-time offset.  Per granule q: its A reads go out
+    // first, then the DMA of granule q + NS7 - 1, then (DTS_L7_DEFER) the row blocks that
+    // fired at q - 1 -- the ring still holds granules q - R .. q - 1 -- while the A reads
+    // land, then H(q) into ring slot q % R.
     static_assert(8 % R == 0, "ring periods divide the unroll");
     const int ngran = G.ngran;
     int sq = 0;
+    L7_STAMP_INIT;
     for (int q0 = 0; q0 < ngran; q0 += 8) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const int q = q0 + s;
             if (q >= ngran) break;
             Z.wait_batch();
+            L7_STAMP(0);
             group_barrier7();
+            L7_STAMP(1);
+            v4i a[T][HKB];
+            {
+                const uint8_t *st = lds7 + sq * Z.stage_bytes;
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int kb = 0; kb < HKB; ++kb) a[t][kb] = *reinterpret_cast<const v4i *>(st + aoff[t][kb]);
+            }
             {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1;
                 frags(q + NS7 - 1);
                 Z.pieces(lds7, q + NS7 - 1, sn);
                 Z.shift();
             }
+            L7_STAMP(2);
+            if (DTS_L7_DEFER) vfire(q - 1);
+            L7_STAMP(4);
             {
-                const uint8_t *st = lds7 + sq * Z.stage_bytes;
-                v4i a[T][HKB];
-#pragma unroll
-                for (int t = 0; t < T; ++t)
-#pragma unroll
-                    for (int kb = 0; kb < HKB; ++kb)
-                        a[t][kb] = *reinterpret_cast<const v4i *>(st + aoff[t][kb]) ^ (int)0x80808080u;
                 v4i ah[T], al[T];
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
@@ -258,8 +356,9 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 for (int kb = 0; kb < HKB; ++kb)
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
-                        ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
-                        al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+                        const v4i x = a[t][kb] ^ ((DTS_L7_ABLATE & 2) ? 0 : (int)0x80808080u);
+                        ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bh[t % CT][kb], ah[t], 0, 0, 0);
+                        al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bl[t % CT][kb], al[t], 0, 0, 0);
                     }
                 const int rs = s % R;
 #pragma unroll
@@ -270,26 +369,17 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                 }
             }
-            while (fg == q) {
-                {
-                    const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
-#pragma unroll
-                    for (int kb = 0; kb < VKB; ++kb) {
-                        vh[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb);
-                        vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
-                    }
-                    fsu = fsu + 1 == FS ? 0 : fsu + 1;
-                }
-                Z.ops += vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g, scr);
-                ++j;
-                fg = j < U.nrb ? (int)fire[j] : 0x7fffffff;
-            }
+            L7_STAMP(3);
+            if (!DTS_L7_DEFER) vfire(q);
+            L7_STAMP(4);
             sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
+    if (DTS_L7_DEFER) vfire(ngran - 1);
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    L7_STAMP_DONE(VAR, ngran);
 }
 
 __global__ __launch_bounds__(64 * kL7MaxWaves)
@@ -309,6 +399,10 @@ void k_ladder7(Ladder7Params P)
         return;
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
+#ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
+    walk7<DTS_L7_ONLYVAR>(P, G, U, S, f, wave, waves);
+    return;
+#endif
     switch (U.variant) {
     case 0: walk7<0>(P, G, U, S, f, wave, waves); break;
     case 1: walk7<1>(P, G, U, S, f, wave, waves); break;
@@ -322,6 +416,18 @@ void k_ladder7(Ladder7Params P)
 }
 
 } // namespace
+
+#if DTS_L7_STAMP
+int ladder7_stamps(unsigned long long *out, bool reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l7_stamp), sizeof(g_l7_stamp)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[(kL6Variants + 1) * 8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_l7_stamp), z, sizeof z) != hipSuccess) return -1;
+    }
+    return (kL6Variants + 1) * 8;
+}
+#endif
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, hipStream_t s)
 {

@@ -56,6 +56,10 @@ __device__ __forceinline__ void put_row6(uint64_t rowp, int at, int room, const 
         else
             *GP6(g_u32, p) = w[0];
     } else {
+        // the plane's last columns: predicated byte stores.  room goes through an empty asm
+        // so the per-byte lane masks are formed here, not hoisted out of the walk (16 SGPR
+        // pairs live across every granule)
+        asm volatile("" : "+v"(room));
 #pragma unroll
         for (int i = 0; i < NB; ++i)
             if (i < room) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));

@@ -269,10 +269,11 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, Plan7 &out)
 {
     out = Plan7{};
-    if (wmax < 1 || wmax > kL7MaxWaves) return false;
+    // (fragment slots hold the row blocks of kL6Stages granules: stages + the one-granule V deferral)
+    if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages + 1 > kL6Stages) return false;
     Plan6 p6;
     if (!plan6_graph(kinds, p6, 16, false)) return false;
     out.frag = std::move(p6.frag);
@@ -308,7 +309,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, Plan7 &out)
             g.X0 = std::min(a, srcW - 64 * g.npc);
             if (g.X0 < 0 || g.X0 % 16) return false;
             // per rendition: the first wave of the group DMAs its V fragments; slots in LDS
-            int lds = kL7Stages * np * g.npc * 1024;
+            int lds = stages * np * g.npc * 1024;
             int flds[DTS_MAX_OUTPUTS], lead[DTS_MAX_OUTPUTS];
             for (int r = 0; r < DTS_MAX_OUTPUTS; ++r) flds[r] = lead[r] = -1;
             for (int i = u; i < u + cnt; ++i) {
