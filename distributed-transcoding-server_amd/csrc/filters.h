@@ -131,6 +131,6 @@ struct Plan7 {
     std::vector<int32_t> fire;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
 };
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, Plan7 &out);
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, Plan7 &out);
 
 } // namespace dts

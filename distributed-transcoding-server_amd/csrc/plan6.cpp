@@ -269,7 +269,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, Plan7 &out)
 {
     out = Plan7{};
     // (fragment slots hold the row blocks of kL6Stages granules: stages + the one-granule V deferral)
@@ -284,11 +284,23 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, Plan7 &out)
         for (const Unit6 &u : p6.units)
             if (u.kind == kind) us.push_back(u);
         if (us.empty()) return false;
-        // window start of a unit (its first tile's x0) orders the plane's units left to right
-        std::stable_sort(us.begin(), us.end(), [](const Unit6 &a, const Unit6 &b) { return a.x0[0] < b.x0[0]; });
-        const int n = (int)us.size(), ng = (n + wmax - 1) / wmax;
-        for (int gi = 0, u = 0; gi < ng; ++gi) {
-            const int cnt = n / ng + (gi < n % ng ? 1 : 0);   // groups as even as possible
+        // window start of a unit (its first tile's x0) orders the plane's units left to right;
+        // by_rung: groups of one rendition each (their waves do the same work per granule)
+        std::stable_sort(us.begin(), us.end(), [&](const Unit6 &a, const Unit6 &b) {
+            if (by_rung && a.rung != b.rung) return a.rung < b.rung;
+            return a.x0[0] < b.x0[0];
+        });
+        // runs of units grouped together: the whole plane kind, or one rendition
+        std::vector<std::pair<int, int>> runs;
+        for (int a = 0, n = (int)us.size(); a < n;) {
+            int z = a + 1;
+            while (z < n && (!by_rung || us[z].rung == us[a].rung)) ++z;
+            const int ng = (z - a + wmax - 1) / wmax;
+            for (int gi = 0; gi < ng; ++gi) runs.push_back({(z - a) / ng + (gi < (z - a) % ng ? 1 : 0), 0});
+            a = z;
+        }
+        for (int gi = 0, u = 0; gi < (int)runs.size(); ++gi) {
+            const int cnt = runs[gi].first;                 // groups as even as possible
             Group7 g{};
             g.kind = kind;
             g.nwaves = cnt;
