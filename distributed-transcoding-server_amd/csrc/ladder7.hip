@@ -44,6 +44,9 @@
 #ifndef DTS_L7_DEFER
 #define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
 #endif
+#ifndef DTS_L7_DEFER_ST
+#define DTS_L7_DEFER_ST 0   // diagnostic: hold a row block's exchanged bytes and store them after the next H
+#endif
 #ifndef DTS_L7_NS
 #define DTS_L7_NS kL7Stages
 #endif
@@ -162,6 +165,109 @@ struct Stage7 {
         e[NS7 - 2] = ops;
     }
 };
+
+// The row block's bytes through the wave's 1-KB LDS exchange: lane (m, g) holds NB bytes
+// of output row m at byte NB g of a 4 NB-byte segment; after the exchange lane 4 m + g
+// does, so four consecutive lanes hold one row's segment (one cache access per row
+// segment).  x[] is what vstore7 writes.
+template <int VAR, class UT>
+__device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR>::T], uint8_t *scr, int m, int g,
+                                      int lane, uint32_t (&x)[4])
+{
+    using W = Walk6<VAR>;
+    __builtin_amdgcn_wave_barrier();
+    const int d = 4 * m + g;
+    if (W::NP == 1) {                                      // luma
+        if (W::CT == 4) {
+            uint32_t o[4];
+            transpose4(w[0], w[1 % W::T], w[2 % W::T], w[3 % W::T], o);
+            *reinterpret_cast<u32x4 *>(scr + 16 * d) = (u32x4){o[0], o[1], o[2], o[3]};
+            const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * lane);
+            x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w;
+        } else {
+            uint32_t o[2];
+            transpose2(w[0], w[1 % W::T], o);
+            *reinterpret_cast<u32x2 *>(scr + 8 * d) = (u32x2){o[0], o[1]};
+            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 8 * lane);
+            x[0] = r.x; x[1] = r.y; x[2] = x[3] = 0;
+        }
+    } else if (U.fmt == DTS_FMT_NV12) {                    // chroma, U V interleaved, 32 B per tile row
+#pragma unroll
+        for (int c = 0; c < W::CT; ++c) {
+            const uint32_t u = w[c], v = w[W::CT + c];
+            *reinterpret_cast<u32x2 *>(scr + 512 * c + 8 * d) =
+                (u32x2){__builtin_amdgcn_perm(v, u, 0x05010400u), __builtin_amdgcn_perm(v, u, 0x07030602u)};
+        }
+#pragma unroll
+        for (int c = 0; c < W::CT; ++c) {
+            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * c + 8 * lane);
+            x[2 * c] = r.x; x[2 * c + 1] = r.y;
+        }
+        if (W::CT == 1) x[2] = x[3] = 0;
+    } else {                                               // chroma, U and V planes
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            if (W::CT == 2) {
+                uint32_t o[2];
+                transpose2(w[2 * p], w[(2 * p + 1) % W::T], o);
+                *reinterpret_cast<u32x2 *>(scr + 512 * p + 8 * d) = (u32x2){o[0], o[1]};
+            } else {
+                *reinterpret_cast<uint32_t *>(scr + 256 * p + 4 * d) = w[p % W::T];
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            if (W::CT == 2) {
+                const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * p + 8 * lane);
+                x[2 * p] = r.x; x[2 * p + 1] = r.y;
+            } else {
+                x[p] = *reinterpret_cast<const uint32_t *>(scr + 256 * p + 4 * lane);
+            }
+        }
+        if (W::CT == 1) x[2] = x[3] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the stores of row block j from x (xchg7); returns the store instructions issued (edge
+// units' byte stores are not counted, which only makes the next source wait longer)
+template <int VAR, class UT>
+__device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4], const uint64_t (&ob)[2],
+                                       const uint32_t (&op)[2], int lane)
+{
+    using W = Walk6<VAR>;
+    const int y = 16 * j + (lane >> 2), q4 = lane & 3;
+    if (y < U.dstH) {
+        if (W::NP == 1) {
+            if (W::CT == 4) {
+                const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
+                put_row6<16>(ob[0] + (uint64_t)y * op[0], U.col0 + 16 * q4, U.dstW - U.col0 - 16 * q4, o);
+            } else {
+                const uint32_t o[2] = {x[0], x[1]};
+                put_row6<8>(ob[0] + (uint64_t)y * op[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
+            }
+        } else if (U.fmt == DTS_FMT_NV12) {
+#pragma unroll
+            for (int c = 0; c < W::CT; ++c) {
+                const uint32_t o[2] = {x[2 * c], x[2 * c + 1]};
+                const int at = 2 * U.col0 + 32 * c + 8 * q4;
+                put_row6<8>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                if (W::CT == 2) {
+                    const uint32_t o[2] = {x[2 * p], x[2 * p + 1]};
+                    put_row6<8>(ob[p] + (uint64_t)y * op[p], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
+                } else {
+                    const uint32_t o[1] = {x[p]};
+                    put_row6<4>(ob[p] + (uint64_t)y * op[p], U.col0 + 4 * q4, U.dstW - U.col0 - 4 * q4, o);
+                }
+            }
+        }
+    }
+    return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? W::CT : 2);
+}
 
 // a wave with no unit: stage its pieces, keep the group's barrier count
 __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
@@ -287,6 +393,18 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             fgf1 = firev(jf + 1);
         }
     };
+    // a row block whose stores wait until after the next H (pj >= 0; DTS_L7_DEFER_ST,
+    // measured slower: cfg2 128.7k vs 145k fps; never for the 4-tile luma walk, whose H
+    // temporaries leave no room for the 4 held registers)
+    constexpr bool DEFER_ST = DTS_L7_DEFER && DTS_L7_DEFER_ST && !(CT == 4);
+    int pj = -1;
+    uint32_t px[4];
+    auto flush = [&]() {
+        if (pj >= 0) {
+            Z.ops += vstore7<VAR>(U, pj, px, ob, op, lane);
+            pj = -1;
+        }
+    };
     // the row blocks firing at granule qq (their window's last granule is in the ring)
     auto vfire = [&](int qq) {
         while (fg == qq) {
@@ -298,7 +416,12 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
             }
             fsu = fsu + 1 == FS ? 0 : fsu + 1;
-            Z.ops += vblock<VAR>(U, j, rh, rl, vh, vl, ob, op, m, g, scr);
+            uint32_t w[T];
+            vcalc<VAR>(rh, rl, vh, vl, w);
+            flush();
+            xchg7<VAR>(U, w, scr, m, g, lane, px);
+            pj = j;
+            if (!DEFER_ST) flush();
             ++j;
             fg = fg1;
             fg1 = firev(j + 1);
@@ -369,13 +492,15 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                 }
             }
+            flush();
             L7_STAMP(3);
-            if (!DTS_L7_DEFER) vfire(q);
+            if (!DTS_L7_DEFER) vfire(q), flush();
             L7_STAMP(4);
             sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
     if (DTS_L7_DEFER) vfire(ngran - 1);
+    flush();
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

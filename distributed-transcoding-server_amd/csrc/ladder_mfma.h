@@ -130,12 +130,13 @@ struct Walk6 {
 };
 
 // one row block: V over the whole ring, then the stores of output row 16 j + m
-template <int VAR, class UT>
-__device__ __forceinline__ int vblock(const UT &U, int j, const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
-                                       const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
-                                       const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
-                                       const uint64_t (&ob)[2], const uint32_t (&op)[2], int m, int g,
-                                       uint8_t *scr)
+// V of one row block over the whole ring: w[t] = 4 consecutive output bytes of row
+// 16 j + m (lane (m, g): columns 4 g .. 4 g + 3 of tile t)
+template <int VAR>
+__device__ __forceinline__ void vcalc(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                      const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                      const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
+                                      uint32_t (&w)[Walk6<VAR>::T])
 {
     using W = Walk6<VAR>;
     // 65536 hh + 256 (hl + lh) + ll + bias as three chained accumulations: the hh chain
@@ -165,14 +166,27 @@ __device__ __forceinline__ int vblock(const UT &U, int j, const v4i (&rh)[Walk6<
     for (int kb = 0; kb < W::VKB; ++kb)
 #pragma unroll
         for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vl[kb], acc[t], 0, 0, 0);
-    uint32_t w[W::T];
 #pragma unroll
     for (int t = 0; t < W::T; ++t) {
         // av_clip_uint8(val >> 19) of 4 columns, packed
+        // (the builtin, not inline asm: the hazard recognizer does not pad an asm statement
+        // that reads an MFMA result)
         const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][0], acc[t][1], 19);
         const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][2], acc[t][3], 19);
         w[t] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
     }
+}
+
+template <int VAR, class UT>
+__device__ __forceinline__ int vblock(const UT &U, int j, const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                       const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                       const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
+                                       const uint64_t (&ob)[2], const uint32_t (&op)[2], int m, int g,
+                                       uint8_t *scr)
+{
+    using W = Walk6<VAR>;
+    uint32_t w[W::T];
+    vcalc<VAR>(rh, rl, vh, vl, w);
     if (DTS_L6_ABLATE & 4) {
 #pragma unroll
         for (int t = 0; t < W::T; ++t) asm volatile("" ::"v"(w[t]));
