@@ -520,6 +520,13 @@ bool l7_by_rung()
     return f ? f[0] == 'r' : false;
 }
 
+// k_ladder7 one-K-block walks with half the tiles (DTS_L7_NARROW=1)
+bool l7_narrow()
+{
+    const char *f = std::getenv("DTS_L7_NARROW");
+    return f ? f[0] == '1' : false;
+}
+
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
 // and k_ladder6 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
@@ -548,7 +555,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_by_rung(), gp.p7);
+    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_by_rung(), l7_narrow(), gp.p7);
     return true;
 }
 

@@ -253,11 +253,19 @@ constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, 
 // variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns
 // per H tile, VKB K blocks of 64 source rows (4 VKB granules held) per V row block, and
 // CT 16-column tiles per plane: 4 MFMA tiles when HKB = VKB = 1, else 2
-constexpr int l6_variant(int np, int hkb, int vkb) { return (np == 2 ? 4 : 0) + 2 * (hkb - 1) + (vkb - 1); }
-constexpr int l6_np(int v) { return v >= 4 ? 2 : 1; }
+// (k_ladder7 only: + 8 = "narrow", the one-K-block variants with half the tiles)
+constexpr int kL7Variants = 16;
+constexpr int l6_variant(int np, int hkb, int vkb, bool narrow = false)
+{
+    return (np == 2 ? 4 : 0) + 2 * (hkb - 1) + (vkb - 1) + (narrow && hkb == 1 && vkb == 1 ? 8 : 0);
+}
+constexpr int l6_np(int v) { return (v & 4) ? 2 : 1; }
 constexpr int l6_hkb(int v) { return ((v >> 1) & 1) + 1; }
 constexpr int l6_vkb(int v) { return (v & 1) + 1; }
-constexpr int l6_ct(int v) { return ((v & 3) == 0 ? 4 : 2) / l6_np(v); }
+constexpr int l6_ct(int v) { return ((v & 3) == 0 && !(v & 8) ? 4 : 2) / l6_np(v); }
+// k_ladder7 variants whose A operands are two ds_read_b64 (K windows on 8-column
+// boundaries allowed): one H K block, two V K blocks (luma 2 tiles, chroma 1 tile per plane)
+constexpr bool l7_b64(int v) { return v == 1 || v == 5; }
 
 struct Unit6 {                      // one wave's share of a frame
     int32_t variant;                // ladder6.hip kVar6[variant]
@@ -309,7 +317,8 @@ struct Unit7 {                      // one wave of a group
     int32_t kind, rung, col0, ncols, ngran, srcH, dstH, nrb, fmt;
     uint32_t hfrag, vfrag;
     int32_t fire, dstW;
-    int32_t xo[4];                  // byte offset of each tile's H K window in the staged strip (x0 - X0, multiple of 16)
+    int32_t xo[4];                  // byte offset of each tile's H K window in the staged strip (x0 - X0, multiple
+                                    // of 16; of 8 in the l7_b64 variants)
     int32_t fs;                     // V fragment slots of the rendition in this group
     int32_t flds;                   // LDS offset of the rendition's fragment slots
     int32_t lead;                   // 1: this wave DMAs the rendition's V fragments for the group

@@ -57,8 +57,8 @@
 namespace dts {
 
 #if DTS_L7_STAMP
-// [variant (8 = staging-only waves)][phase]: cycles summed over every wave; [v][6]: granules, [v][7]: waves
-__device__ unsigned long long g_l7_stamp[kL6Variants + 1][8];
+// [variant (16 = staging-only waves)][phase]: cycles summed over every wave; [v][6]: granules, [v][7]: waves
+__device__ unsigned long long g_l7_stamp[kL7Variants + 1][8];
 #define L7_STAMP(k)                                                        \
     do {                                                                   \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();        \
@@ -294,7 +294,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
         L7_STAMP(2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    L7_STAMP_DONE(kL6Variants, G.ngran);
+    L7_STAMP_DONE(kL7Variants, G.ngran);
 }
 
 template <int VAR>
@@ -330,17 +330,24 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             bh[c][kb] = *GP6(g_cv4i, o);
             bl[c][kb] = *GP6(g_cv4i, o + 1024);
         }
-    // A read offsets in a stage: tile t = (plane t / CT, column tile t % CT), K block kb
-    uint32_t aoff[T][HKB];
+    // A read offsets in a stage: tile t = (plane t / CT, column tile t % CT), K block kb;
+    // B64 variants: the two 8-byte halves of the lane's 16 (windows 8-column aligned)
+    constexpr bool B64 = l7_b64(VAR);
+    constexpr int NH = B64 ? 2 : 1;
+    uint32_t aoff[T][HKB][NH];
     {
         const uint32_t sw = 2u * (uint32_t)((m >> 3) & 1);
 #pragma unroll
         for (int t = 0; t < T; ++t)
 #pragma unroll
-            for (int kb = 0; kb < HKB; ++kb) {
-                const uint32_t c = (uint32_t)U.xo[t % CT] / 16u + 4u * (uint32_t)kb + (uint32_t)g;
-                aoff[t][kb] = (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u + 16u * (4u * (uint32_t)m + ((c & 3u) ^ sw));
-            }
+            for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const uint32_t b = (uint32_t)U.xo[t % CT] + 64u * (uint32_t)kb + 16u * (uint32_t)g + 8u * (uint32_t)h;
+                    const uint32_t c = b / 16u;
+                    aoff[t][kb][h] = (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u +
+                                     16u * (4u * (uint32_t)m + ((c & 3u) ^ sw)) + (B64 ? (b & 8u) : 0u);
+                }
     }
     // V: the next row block to run and its fire granule (fg; fg1 the one after, loaded a
     // block ahead so no compare waits on a scalar load); the next one whose fragments
@@ -457,7 +464,16 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 #pragma unroll
                 for (int t = 0; t < T; ++t)
 #pragma unroll
-                    for (int kb = 0; kb < HKB; ++kb) a[t][kb] = *reinterpret_cast<const v4i *>(st + aoff[t][kb]);
+                    for (int kb = 0; kb < HKB; ++kb) {
+                        if (B64) {
+                            typedef int v2i __attribute__((ext_vector_type(2)));
+                            const v2i x = *reinterpret_cast<const v2i *>(st + aoff[t][kb][0]);
+                            const v2i y = *reinterpret_cast<const v2i *>(st + aoff[t][kb][NH - 1]);
+                            a[t][kb] = (v4i){x.x, x.y, y.x, y.y};
+                        } else {
+                            a[t][kb] = *reinterpret_cast<const v4i *>(st + aoff[t][kb][0]);
+                        }
+                    }
             }
             {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1;
@@ -536,7 +552,9 @@ void k_ladder7(Ladder7Params P)
     case 4: walk7<4>(P, G, U, S, f, wave, waves); break;
     case 5: walk7<5>(P, G, U, S, f, wave, waves); break;
     case 6: walk7<6>(P, G, U, S, f, wave, waves); break;
-    default: walk7<7>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12>(P, G, U, S, f, wave, waves); break;
     }
 }
 
@@ -547,10 +565,10 @@ int ladder7_stamps(unsigned long long *out, bool reset)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l7_stamp), sizeof(g_l7_stamp)) != hipSuccess) return -1;
     if (reset) {
-        static const unsigned long long z[(kL6Variants + 1) * 8] = {};
+        static const unsigned long long z[(kL7Variants + 1) * 8] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_l7_stamp), z, sizeof z) != hipSuccess) return -1;
     }
-    return (kL6Variants + 1) * 8;
+    return (kL7Variants + 1) * 8;
 }
 #endif
 

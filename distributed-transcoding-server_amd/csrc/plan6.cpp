@@ -144,7 +144,7 @@ bool plan_v6(const VTable &v, int srcH, int dstH, Rend6 &r)
 
 } // namespace
 
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool narrow)
 {
     out = Plan6{};
     struct Cost { Unit6 u; int64_t cost; };
@@ -173,9 +173,22 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
             Pending p;
             p.kind = kind;
             p.rung = k;
-            if (!plan_h6(f, in.srcW, R.dstW, p.r, align) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
             const int np = in.chroma ? 2 : 1;
-            p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb));
+            if (align) {
+                if (!plan_h6(f, in.srcW, R.dstW, p.r, align) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
+            } else {
+                // k_ladder7: K windows on 16-column boundaries (one ds_read_b128 per A operand),
+                // or on 8-column boundaries where that saves a K block and the variant reads
+                // its A operands as two ds_read_b64 (l7_b64: the one-K-block, two-tile variants)
+                Rend6 r8 = p.r;
+                const bool ok16 = plan_h6(f, in.srcW, R.dstW, p.r, 16) && plan_v6(*R.v, in.srcH, R.dstH, p.r);
+                const bool ok8 = plan_h6(f, in.srcW, R.dstW, r8, 8) && plan_v6(*R.v, in.srcH, R.dstH, r8);
+                if (ok8 && l7_b64(l6_variant(np, r8.hkb, r8.vkb)) && (!ok16 || r8.hkb < p.r.hkb))
+                    p.r = r8;
+                else if (!ok16)
+                    return false;
+            }
+            p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb, narrow));
             const int ntiles = (R.dstW + 15) / 16;
             const int ntp = (ntiles + p.ct - 1) / p.ct * p.ct;  // tiles padded to whole units
             p.r.x0.resize(ntp, 0);
@@ -195,7 +208,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
         const SwsFilter &f = *R.fh;
         const VTable &v = *R.v;
         const int np = in.chroma ? 2 : 1;
-        const int var = l6_variant(np, p.r.hkb, p.r.vkb);
+        const int var = l6_variant(np, p.r.hkb, p.r.vkb, narrow);
         const int ntp = (int)p.r.x0.size();
         for (int t = 0; t < ntp; ++t)
             for (int kb = 0; kb < p.r.hkb; ++kb) {
@@ -269,17 +282,18 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort)
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, bool narrow, Plan7 &out)
 {
     out = Plan7{};
     // (fragment slots hold the row blocks of kL6Stages granules: stages + the one-granule V deferral)
     if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages + 1 > kL6Stages) return false;
     Plan6 p6;
-    if (!plan6_graph(kinds, p6, 16, false)) return false;
+    if (!plan6_graph(kinds, p6, 0, false, narrow)) return false;
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
     for (int kind = 0; kind < 2; ++kind) {
         const int srcW = kinds[kind].srcW, np = kinds[kind].chroma ? 2 : 1;
+        if (srcW % 16) return false;
         std::vector<Unit6> us;
         for (const Unit6 &u : p6.units)
             if (u.kind == kind) us.push_back(u);
@@ -317,6 +331,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, Pla
                         z = std::max(z, w.x0[c] + 64 * hkb);
                     }
             }
+            a &= ~15;                                      // (8-aligned windows of the b64 variants)
             g.npc = (z - a + 63) / 64;
             g.X0 = std::min(a, srcW - 64 * g.npc);
             if (g.X0 < 0 || g.X0 % 16) return false;
