@@ -443,9 +443,13 @@ def main():
         if rungq:                          # every rendition vs its reference, then the segment's record
             for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
                 ctx.quality_device(w, h, fmt, ods[k], qref_batch(k, i), B, qraws[k].data_ptr(), sptr)
+            # the segment's record (computed in warmup too, so torch's reduction kernels are
+            # loaded before the timed region)
+            sse = torch.stack([q.view(torch.int64)[:, :3].sum(0) for q in qraws])
+            ssim = torch.stack([q.view(torch.float64)[:, 3:].sum(0) for q in qraws])
             if i >= args.warmup:
-                seg_sse.append(torch.stack([q.view(torch.int64)[:, :3].sum(0) for q in qraws]))
-                seg_ssim.append(torch.stack([q.view(torch.float64)[:, 3:].sum(0) for q in qraws]))
+                seg_sse.append(sse)
+                seg_ssim.append(ssim)
 
     for s in range(args.warmup):
         step(s)
