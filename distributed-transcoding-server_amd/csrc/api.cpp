@@ -520,6 +520,13 @@ bool l7_by_rung()
     return f ? f[0] == 'r' : false;
 }
 
+// granules per k_ladder7 staging batch (DTS_L7_PB; a kernel built with DTS_L7_PAIR=1 stages 2)
+int l7_pb()
+{
+    const char *f = std::getenv("DTS_L7_PB");
+    return f ? std::atoi(f) : kL7Batch;
+}
+
 // k_ladder7 one-K-block walks with half the tiles (DTS_L7_NARROW=1)
 bool l7_narrow()
 {
@@ -555,7 +562,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_by_rung(), l7_narrow(), gp.p7);
+    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), gp.p7);
     return true;
 }
 
@@ -1305,7 +1312,9 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
-        const bool aligned7 = g->v7 && planes_aligned7(pp.src);
+        // (k_ladder7 stores whole 4-, 8- or 16-byte row segments: outputs as k_ladder6 needs them)
+        bool aligned7 = g->v7 && planes_aligned7(pp.src);
+        for (int k = 0; k < s.nout && aligned7; ++k) aligned7 = planes_aligned6(pp.dst[k]);
         if (aligned7) {
             Ladder7Params q{};
             q.src = pp.src;

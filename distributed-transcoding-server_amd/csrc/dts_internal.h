@@ -309,7 +309,8 @@ int ladder6_lds_bytes(const Unit6 &u);
 // the source crosses L2 -> CU about once per frame instead of once per rendition
 // and column tile.
 // ---------------------------------------------------------------------------
-constexpr int kL7Stages = 3;        // source granules staged per group (in flight + being read)
+constexpr int kL7Stages = 2;        // staging batches per group (in flight + being read)
+constexpr int kL7Batch = 2;         // granules per staging batch (one barrier per batch; 1: cfg2 143k, 2: 154k fps)
 constexpr int kL7MaxWaves = 16;     // waves per group (workgroup of <= 1024 threads)
 
 struct Unit7 {                      // one wave of a group

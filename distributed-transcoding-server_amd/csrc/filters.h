@@ -120,7 +120,9 @@ struct Plan6 {
 // align: the H K windows start on multiples of align source columns (4 for k_ladder6;
 // 16 for k_ladder7, whose A operands are 16-B LDS reads); sort: heaviest units first.
 // narrow (k_ladder7): the one-K-block walks get 2 tiles per plane (luma) / 1 (chroma), not 4 / 2
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align = 4, bool sort = true, bool narrow = false);
+// fs_window: granules whose firing row blocks share the V fragment slots
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align = 4, bool sort = true, bool narrow = false,
+                 int fs_window = kL6Stages);
 
 // v7 ladder plan: the v6 units (align 16) in groups of at most wmax waves over one
 // source strip (Group7, Unit7).  false: the graph does not fit k_ladder7 (plane widths
@@ -132,6 +134,6 @@ struct Plan7 {
     std::vector<int32_t> fire;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
 };
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, bool narrow, Plan7 &out);
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out);
 
 } // namespace dts

@@ -50,6 +50,9 @@
 #ifndef DTS_L7_NS
 #define DTS_L7_NS kL7Stages
 #endif
+#ifndef DTS_L7_PAIR
+#define DTS_L7_PAIR (kL7Batch == 2)  // 1: stage 2 granules per batch (one barrier per 2 granules); plan with DTS_L7_PB=2
+#endif
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
 #endif
@@ -86,7 +89,8 @@ __device__ unsigned long long g_l7_stamp[kL7Variants + 1][8];
 namespace {
 
 constexpr int NS7 = DTS_L7_NS;
-static_assert(NS7 >= 2 && NS7 + DTS_L7_DEFER <= kL6Stages, "the planner sizes V fragment slots for kL6Stages granules");
+constexpr int PB7 = DTS_L7_PAIR ? 2 : 1;   // granules per staging batch
+static_assert(NS7 >= 2 && NS7 <= 4, "stages (plan7_graph: V fragment slots for PB7 (NS7 + 1) granules)");
 
 // s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0: waiting for fewer outstanding
 // operations than were issued after the batch is never too short
@@ -136,17 +140,22 @@ struct Stage7 {
         nw = waves;
         srcH1 = G.srcH - 1;
         ngran = G.ngran;
-        stage_bytes = npieces * 1024;
+        stage_bytes = PB7 * npieces * 1024;
         dr = lane >> 2;
         lcol = (uint32_t)G.X0 + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
         ops = 0;
     }
-    // this wave's pieces of granule q into stage st (nothing past the plane)
-    __device__ __forceinline__ void pieces(uint8_t *lds, int q, int st)
+    // this wave's pieces of batch b (granules PB7 b ..) into stage st (nothing past the plane)
+    __device__ __forceinline__ void pieces(uint8_t *lds, int b, int st)
+    {
+#pragma unroll
+        for (int h = 0; h < PB7; ++h) gran(lds, PB7 * b + h, st * stage_bytes + h * npieces * 1024);
+    }
+    __device__ __forceinline__ void gran(uint8_t *lds, int q, int at)
     {
         if (q >= ngran) return;
         const uint32_t row = (uint32_t)min(kL6Gran * q + dr, srcH1);
-        uint8_t *dst = lds + st * stage_bytes;
+        uint8_t *dst = lds + at;
         for (int k = w; k < npieces; k += nw) {
             const int p = k >= npc ? 1 : 0, i = k - p * npc;
             const uint64_t src = (p ? sb[1] : sb[0]) + (uint64_t)(row * (p ? sp[1] : sp[0])) + lcol + 64u * (uint32_t)i;
@@ -282,13 +291,14 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
     }
     int sq = 0;
     L7_STAMP_INIT;
-    for (int q = 0; q < G.ngran; ++q) {
+    const int nb = (G.ngran + PB7 - 1) / PB7;
+    for (int b = 0; b < nb; ++b) {
         Z.wait_batch();
         L7_STAMP(0);
         group_barrier7();
         L7_STAMP(1);
         const int sn = sq == 0 ? NS7 - 1 : sq - 1;
-        Z.pieces(lds7, q + NS7 - 1, sn);
+        Z.pieces(lds7, b + NS7 - 1, sn);
         Z.shift();
         sq = sq + 1 == NS7 ? 0 : sq + 1;
         L7_STAMP(2);
@@ -436,7 +446,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     };
 #pragma unroll
     for (int i = 0; i < NS7 - 1; ++i) {
-        frags(i);
+        frags(PB7 * i + PB7 - 1);
         Z.pieces(lds7, i, i);
         Z.e[i] = Z.ops;
     }
@@ -454,13 +464,15 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         for (int s = 0; s < 8; ++s) {
             const int q = q0 + s;
             if (q >= ngran) break;
-            Z.wait_batch();
-            L7_STAMP(0);
-            group_barrier7();
-            L7_STAMP(1);
+            if (s % PB7 == 0) {
+                Z.wait_batch();
+                L7_STAMP(0);
+                group_barrier7();
+                L7_STAMP(1);
+            }
             v4i a[T][HKB];
             {
-                const uint8_t *st = lds7 + sq * Z.stage_bytes;
+                const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
 #pragma unroll
                 for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -475,10 +487,10 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                     }
             }
-            {
-                const int sn = sq == 0 ? NS7 - 1 : sq - 1;
-                frags(q + NS7 - 1);
-                Z.pieces(lds7, q + NS7 - 1, sn);
+            if (s % PB7 == 0) {
+                const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
+                frags(PB7 * bn + PB7 - 1);
+                Z.pieces(lds7, bn, sn);
                 Z.shift();
             }
             L7_STAMP(2);
@@ -512,7 +524,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             L7_STAMP(3);
             if (!DTS_L7_DEFER) vfire(q), flush();
             L7_STAMP(4);
-            sq = sq + 1 == NS7 ? 0 : sq + 1;
+            if (s % PB7 == PB7 - 1) sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
     if (DTS_L7_DEFER) vfire(ngran - 1);
@@ -523,7 +535,14 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     L7_STAMP_DONE(VAR, ngran);
 }
 
+#ifndef DTS_L7_WPE
+#define DTS_L7_WPE 0        // > 0: ask the compiler for at least this many waves per SIMD (register budget)
+#endif
+
 __global__ __launch_bounds__(64 * kL7MaxWaves)
+#if DTS_L7_WPE > 0
+__attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
+#endif
 void k_ladder7(Ladder7Params P)
 {
     // workgroup b: XCD b % 8; frame 8 (k / ngroups) + b % 8, group k % ngroups (k = b / 8)

@@ -144,7 +144,7 @@ bool plan_v6(const VTable &v, int srcH, int dstH, Rend6 &r)
 
 } // namespace
 
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool narrow)
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool narrow, int fs_window)
 {
     out = Plan6{};
     struct Cost { Unit6 u; int64_t cost; };
@@ -240,11 +240,11 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
         }
         const int ngran = (in.srcH + kL6Gran - 1) / kL6Gran;
         const int nrb = (int)p.r.fire.size();
-        // V fragment slots: the fragments of the row blocks firing in granules q .. q + kL6Stages - 1
+        // V fragment slots: the fragments of the row blocks firing in granules q .. q + fs_window - 1
         // are in LDS together (each is DMA'd with the source of its fire granule)
         int fs = 1;
         for (int a = 0, z = 0; a < nrb; ++a) {
-            while (z < nrb && p.r.fire[z] < p.r.fire[a] + kL6Stages) ++z;
+            while (z < nrb && p.r.fire[z] < p.r.fire[a] + fs_window) ++z;
             fs = std::max(fs, z - a);
         }
         for (int u = 0; u * p.ct < ntp; ++u) {
@@ -282,13 +282,14 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, bool narrow, Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out)
 {
     out = Plan7{};
-    // (fragment slots hold the row blocks of kL6Stages granules: stages + the one-granule V deferral)
-    if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages + 1 > kL6Stages) return false;
+    // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
+    // granules (the batches in flight + the one-granule V deferral; ladder7.hip)
+    if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages > 4 || pb < 1 || pb > 2) return false;
     Plan6 p6;
-    if (!plan6_graph(kinds, p6, 0, false, narrow)) return false;
+    if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1))) return false;
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
     for (int kind = 0; kind < 2; ++kind) {
@@ -336,7 +337,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, bool by_rung, boo
             g.X0 = std::min(a, srcW - 64 * g.npc);
             if (g.X0 < 0 || g.X0 % 16) return false;
             // per rendition: the first wave of the group DMAs its V fragments; slots in LDS
-            int lds = stages * np * g.npc * 1024;
+            int lds = stages * pb * np * g.npc * 1024;
             int flds[DTS_MAX_OUTPUTS], lead[DTS_MAX_OUTPUTS];
             for (int r = 0; r < DTS_MAX_OUTPUTS; ++r) flds[r] = lead[r] = -1;
             for (int i = u; i < u + cnt; ++i) {

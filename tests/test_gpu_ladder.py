@@ -166,6 +166,63 @@ def test_device_path_matches_host_path(ctx, n, w, h):
             assert planes_equal([y, uv, None], want), first_diff([y, uv, None], want)
 
 
+@pytest.mark.parametrize("pad", [0, 4, 1])
+def test_device_path_plane_alignment(ctx, pad):
+    """dts_graph_run_device takes source planes on 16-byte boundaries (k_ladder7 stages
+    rows with 16-byte LDS-DMA lanes; include/dts.h): pitches padded by 0 run bit-exact,
+    pitches padded by 4 or 1 are refused with DTS_E_INVAL before any launch."""
+    import torch
+    n, w, h = 3, 320, 180
+    outs = [(160, 90, D.FMT_NV12, BIC), (104, 60, D.FMT_YUV420P, BIC)]
+    g = D.Graph(ctx, D.make_spec(w, h, D.FMT_YUV420P, outs))
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    pl, pc = w + pad, cw + pad
+    size = pl * h + 2 * pc * ch
+    src = torch.zeros((n, (size + 64 + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    host = [D.synth_host(w, h, D.FMT_YUV420P, 0, 7, f) for f in range(n)]
+    for f in range(n):
+        buf = np.zeros(src.shape[1], np.uint8)
+        for p_, (off, pitch, rows) in enumerate([(0, pl, h), (pl * h, pc, ch), (pl * h + pc * ch, pc, ch)]):
+            plane = host[f][p_]
+            for y in range(rows):
+                buf[off + y * pitch: off + y * pitch + plane.shape[1]] = plane[y]
+        src[f].copy_(torch.from_numpy(buf))
+    base = src.data_ptr()
+    sf = D.DevFrames()
+    sf.data[0], sf.data[1], sf.data[2] = base, base + pl * h, base + pl * h + pc * ch
+    sf.pitch[0], sf.pitch[1], sf.pitch[2] = pl, pc, pc
+    sf.frame_stride = src.stride(0)
+    dsts, bufs = [], []
+    for (ow, oh, of, _m) in outs:
+        ocw, och = (ow + 1) // 2, (oh + 1) // 2
+        b = torch.zeros((n, ow * oh + 2 * ocw * och + 64), dtype=torch.uint8, device="cuda")
+        d = D.DevFrames()
+        d.data[0], d.data[1] = b.data_ptr(), b.data_ptr() + ow * oh
+        d.data[2] = 0 if of == D.FMT_NV12 else b.data_ptr() + ow * oh + ocw * och
+        d.pitch[0], d.pitch[1], d.pitch[2] = ow, 2 * ocw if of == D.FMT_NV12 else ocw, 0 if of == D.FMT_NV12 else ocw
+        d.frame_stride = b.stride(0)
+        dsts.append(d)
+        bufs.append(b)
+    if pad:
+        with pytest.raises(D.DtsError):
+            g.run_device(sf, n, dsts, stream=torch.cuda.current_stream().cuda_stream)
+        return
+    g.run_device(sf, n, dsts, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for f in range(n):
+        for k, (ow, oh, of, m) in enumerate(outs):
+            raw = bufs[k][f].cpu().numpy()
+            ocw, och = (ow + 1) // 2, (oh + 1) // 2
+            y = raw[:ow * oh].reshape(oh, ow)
+            if of == D.FMT_NV12:
+                got = [y, raw[ow * oh: ow * oh + 2 * ocw * och].reshape(och, 2 * ocw), None]
+            else:
+                got = [y, raw[ow * oh: ow * oh + ocw * och].reshape(och, ocw),
+                       raw[ow * oh + ocw * och: ow * oh + 2 * ocw * och].reshape(och, ocw)]
+            want = oracle_frame(host[f], w, h, D.FMT_YUV420P, ow, oh, of, m)
+            assert planes_equal(got, want), f"pad {pad} frame {f} out {k}: {first_diff(got, want)}"
+
+
 @pytest.mark.parametrize("method", [BIC, LAN, D.SCALE_GAUSS])
 def test_clip_stress(ctx, method):
     """Patterns that drive the 15-bit horizontal clip (FFMIN(val >> 7, 32767)) and the
