@@ -527,6 +527,13 @@ int l7_pb()
     return f ? std::atoi(f) : kL7Batch;
 }
 
+// a staging-only wave in every k_ladder7 group (DTS_L7_STAGER=1; plan groups of W - 1 units)
+bool l7_stager()
+{
+    const char *f = std::getenv("DTS_L7_STAGER");
+    return f ? f[0] == '1' : false;
+}
+
 // k_ladder7 one-K-block walks with half the tiles (DTS_L7_NARROW=1)
 bool l7_narrow()
 {
@@ -562,7 +569,8 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), gp.p7);
+    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), l7_stager(),
+                                                  gp.p7);
     return true;
 }
 

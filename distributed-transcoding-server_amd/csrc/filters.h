@@ -134,6 +134,8 @@ struct Plan7 {
     std::vector<int32_t> fire;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
 };
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out);
+// stager: one more wave per workgroup that only stages (groups of wmax units then have it too)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, bool stager,
+                 Plan7 &out);
 
 } // namespace dts

@@ -136,8 +136,10 @@ struct Stage7 {
         }
         npc = G.npc;
         npieces = np * npc;
-        w = wave;
-        nw = waves;
+        // the waves beyond the group's units (if any) stage every piece; else all deal them
+        const int stagers = waves - G.nwaves;
+        w = stagers > 0 ? (wave >= G.nwaves ? wave - G.nwaves : npieces) : wave;
+        nw = stagers > 0 ? stagers : waves;
         srcH1 = G.srcH - 1;
         ngran = G.ngran;
         stage_bytes = PB7 * npieces * 1024;

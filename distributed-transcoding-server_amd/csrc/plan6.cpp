@@ -282,7 +282,8 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, bool stager,
+                 Plan7 &out)
 {
     out = Plan7{};
     // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
@@ -378,6 +379,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     }
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
+    if (stager) ++out.waves;                               // one staging-only wave in every group
     for (const Group7 &g : out.groups) out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
     return out.lds_bytes <= 160 * 1024;
 }
