@@ -654,22 +654,21 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
         const int gx = bx0 + bx, gy = by0 + by;
         int4 r = make_int4(0, 0, 0, 0);
         if (gx < W4 && gy < H4) {
-            int s1 = 0, s2 = 0, ss = 0, s12 = 0;
+            // the 4x4 block's sums by v_dot4_u32_u8 (four byte products per instruction;
+            // exact: ss <= 16 * 2 * 255^2)
+            uint32_t s1 = 0, s2 = 0, ss = 0, s12 = 0;
 #pragma unroll
             for (int yy = 0; yy < 4; ++yy) {
                 const uint32_t va = load4(A + (int64_t)(4 * gy + yy) * pa, 4 * gx, inter, comp);
                 const uint32_t vb = load4(B + (int64_t)(4 * gy + yy) * pb, 4 * gx, inter, comp);
-#pragma unroll
-                for (int xx = 0; xx < 4; ++xx) {
-                    const int a = (va >> (8 * xx)) & 255, b = (vb >> (8 * xx)) & 255;
-                    s1 += a;
-                    s2 += b;
-                    ss += a * a + b * b;
-                    s12 += a * b;
-                }
+                s1 = __builtin_amdgcn_udot4(va, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(vb, 0x01010101u, s2, false);
+                ss = __builtin_amdgcn_udot4(va, va, ss, false);
+                ss = __builtin_amdgcn_udot4(vb, vb, ss, false);
+                s12 = __builtin_amdgcn_udot4(va, vb, s12, false);
             }
-            r = make_int4(s1, s2, ss, s12);
-            if (bx < kQTileBX && by < kQTileBY) sse += (unsigned long long)(ss - 2 * s12);
+            r = make_int4((int)s1, (int)s2, (int)ss, (int)s12);
+            if (bx < kQTileBX && by < kQTileBY) sse += (unsigned long long)((int)ss - 2 * (int)s12);
         }
         bs[by][bx] = r;
     }
