@@ -45,6 +45,12 @@ LADDER = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_NV12, D.S
 # default bench line); cfg3 / cfg4 are extra lines (--workload) with their own
 # algorithmic bytes.
 WORKLOADS = {
+    # BASELINE config 1's filtergraph on the GPU: 1080p30 yuv420p -> 720p bicubic (the
+    # reference's libx264 encode is host work and absent from the image)
+    "cfg1": {"src": (1920, 1080, D.FMT_YUV420P), "outs": [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)],
+             "tonemap": None, "quality": False, "batch": 512,
+             "desc": "cfg1: 1080p30 yuv420p -> 720p yuv420p bicubic (the scale of the reference's one-worker "
+                     "plumbing case; libx264 is out of scope)"},
     "cfg2": {"src": (SRC_W, SRC_H, D.FMT_YUV420P), "outs": LADDER, "tonemap": None, "quality": False,
              "desc": "cfg2: 4K60 8-bit yuv420p -> 1080p/720p/854x480 nv12 ABR ladder, bicubic "
                      "(SWS_BITEXACT|ACCURATE_RND semantics), one fused launch per batch"},

@@ -180,28 +180,44 @@ struct Stage7 {
 // The row block's bytes through the wave's 1-KB LDS exchange: lane (m, g) holds NB bytes
 // of output row m at byte NB g of a 4 NB-byte segment; after the exchange lane 4 m + g
 // does, so four consecutive lanes hold one row's segment (one cache access per row
-// segment).  x[] is what vstore7 writes.
+// segment).  x[] is what vstore7 writes.  Chunk g of row m sits at chunk position
+// g ^ ((m >> 2) & 3) of the row, so the 8 (16) lanes of a ds_write_b128 (b64) group
+// meet distinct banks; the readers' four lanes of a row cover its four positions.
+// nv12 chroma of two tiles: the two 32-byte tile rows make one 64-byte row (16-byte
+// chunks, one store per lane).
 template <int VAR, class UT>
 __device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR>::T], uint8_t *scr, int m, int g,
                                       int lane, uint32_t (&x)[4])
 {
     using W = Walk6<VAR>;
     __builtin_amdgcn_wave_barrier();
-    const int d = 4 * m + g;
+    const int d = 4 * m + (g ^ ((m >> 2) & 3));            // writer's chunk position
+    const int r4 = lane >> 2, dr = 4 * r4 + ((lane & 3) ^ ((r4 >> 2) & 3));   // reader's
     if (W::NP == 1) {                                      // luma
         if (W::CT == 4) {
             uint32_t o[4];
             transpose4(w[0], w[1 % W::T], w[2 % W::T], w[3 % W::T], o);
             *reinterpret_cast<u32x4 *>(scr + 16 * d) = (u32x4){o[0], o[1], o[2], o[3]};
-            const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * lane);
+            const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * dr);
             x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w;
         } else {
             uint32_t o[2];
             transpose2(w[0], w[1 % W::T], o);
             *reinterpret_cast<u32x2 *>(scr + 8 * d) = (u32x2){o[0], o[1]};
-            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 8 * lane);
+            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 8 * dr);
             x[0] = r.x; x[1] = r.y; x[2] = x[3] = 0;
         }
+    } else if (U.fmt == DTS_FMT_NV12 && W::CT == 2) {      // chroma, U V interleaved, 64 B per row
+        // tile c's 8 bytes of row m are bytes 32 c + 8 g: 16-byte chunk 2 c + (g >> 1), half g & 1
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t u = w[c], v = w[2 + c];
+            const int ch = (2 * c + (g >> 1)) ^ ((m >> 2) & 3);
+            *reinterpret_cast<u32x2 *>(scr + 64 * m + 16 * ch + 8 * (g & 1)) =
+                (u32x2){__builtin_amdgcn_perm(v, u, 0x05010400u), __builtin_amdgcn_perm(v, u, 0x07030602u)};
+        }
+        const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * dr);
+        x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w;
     } else if (U.fmt == DTS_FMT_NV12) {                    // chroma, U V interleaved, 32 B per tile row
 #pragma unroll
         for (int c = 0; c < W::CT; ++c) {
@@ -211,7 +227,7 @@ __device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR
         }
 #pragma unroll
         for (int c = 0; c < W::CT; ++c) {
-            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * c + 8 * lane);
+            const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * c + 8 * dr);
             x[2 * c] = r.x; x[2 * c + 1] = r.y;
         }
         if (W::CT == 1) x[2] = x[3] = 0;
@@ -229,10 +245,10 @@ __device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             if (W::CT == 2) {
-                const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * p + 8 * lane);
+                const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 512 * p + 8 * dr);
                 x[2 * p] = r.x; x[2 * p + 1] = r.y;
             } else {
-                x[p] = *reinterpret_cast<const uint32_t *>(scr + 256 * p + 4 * lane);
+                x[p] = *reinterpret_cast<const uint32_t *>(scr + 256 * p + 4 * dr);
             }
         }
         if (W::CT == 1) x[2] = x[3] = 0;
@@ -257,6 +273,10 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
                 const uint32_t o[2] = {x[0], x[1]};
                 put_row6<8>(ob[0] + (uint64_t)y * op[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
             }
+        } else if (U.fmt == DTS_FMT_NV12 && W::CT == 2) {
+            const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
+            const int at = 2 * U.col0 + 16 * q4;
+            put_row6<16>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
         } else if (U.fmt == DTS_FMT_NV12) {
 #pragma unroll
             for (int c = 0; c < W::CT; ++c) {
@@ -277,7 +297,7 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
             }
         }
     }
-    return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? W::CT : 2);
+    return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
 }
 
 // a wave with no unit: stage its pieces, keep the group's barrier count
