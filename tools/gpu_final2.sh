@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 tag=${1:-r02d}
 bash tools/gpu_check.sh tests smoke || exit $?
-for w in cfg2 cfg3 cfg4 cfg5 yadif; do
+for w in cfg2 cfg1 cfg3 cfg4 cfg5 yadif; do
   extra="--cpu-seconds 10"
   [ $w = cfg5 ] && extra="--steps 8 --warmup 2 --cpu-seconds 10"
   timeout -k 10 400 python -u bench.py --workload $w $extra > gpurun_out/final_$w.log 2>&1
