@@ -167,6 +167,12 @@ static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
     if (get_i32(env, o, "quality", 0, &s->quality) || get_i32(env, o, "qualityOut", 0, &s->quality_out) ||
         get_i32(env, o, "maxBatch", 0, &s->max_batch))
         return -1;
+    /* srcRange / dstRange: 0 = tv (limited), 1 = pc (full) -> dts_graph_spec.range */
+    {
+        int32_t sr = 0, dr = 0;
+        if (get_i32(env, o, "srcRange", 0, &sr) || get_i32(env, o, "dstRange", 0, &dr)) return -1;
+        s->range = (sr & 1) | ((dr & 1) << 4);
+    }
     /* deint: {mode, tff} -> yadif ahead of the ladder (sources carry a context frame each side) */
     bool has_di = false;
     napi_has_named_property(env, o, "deint", &has_di);

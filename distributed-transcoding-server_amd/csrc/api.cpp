@@ -453,6 +453,9 @@ int validate_spec(const dts_graph_spec &s)
         if (!method_ok(o.method)) return DTS_E_UNSUPPORTED;
     }
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
+    if ((s.range & ~0x11) != 0) return DTS_E_INVAL;              // DTS_RANGE_* in bits 0 and 4
+    if ((s.range & 1) != ((s.range >> 4) & 1) && (s.hdr_to_sdr || s.src_fmt != DTS_FMT_YUV420P))
+        return DTS_E_UNSUPPORTED;                                // range conversion: k_ladder7 sources only
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
     if (s.quality && !fmt_8bit(s.out[s.quality_out].fmt)) return DTS_E_UNSUPPORTED;   // vf_psnr/vf_ssim: 8-bit
     if (s.deint) {                                        // yadif ahead of the ladder: 8-bit yuv420p, frame modes
@@ -554,6 +557,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
         in.nv12_chroma = kind == 1 && s.src_fmt == DTS_FMT_NV12;
         in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
         in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
+        if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         for (int k = 0; k < s.nout; ++k) {
             const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
             in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
@@ -601,6 +605,8 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
         if (e) return e;
     }
     const bool v5 = plan5_graph(s, gp);
+    // range conversion runs in k_ladder7's H epilogue only
+    if ((s.range & 1) != ((s.range >> 4) & 1) && !gp.v7) return DTS_E_UNSUPPORTED;
     int ndmax_need = 1;
     for (int k = 0; k < s.nout; ++k)
         for (int kind = 0; kind < 2; ++kind) {
@@ -711,7 +717,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.4 (gfx950; abi 4)"; }
+const char *dts_version(void) { return "dts-mi355x 0.5 (gfx950; abi 5)"; }
 
 const char *dts_strerror(int err)
 {
@@ -1323,6 +1329,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         // (k_ladder7 stores whole 4-, 8- or 16-byte row segments: outputs as k_ladder6 needs them)
         bool aligned7 = g->v7 && planes_aligned7(pp.src);
         for (int k = 0; k < s.nout && aligned7; ++k) aligned7 = planes_aligned6(pp.dst[k]);
+        if (!aligned7 && (s.range & 1) != ((s.range >> 4) & 1)) return DTS_E_UNSUPPORTED;   // range conversion: v7 only
         if (aligned7) {
             Ladder7Params q{};
             q.src = pp.src;
@@ -1335,7 +1342,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.fire = g->dev_fire7;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
-            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, st));
+            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1), st));
             continue;
         }
         bool aligned6 = g->v6 && planes_aligned6(pp.src);

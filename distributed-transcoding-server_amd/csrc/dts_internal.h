@@ -323,7 +323,9 @@ struct Unit7 {                      // one wave of a group
     int32_t fs;                     // V fragment slots of the rendition in this group
     int32_t flds;                   // LDS offset of the rendition's fragment slots
     int32_t lead;                   // 1: this wave DMAs the rendition's V fragments for the group
-    int32_t pad_;
+    int32_t rc_sh;                  // range conversion of the 15-bit H output (0: none):
+    int32_t rc_cap, rc_mul, rc_add; //   y = (min(y, cap) * mul + add) >> sh, as swscale.c's lum/chr
+                                    //   RangeToJpeg_c / RangeFromJpeg_c (int16 store)
 };
 
 struct Group7 {                     // one workgroup's strip of one frame
@@ -346,7 +348,7 @@ struct Ladder7Params {
     const int32_t *fire;
 };
 
-hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, hipStream_t s);
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

@@ -88,6 +88,7 @@ struct Plan5In {
     bool nv12_chroma = false;        // chroma staged from an interleaved nv12 plane
     int srcW = 0, srcH = 0;          // plane size
     int lds_cap = 160 * 1024;        // bytes per workgroup (one per CU)
+    int range_conv = 0;              // 0 none, 1 *RangeToJpeg, 2 *RangeFromJpeg (k_ladder7 only)
     std::vector<Plan5Rung> rungs;
 };
 

@@ -329,7 +329,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
     L7_STAMP_DONE(kL7Variants, G.ngran);
 }
 
-template <int VAR>
+template <int VAR, bool RC>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -534,12 +534,30 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bl[t % CT][kb], al[t], 0, 0, 0);
                     }
                 const int rs = s % R;
+                if (!RC) {
 #pragma unroll
-                for (int t = 0; t < T; ++t) {
-                    const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
-                    const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
-                    rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                    rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                    for (int t = 0; t < T; ++t) {
+                        const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
+                        const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
+                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                    }
+                } else {
+                    // range conversion of the 15-bit H output (swscale.c lum/chrRange{To,From}Jpeg_c:
+                    // FFMIN(y, cap) * mul + add, >> sh, stored as int16)
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {
+                        int y[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int v = min(((ah[t][i] << 8) + al[t][i]) >> 7, 32767);
+                            y[i] = (min(v, U.rc_cap) * U.rc_mul + U.rc_add) >> U.rc_sh;
+                        }
+                        const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)y[1], (uint32_t)y[0], 0x05040100u);
+                        const uint32_t p1 = __builtin_amdgcn_perm((uint32_t)y[3], (uint32_t)y[2], 0x05040100u);
+                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                    }
                 }
             }
             flush();
@@ -561,6 +579,9 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 #define DTS_L7_WPE 0        // > 0: ask the compiler for at least this many waves per SIMD (register budget)
 #endif
 
+// RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
+// the common kernel keeps its register allocation)
+template <bool RC>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -582,20 +603,20 @@ void k_ladder7(Ladder7Params P)
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
-    walk7<DTS_L7_ONLYVAR>(P, G, U, S, f, wave, waves);
+    walk7<DTS_L7_ONLYVAR, RC>(P, G, U, S, f, wave, waves);
     return;
 #endif
     switch (U.variant) {
-    case 0: walk7<0>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC>(P, G, U, S, f, wave, waves); break;
     }
 }
 
@@ -613,10 +634,13 @@ int ladder7_stamps(unsigned long long *out, bool reset)
 }
 #endif
 
-hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, hipStream_t s)
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s)
 {
     if (waves < 1 || waves > kL7MaxWaves) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ladder7, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
+    if (range_conv)
+        hipLaunchKernelGGL(k_ladder7<true>, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
+    else
+        hipLaunchKernelGGL(k_ladder7<false>, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
     return hipGetLastError();
 }
 

@@ -362,6 +362,17 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                 for (int c = 0; c < 4; ++c)
                     v.xo[c] = (c < ct && 16 * c < w.ncols) ? w.x0[c] - g.X0 : w.x0[0] - g.X0;
                 v.fs = w.fs;
+                // swscale.c (FFmpeg 4.4) range converters (oracle/swscale_ref.c restates them)
+                static const int32_t rc[2][2][4] = {
+                    {{14, 30189, 19077, -39057361}, {14, 32767, 14071, 33561947}},   // luma: To, From
+                    {{12, 30775, 4663, -9289992}, {11, 32767, 1799, 4081085}}};     // chroma: To, From
+                if (kinds[kind].range_conv) {
+                    const int32_t *c = rc[kind][kinds[kind].range_conv - 1];
+                    v.rc_sh = c[0];
+                    v.rc_cap = c[1];
+                    v.rc_mul = c[2];
+                    v.rc_add = c[3];
+                }
                 if (lead[w.rung] < 0) {
                     lead[w.rung] = i;
                     flds[w.rung] = lds;

@@ -23,7 +23,10 @@ const MAX_OUTPUTS = 4;
 // worker would put on its ffmpeg command line:
 //   {"scale": "bicubic", "format": "nv12", "param": [b, c], "tonemap": {"mode": "hable", ...},
 //    "quality": "psnr" | "ssim" | "both", "qualityRef": "lanczos",
-//    "deinterlace": "yadif" | {"mode": 0 | 2, "parity": "tff" | "bff"}}
+//    "deinterlace": "yadif" | {"mode": 0 | 2, "parity": "tff" | "bff"},
+//    "inRange": "tv" | "pc", "outRange": "tv" | "pc"}
+// inRange / outRange: `scale=in_range=R:out_range=R` (libswscale range conversion on
+// the horizontally scaled lines; dts_graph_spec.range).
 // deinterlace: `yadif=MODE:PARITY` ahead of the scale (frame-rate modes; vf_yadif.c),
 // run on the GPU in the same graph (dts_graph_spec.deint).
 // quality: `[rendition][reference]psnr` / `ssim` per segment against a reference
@@ -51,6 +54,19 @@ function outputOf(job) {
 }
 
 const QUALITY = { psnr: 1, ssim: 2, both: 3, true: 3 };
+const RANGE = { tv: 0, mpeg: 0, limited: 0, pc: 1, jpeg: 1, full: 1 };
+
+// {src, dst}: DTS_RANGE_* of the source and of the renditions
+function rangeOf(job) {
+    const s = parseSettings(job.codecSettings);
+    const r = function (v, what) {
+        if (v === undefined) return 0;
+        const x = RANGE[String(v).toLowerCase()];
+        if (x === undefined) throw new Error("job " + job.id + ": unknown " + what + " " + v);
+        return x;
+    };
+    return { src: r(s.inRange, "inRange"), dst: r(s.outRange, "outRange") };
+}
 
 // {mode, tff} or null
 function deintOf(job) {
@@ -120,12 +136,19 @@ function planLadders(jobs, sources) {
                     throw new Error("jobs " + part[0].id + "/" + r.id + ": one graph needs one deinterlace setting");
             });
             if (di) spec.deint = di;
+            const rg = rangeOf(part[0]);
+            part.forEach(function (r) {
+                if (JSON.stringify(rangeOf(r)) !== JSON.stringify(rg))
+                    throw new Error("jobs " + part[0].id + "/" + r.id + ": one graph needs one range setting");
+            });
+            if (rg.src || rg.dst) { spec.srcRange = rg.src; spec.dstRange = rg.dst; }
             // per-rendition quality (codecSettings.quality): run by the scheduler after the
             // ladder, each requesting row against its reference rendition
             const q = part.map(qualityOf);
             const quality = q.some(function (x) { return x; }) ? {
                 rows: q.map(function (x) { return x ? x.mode : 0; }),
                 refSpec: { src: spec.src, quality: 0, maxBatch: spec.maxBatch, deint: spec.deint,
+                           srcRange: spec.srcRange, dstRange: spec.dstRange,
                            outputs: spec.outputs.map(function (o, k) {
                                return { w: o.w, h: o.h, fmt: o.fmt, method: q[k] ? q[k].ref : o.method };
                            }) }
@@ -178,6 +201,6 @@ function summarizeQuality(stats, w, h) {
 }
 
 module.exports = { FMT: FMT, METHOD: METHOD, TONEMAP: TONEMAP, MAX_OUTPUTS: MAX_OUTPUTS, parseSettings: parseSettings,
-                   outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, deintOf: deintOf,
+                   outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, deintOf: deintOf, rangeOf: rangeOf,
                    planLadders: planLadders,
                    rateOf: rateOf, fpsFrames: fpsFrames, summarizeQuality: summarizeQuality };

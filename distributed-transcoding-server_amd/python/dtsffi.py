@@ -51,7 +51,7 @@ class GraphSpec(ctypes.Structure):
                 ("quality", ctypes.c_int32), ("quality_out", ctypes.c_int32), ("max_batch", ctypes.c_int32),
                 ("hdr_to_sdr", ctypes.c_int32), ("tonemap", TonemapSpec),
                 ("deint", ctypes.c_int32), ("deint_mode", ctypes.c_int32), ("deint_tff", ctypes.c_int32),
-                ("pad2_", ctypes.c_int32)]
+                ("range", ctypes.c_int32)]
 
 
 class Frame(ctypes.Structure):
@@ -232,7 +232,7 @@ def graph_plan(spec):
 
 
 def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0, tonemap=None,
-              deint=None):
+              deint=None, src_range=0, dst_range=0):
     """outputs: list of (w, h, fmt, method[, (p0, p1)]).  tonemap: None, or a dict
     {mode, param, desat, peak, npl} turning on HDR10 -> SDR (dts_tonemap_spec).
     deint: None, or (mode, tff) for yadif ahead of the ladder (sources then carry one
@@ -254,6 +254,7 @@ def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max
         s.tonemap.npl = tonemap.get("npl", 100.0)
     if deint is not None:
         s.deint, s.deint_mode, s.deint_tff = 1, deint[0], deint[1]
+    s.range = (src_range & 1) | ((dst_range & 1) << 4)   # DTS_RANGE_*: 0 MPEG (limited), 1 JPEG (full)
     return s
 
 

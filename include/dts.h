@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DTS_ABI_VERSION 4
+#define DTS_ABI_VERSION 5
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -128,8 +128,17 @@ typedef struct dts_graph_spec {
     int32_t deint;                      /* 0 = off, 1 = yadif */
     int32_t deint_mode;                 /* 0 or 2 */
     int32_t deint_tff;                  /* 1 = top field first, 0 = bottom */
-    int32_t pad2_;
+    /* YUV range conversion (`scale=in_range=R:out_range=R`, libswscale srcRange /
+     * dstRange): source range | output range << 4, each DTS_RANGE_*.  Different
+     * ranges run swscale.c's lum/chrRangeToJpeg / FromJpeg on the 15-bit
+     * horizontal output (every rendition takes the output range).  Supported for
+     * 8-bit planar sources on the v7 ladder (plane widths multiples of 16, no HDR);
+     * else dts_graph_create returns DTS_E_UNSUPPORTED. */
+    int32_t range;
 } dts_graph_spec;
+
+#define DTS_RANGE_MPEG 0                /* limited / tv (16..235, 16..240) */
+#define DTS_RANGE_JPEG 1                /* full / pc (0..255) */
 
 /* host frame: plane p at data[p] with row pitch pitch[p] bytes.
  * yuv420p: Y, U, V.  nv12 / p010le: Y, interleaved UV, (unused). */

@@ -63,6 +63,15 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
                     uint8_t *const dst[3], const int64_t dst_pitch[3],
                     int flags, const double param[2]);
 
+/* The same with libswscale's range conversion: src_range / dst_range 0 = MPEG
+ * (limited), 1 = JPEG (full); different ranges run swscale.c's lum/chrRange
+ * To/FromJpeg_c on the 15-bit horizontal output. */
+int orc_scale_frame_range(int srcW, int srcH, int srcFmt,
+                          const uint8_t *const src[3], const int64_t src_pitch[3],
+                          int dstW, int dstH, int dstFmt,
+                          uint8_t *const dst[3], const int64_t dst_pitch[3],
+                          int flags, const double param[2], int src_range, int dst_range);
+
 /* vf_psnr compute_images_mse for one 8-bit plane: returns the integer SSE. */
 uint64_t orc_plane_sse8(const uint8_t *a, int64_t apitch, const uint8_t *b,
                         int64_t bpitch, int w, int h);

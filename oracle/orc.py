@@ -35,6 +35,9 @@ def lib():
         L.orc_get_local_pos.argtypes = [i32, i32]
         L.orc_scale_frame.argtypes = [i32, i32, i32, ctypes.POINTER(vp), ctypes.POINTER(i64), i32, i32, i32,
                                       ctypes.POINTER(vp), ctypes.POINTER(i64), i32, ctypes.POINTER(ctypes.c_double)]
+        L.orc_scale_frame_range.argtypes = [i32, i32, i32, ctypes.POINTER(vp), ctypes.POINTER(i64), i32, i32, i32,
+                                            ctypes.POINTER(vp), ctypes.POINTER(i64), i32,
+                                            ctypes.POINTER(ctypes.c_double), i32, i32]
         L.orc_plane_sse8.argtypes = [vp, i64, vp, i64, i32, i32]
         L.orc_plane_sse8.restype = ctypes.c_uint64
         L.orc_plane_ssim8.argtypes = [vp, i64, vp, i64, i32, i32]
@@ -87,14 +90,15 @@ def _alloc(w, h, fmt):
 
 
 def scale_frame(src_planes, src_w, src_h, src_fmt, dst_w, dst_h, dst_fmt, method,
-                param=(PARAM_DEFAULT, PARAM_DEFAULT)):
-    """sws_scale of one frame through the restated C path; returns dst planes."""
+                param=(PARAM_DEFAULT, PARAM_DEFAULT), src_range=0, dst_range=0):
+    """sws_scale of one frame through the restated C path; returns dst planes.
+    src_range / dst_range: 0 MPEG (limited), 1 JPEG (full) (libswscale range conversion)."""
     dst = _alloc(dst_w, dst_h, dst_fmt)
     sd, sp = _ptrs(src_planes)
     dd, dp = _ptrs(dst)
     par = (ctypes.c_double * 2)(*param)
-    r = lib().orc_scale_frame(src_w, src_h, src_fmt, sd, sp, dst_w, dst_h, dst_fmt, dd, dp,
-                              method | SWS_ACCURATE_RND | SWS_BITEXACT, par)
+    r = lib().orc_scale_frame_range(src_w, src_h, src_fmt, sd, sp, dst_w, dst_h, dst_fmt, dd, dp,
+                                    method | SWS_ACCURATE_RND | SWS_BITEXACT, par, src_range, dst_range)
     if r != 0:
         raise RuntimeError(f"orc_scale_frame failed ({r})")
     return dst

@@ -506,14 +506,47 @@ static int16_t *hpass(const uint8_t *base, int64_t pitch, int kind, int comp,
 
 static int fmt_is_nv(int fmt) { return fmt == ORC_FMT_NV12 || fmt == ORC_FMT_P010LE; }
 
+/* swscale.c (FFmpeg 4.4) range converters on the 15-bit horizontally scaled lines,
+ * installed by ff_sws_init_range_convert when srcRange != dstRange for a YUV
+ * destination of <= 14 bits: srcRange = 1 (JPEG / full) -> *FromJpeg_c, else
+ * *ToJpeg_c; applied to every luma line (lumConvertRange) and to both chroma lines
+ * (chrConvertRange) right after hScale.  The int16 stores truncate as C does. */
+static void lum_range_to_jpeg(int16_t *dst, int width)
+{
+    int i;
+    for (i = 0; i < width; i++)
+        dst[i] = (int16_t)((FFMIN(dst[i], 30189) * 19077 - 39057361) >> 14);
+}
+
+static void chr_range_to_jpeg(int16_t *dst, int width)
+{
+    int i;
+    for (i = 0; i < width; i++)
+        dst[i] = (int16_t)((FFMIN(dst[i], 30775) * 4663 - 9289992) >> 12);   /* -264 */
+}
+
+static void lum_range_from_jpeg(int16_t *dst, int width)
+{
+    int i;
+    for (i = 0; i < width; i++)
+        dst[i] = (int16_t)((dst[i] * 14071 + 33561947) >> 14);
+}
+
+static void chr_range_from_jpeg(int16_t *dst, int width)
+{
+    int i;
+    for (i = 0; i < width; i++)
+        dst[i] = (int16_t)((dst[i] * 1799 + 4081085) >> 11);               /* 1469 */
+}
+
 /* swscale.c swscale() main loop for 4:2:0 -> 4:2:0, 8-bit or p010 output,
- * restricted to the BITEXACT|ACCURATE_RND C path (no range conversion:
- * both sides limited-range YUV). */
-int orc_scale_frame(int srcW, int srcH, int srcFmt,
-                    const uint8_t *const src[3], const int64_t src_pitch[3],
-                    int dstW, int dstH, int dstFmt,
-                    uint8_t *const dst[3], const int64_t dst_pitch[3],
-                    int flags, const double param[2])
+ * restricted to the BITEXACT|ACCURATE_RND C path; src_range / dst_range
+ * (0 = MPEG / limited, 1 = JPEG / full) select the range converters above. */
+int orc_scale_frame_range(int srcW, int srcH, int srcFmt,
+                          const uint8_t *const src[3], const int64_t src_pitch[3],
+                          int dstW, int dstH, int dstFmt,
+                          uint8_t *const dst[3], const int64_t dst_pitch[3],
+                          int flags, const double param[2], int src_range, int dst_range)
 {
     orc_filter hl, hc, vl, vc;
     int chrSrcW = (srcW + 1) >> 1, chrSrcH = (srcH + 1) >> 1;
@@ -542,6 +575,14 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
     } else {
         lu = hpass(src[1], src_pitch[1], 0, 0, chrSrcW, chrSrcH, chrDstW, &hc);
         lv = hpass(src[2], src_pitch[2], 0, 0, chrSrcW, chrSrcH, chrDstW, &hc);
+    }
+
+    if (!!src_range != !!dst_range) {
+        for (y = 0; y < srcH; y++) (src_range ? lum_range_from_jpeg : lum_range_to_jpeg)(ly + (size_t)y * dstW, dstW);
+        for (y = 0; y < chrSrcH; y++) {
+            (src_range ? chr_range_from_jpeg : chr_range_to_jpeg)(lu + (size_t)y * chrDstW, chrDstW);
+            (src_range ? chr_range_from_jpeg : chr_range_to_jpeg)(lv + (size_t)y * chrDstW, chrDstW);
+        }
     }
 
     for (y = 0; y < dstH; y++) {
@@ -590,6 +631,16 @@ int orc_scale_frame(int srcW, int srcH, int srcFmt,
     free_filter(&vl);
     free_filter(&vc);
     return 0;
+}
+
+int orc_scale_frame(int srcW, int srcH, int srcFmt,
+                    const uint8_t *const src[3], const int64_t src_pitch[3],
+                    int dstW, int dstH, int dstFmt,
+                    uint8_t *const dst[3], const int64_t dst_pitch[3],
+                    int flags, const double param[2])
+{
+    return orc_scale_frame_range(srcW, srcH, srcFmt, src, src_pitch, dstW, dstH, dstFmt, dst, dst_pitch, flags,
+                                 param, 0, 0);
 }
 
 /* libavfilter/vf_fps.c (4.4) frame selection with round=near for a constant

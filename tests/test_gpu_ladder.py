@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import dtsffi as D
+import orc
 from _util import first_diff, oracle_frame, planes_equal, random_frame
 
 pytestmark = pytest.mark.gpu
@@ -221,6 +222,32 @@ def test_device_path_plane_alignment(ctx, pad):
                        raw[ow * oh + ocw * och: ow * oh + 2 * ocw * och].reshape(och, ocw)]
             want = oracle_frame(host[f], w, h, D.FMT_YUV420P, ow, oh, of, m)
             assert planes_equal(got, want), f"pad {pad} frame {f} out {k}: {first_diff(got, want)}"
+
+
+@pytest.mark.parametrize("src_range,dst_range", [(0, 1), (1, 0)])
+@pytest.mark.parametrize("method", [BIC, LAN, BIL])
+def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method):
+    """`scale=in_range:out_range`: swscale.c's lum/chrRange{To,From}Jpeg_c on the
+    15-bit H output, in k_ladder7's H epilogue, bit-exact vs the oracle (random and
+    full-swing frames, nv12 and yuv420p renditions).  Other kernels refuse it."""
+    sw, sh = 384, 216
+    outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_YUV420P, method), (384, 216, D.FMT_NV12, method)]
+    spec = D.make_spec(sw, sh, D.FMT_YUV420P, outs, src_range=src_range, dst_range=dst_range)
+    if ladder_kernel != "v7":
+        with pytest.raises(D.DtsError):
+            D.Graph(ctx, spec)
+        return
+    rng = np.random.default_rng(17 + src_range + method)
+    swing = [np.where((np.arange(sw)[None, :] // 3) % 2 == 0, 255, 0).astype(np.uint8).repeat(sh, 0),
+             np.full((sh // 2, sw // 2), 255, np.uint8), np.zeros((sh // 2, sw // 2), np.uint8)]
+    frames = [random_frame(sw, sh, D.FMT_YUV420P, rng), D.synth_host(sw, sh, D.FMT_YUV420P, 0, 3, 1), swing]
+    g = D.Graph(ctx, spec)
+    got, _ = g.run_host(frames)
+    for f, src in enumerate(frames):
+        for k, (w, h, fmt, m) in enumerate(outs):
+            want = orc.scale_frame(src, sw, sh, D.FMT_YUV420P, w, h, fmt, m, src_range=src_range, dst_range=dst_range)
+            assert planes_equal(got[f][k], want), f"frame {f} out {k}: {first_diff(got[f][k], want)}"
+    g.close()
 
 
 @pytest.mark.parametrize("method", [BIC, LAN, D.SCALE_GAUSS])

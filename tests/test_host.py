@@ -182,3 +182,26 @@ def test_plan_v7_groups(monkeypatch):
     monkeypatch.delenv("DTS_L7_W", raising=False)
     assert D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 2
     assert D.graph_plan(D.make_spec(384, 216, D.FMT_YUV420P, [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 == 3
+
+
+def test_plan_range_conversion(monkeypatch):
+    """Range conversion (dts_graph_spec.range) plans onto k_ladder7 only: 8-bit planar
+    sources with plane widths multiples of 16; nv12 / p010 sources, HDR graphs, other
+    widths and DTS_LADDER=6 are refused with DTS_E_UNSUPPORTED, bad bits with INVAL."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    outs = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]
+    for sr, dr in [(0, 1), (1, 0), (1, 1)]:
+        assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=sr, dst_range=dr)).ladder_v5 == 3
+    for fmt in (D.FMT_NV12, D.FMT_P010LE):
+        with pytest.raises(D.DtsError):
+            D.graph_plan(D.make_spec(3840, 2160, fmt, outs, src_range=1))
+    with pytest.raises(D.DtsError):
+        D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, outs, dst_range=1))
+    s = D.make_spec(3840, 2160, D.FMT_YUV420P, outs)
+    s.range = 2
+    with pytest.raises(D.DtsError):
+        D.graph_plan(s)
+    monkeypatch.setenv("DTS_LADDER", "6")
+    with pytest.raises(D.DtsError):
+        D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1))
+    assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1, dst_range=1)).ladder_v5 == 2

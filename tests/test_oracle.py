@@ -127,3 +127,19 @@ def test_yadif_oracle_properties():
     for mode in range(4):
         oc = orc.yadif_frame(c, c, c, w, h, mode, 1, 0)
         assert all(np.array_equal(a, b) for a, b in zip(oc, c))
+
+
+@pytest.mark.parametrize("v,src_range,dst_range,luma,chroma", [
+    (16, 0, 1, 0, 0), (235, 0, 1, 255, 250), (128, 0, 1, 130, 128),
+    (0, 1, 0, 16, 16), (255, 1, 0, 235, 240), (128, 1, 0, 126, 128)])
+def test_range_conversion_known_answers(v, src_range, dst_range, luma, chroma):
+    """swscale.c lum/chrRangeToJpeg_c and *FromJpeg_c on a constant frame at 1:1:
+    MPEG black / white 16 / 235 map to JPEG 0 / 255 and back, neutral chroma 128
+    stays 128, JPEG chroma 255 maps to the MPEG chroma ceiling 240."""
+    w, h = 64, 32
+    f = [np.full((h, w), v, np.uint8), np.full((h // 2, w // 2), v, np.uint8), np.full((h // 2, w // 2), v, np.uint8)]
+    out = orc.scale_frame(f, w, h, 0, w, h, 0, BIC, src_range=src_range, dst_range=dst_range)   # yuv420p
+    assert set(np.unique(out[0])) == {luma}
+    assert set(np.unique(out[1])) == {chroma} and set(np.unique(out[2])) == {chroma}
+    same = orc.scale_frame(f, w, h, 0, w, h, 0, BIC, src_range=src_range, dst_range=src_range)
+    assert all(np.array_equal(a, b) for a, b in zip(same, f))      # equal ranges: no conversion
