@@ -304,6 +304,9 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
 __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
+#ifdef DTS_L7_STAGER_PRIO
+    __builtin_amdgcn_s_setprio(DTS_L7_STAGER_PRIO);     // diagnostic: the staging wave issues first
+#endif
     Stage7 Z;
     Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63);
 #pragma unroll
