@@ -649,13 +649,12 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
     const int64_t pa = P.a.pitch[dp], pb = P.b.pitch[dp];
 
     unsigned long long sse = 0;
-    for (int i = t; i < (kQTileBY + 1) * (kQTileBX + 1); i += kThreads) {
-        const int by = i / (kQTileBX + 1), bx = i - by * (kQTileBX + 1);
+    // the 4x4 block's sums by v_dot4_u32_u8 (four byte products per instruction;
+    // exact: ss <= 16 * 2 * 255^2)
+    auto block = [&](int bx, int by) {
         const int gx = bx0 + bx, gy = by0 + by;
         int4 r = make_int4(0, 0, 0, 0);
         if (gx < W4 && gy < H4) {
-            // the 4x4 block's sums by v_dot4_u32_u8 (four byte products per instruction;
-            // exact: ss <= 16 * 2 * 255^2)
             uint32_t s1 = 0, s2 = 0, ss = 0, s12 = 0;
 #pragma unroll
             for (int yy = 0; yy < 4; ++yy) {
@@ -671,6 +670,58 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
             if (bx < kQTileBX && by < kQTileBY) sse += (unsigned long long)((int)ss - 2 * (int)s12);
         }
         bs[by][bx] = r;
+    };
+    // 16-pixel runs of 4 blocks along a block row: one 16-byte load per row and image
+    // (interleaved chroma: two, de-interleaved by v_perm), then the apron column
+    constexpr int NQ = kQTileBX / 4;
+    const bool vec16 = (((uintptr_t)A | (uintptr_t)B | (uint64_t)pa | (uint64_t)pb) & 15) == 0;
+    for (int i = t; i < (kQTileBY + 1) * (NQ + 1); i += kThreads) {
+        const int by = i / (NQ + 1), qx = i - by * (NQ + 1);
+        if (qx == NQ) {
+            block(kQTileBX, by);
+            continue;
+        }
+        const int gx = bx0 + 4 * qx, gy = by0 + by;
+        if (gy >= H4 || gx + 3 >= W4 || !vec16) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) block(4 * qx + k, by);
+            continue;
+        }
+        uint32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, ss[4] = {0, 0, 0, 0}, s12[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int yy = 0; yy < 4; ++yy) {
+            const uint8_t *ra = A + (int64_t)(4 * gy + yy) * pa, *rb = B + (int64_t)(4 * gy + yy) * pb;
+            uint32_t va[4], vb[4];
+            if (!inter) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(ra + 4 * gx);
+                const uint4 y = *reinterpret_cast<const uint4 *>(rb + 4 * gx);
+                va[0] = x.x; va[1] = x.y; va[2] = x.z; va[3] = x.w;
+                vb[0] = y.x; vb[1] = y.y; vb[2] = y.z; vb[3] = y.w;
+            } else {
+                const uint4 x0 = *reinterpret_cast<const uint4 *>(ra + 8 * gx);
+                const uint4 x1 = *reinterpret_cast<const uint4 *>(ra + 8 * gx + 16);
+                const uint4 y0 = *reinterpret_cast<const uint4 *>(rb + 8 * gx);
+                const uint4 y1 = *reinterpret_cast<const uint4 *>(rb + 8 * gx + 16);
+                const uint32_t sel = comp ? 0x07050301u : 0x06040200u;
+                va[0] = perm(x0.y, x0.x, sel); va[1] = perm(x0.w, x0.z, sel);
+                va[2] = perm(x1.y, x1.x, sel); va[3] = perm(x1.w, x1.z, sel);
+                vb[0] = perm(y0.y, y0.x, sel); vb[1] = perm(y0.w, y0.z, sel);
+                vb[2] = perm(y1.y, y1.x, sel); vb[3] = perm(y1.w, y1.z, sel);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s1[k] = __builtin_amdgcn_udot4(va[k], 0x01010101u, s1[k], false);
+                s2[k] = __builtin_amdgcn_udot4(vb[k], 0x01010101u, s2[k], false);
+                ss[k] = __builtin_amdgcn_udot4(va[k], va[k], ss[k], false);
+                ss[k] = __builtin_amdgcn_udot4(vb[k], vb[k], ss[k], false);
+                s12[k] = __builtin_amdgcn_udot4(va[k], vb[k], s12[k], false);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bs[by][4 * qx + k] = make_int4((int)s1[k], (int)s2[k], (int)ss[k], (int)s12[k]);
+            if (by < kQTileBY) sse += (unsigned long long)((int)ss[k] - 2 * (int)s12[k]);
+        }
     }
     // pixels outside whole blocks, inside this tile's pixel rectangle
     {
