@@ -18,6 +18,8 @@
 //    when the block runs after granule q.  B byte 4d + i of lane (output row n,
 //    g) is the tap of source row 16 granule + 4 g + i.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "filters.h"
@@ -388,6 +390,9 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             u += cnt;
         }
     }
+    if (std::getenv("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
+        for (const Group7 &g : out.groups)
+            std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d\n", g.kind, g.X0, g.npc, g.nwaves);
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
     if (stager) ++out.waves;                               // one staging-only wave in every group
