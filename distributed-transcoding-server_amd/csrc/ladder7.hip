@@ -47,6 +47,9 @@
 #ifndef DTS_L7_DEFER_ST
 #define DTS_L7_DEFER_ST 0   // diagnostic: hold a row block's exchanged bytes and store them after the next H
 #endif
+#ifndef DTS_L7_SRC_AUX
+#define DTS_L7_SRC_AUX 0    // cache-policy bits of the source staging loads (diagnostic A/B)
+#endif
 #ifndef DTS_L7_NS
 #define DTS_L7_NS kL7Stages
 #endif
@@ -162,7 +165,8 @@ struct Stage7 {
             const int p = k >= npc ? 1 : 0, i = k - p * npc;
             const uint64_t src = (p ? sb[1] : sb[0]) + (uint64_t)(row * (p ? sp[1] : sp[0])) + lcol + 64u * (uint32_t)i;
             __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)src,
-                                             (__attribute__((address_space(3))) void *)(dst + 1024 * k), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void *)(dst + 1024 * k), 16, 0,
+                                             DTS_L7_SRC_AUX);
             ++ops;
         }
     }

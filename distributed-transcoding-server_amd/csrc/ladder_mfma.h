@@ -9,6 +9,9 @@
 #ifndef DTS_L6_ABLATE
 #define DTS_L6_ABLATE 0     // diagnostic builds only (ladder6.hip)
 #endif
+#ifndef DTS_NT_STORES
+#define DTS_NT_STORES 0     // 1: non-temporal output row stores (ladder7 A/B)
+#endif
 
 namespace dts {
 namespace {
@@ -49,12 +52,22 @@ __device__ __forceinline__ void put_row6(uint64_t rowp, int at, int room, const 
 {
     g_u8 *p = GP6(g_u8, rowp + (uint64_t)(int64_t)at);
     if (room >= NB) {
+#if DTS_NT_STORES
+        // diagnostic: non-temporal output stores (keep L2 / Infinity Cache for the source)
+        if (NB == 16)
+            __builtin_nontemporal_store((u32x4){w[0], w[1], w[2 % (NB / 4)], w[3 % (NB / 4)]}, GP6(g_u32x4, p));
+        else if (NB == 8)
+            __builtin_nontemporal_store((u32x2){w[0], w[1 % (NB / 4)]}, GP6(g_u32x2, p));
+        else
+            __builtin_nontemporal_store(w[0], GP6(g_u32, p));
+#else
         if (NB == 16)
             *GP6(g_u32x4, p) = (u32x4){w[0], w[1], w[2 % (NB / 4)], w[3 % (NB / 4)]};
         else if (NB == 8)
             *GP6(g_u32x2, p) = (u32x2){w[0], w[1 % (NB / 4)]};
         else
             *GP6(g_u32, p) = w[0];
+#endif
     } else {
         // the plane's last columns: predicated byte stores.  room goes through an empty asm
         // so the per-byte lane masks are formed here, not hoisted out of the walk (16 SGPR
