@@ -224,6 +224,31 @@ def test_device_path_plane_alignment(ctx, pad):
             assert planes_equal(got, want), f"pad {pad} frame {f} out {k}: {first_diff(got, want)}"
 
 
+V7_GEOMS = [
+    (128, 18, [(64, 9), (128, 18)]),                  # one granule row (chroma: 9 rows), 1:1 rendition
+    (256, 48, [(400, 90), (128, 24)]),                # upscale (several row blocks per granule) + 2:1
+    (1024, 16, [(512, 8), (341, 5)]),                 # a single source granule
+    (256, 1000, [(64, 900), (128, 250)]),             # tall: mild vertical, 4:1 / 2:1 horizontal
+    (4096, 64, [(1024, 16), (2730, 40)]),             # wide: many groups, 1.5:1
+    (640, 480, [(640, 480), (320, 240), (214, 160)]),  # 1:1 + ladder
+]
+
+
+@pytest.mark.parametrize("sw,sh,outs", V7_GEOMS)
+@pytest.mark.parametrize("method", [BIC, LAN, BIL, D.SCALE_AREA])
+def test_v7_geometries(ctx, ladder_kernel, sw, sh, outs, method):
+    """Plane widths that are multiples of 16 (k_ladder7's domain): single-granule
+    planes, upscales, tall / wide planes, 1:1 renditions; nv12 and yuv420p outputs,
+    bit-exact vs the oracle on every kernel."""
+    if ladder_kernel not in ("v7", "v6"):
+        pytest.skip("the v5 / v4 / v3 kernels are covered by the other geometry tests")
+    rng = np.random.default_rng(sw + 7 * sh + method)
+    frames = [random_frame(sw, sh, D.FMT_YUV420P, rng), D.synth_host(sw, sh, D.FMT_YUV420P, 0, 5, 3)]
+    run_and_check(ctx, sw, sh, D.FMT_YUV420P,
+                  [(w, h, D.FMT_NV12 if k % 2 == 0 else D.FMT_YUV420P, method) for k, (w, h) in enumerate(outs)],
+                  frames)
+
+
 @pytest.mark.parametrize("src_range,dst_range", [(0, 1), (1, 0)])
 @pytest.mark.parametrize("method", [BIC, LAN, BIL])
 def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method):
