@@ -33,10 +33,12 @@ __device__ __forceinline__ float pw(float x, float y)
 }
 
 // table t[0..kTmLutN] of (value, slope to the next entry) of a curve on [0, 1],
-// linearly interpolated: clamp (v_med3), scale, truncate / fract, one 8-byte LDS read, fma
-__device__ __forceinline__ float lut(const float2 *t, float v)
+// linearly interpolated; the argument arrives pre-scaled by kTmLutN (the scale is
+// folded into the producing FMA): clamp (v_med3), truncate / fract, one 8-byte LDS
+// read, fma
+__device__ __forceinline__ float lut(const float2 *t, float xn)
 {
-    const float x = __builtin_amdgcn_fmed3f(v, 0.f, 1.f) * (float)kTmLutN;
+    const float x = __builtin_amdgcn_fmed3f(xn, 0.f, (float)kTmLutN);
     const float2 e = t[(int)x];
     return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
 }
@@ -63,22 +65,27 @@ __device__ __forceinline__ int q8(float v)
     return (int)__builtin_amdgcn_fmed3f(v + 0.5f, 0.f, 255.f);
 }
 
-// One pixel: 10-bit Y, chroma (Cb', Cr' already centred) -> bt709 Y' / Cb' / Cr'
-__device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, int y10, float cb, float cr, float &Y,
-                                      float &Cb, float &Cr)
+// One pixel: 10-bit Y code, chroma (Cb', Cr' already centred) -> bt709 (Y', Cb', Cr').
+// The curve and the desaturation switch are template parameters: a branch per pixel
+// would keep the compiler from interleaving a thread's four pixels (LUT reads in flight).
+template <int MODE, bool DESAT>
+__device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, float y10, float2 c, float &Y,
+                                      float2 &C)
 {
     const float2 *pq = tl, *oetf = tl + kTmLutN + 1;          // pq already scaled by 10000 / npl
+    constexpr float N = (float)kTmLutN;
     constexpr float kr2 = 0.2627f, kb2 = 0.0593f, kg2 = 1.f - kr2 - kb2;
     constexpr float kr7 = 0.2126f, kb7 = 0.0722f, kg7 = 1.f - kr7 - kb7;
-    const float yy = (float)(y10 - 64) * (1.f / 876.f);
-    const float rp = yy + 2.f * (1.f - kr2) * cr, bp = yy + 2.f * (1.f - kb2) * cb;
-    const float gp = (yy - kr2 * rp - kb2 * bp) * (1.f / kg2);
+    // non-linear R'G'B' x N (the table scale)
+    const float yy = __builtin_fmaf(y10, N / 876.f, -64.f * N / 876.f);
+    const float rp = __builtin_fmaf(c.y, 2.f * (1.f - kr2) * N, yy), bp = __builtin_fmaf(c.x, 2.f * (1.f - kb2) * N, yy);
+    const float gp = __builtin_fmaf(-kb2 / kg2, bp, __builtin_fmaf(-kr2 / kg2, rp, yy * (1.f / kg2)));
     const float r0 = lut(pq, rp), g0 = lut(pq, gp), b0 = lut(pq, bp);
     float r = P.m[0] * r0 + P.m[1] * g0 + P.m[2] * b0;
     float g = P.m[3] * r0 + P.m[4] * g0 + P.m[5] * b0;
     float b = P.m[6] * r0 + P.m[7] * g0 + P.m[8] * b0;
     // vf_tonemap.c tonemap()
-    if (P.desat > 0.f) {
+    if (DESAT) {
         const float luma = kr7 * r + kg7 * g + kb7 * b;
         const float ob = fmaxf(luma - P.desat, 1e-6f) / fmaxf(luma, 1e-6f);
         r = r * (1.f - ob) + luma * ob;
@@ -87,7 +94,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     }
     const float sig0 = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     float sig = sig0;
-    switch (P.mode) {                                            // uniform over the launch
+    switch (MODE) {
     case DTS_TM_LINEAR: sig = sig * P.param / P.peak; break;
     case DTS_TM_GAMMA:
         sig = sig > 0.05f ? pw(sig / P.peak, 1.f / P.param) : sig * pw(0.05f / P.peak, 1.f / P.param) / 0.05f;
@@ -98,37 +105,48 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
-    const float k = sig * rcp(sig0);
+    const float k = sig * N * rcp(sig0);
     r = lut(oetf, r * k);
     g = lut(oetf, g * k);
     b = lut(oetf, b * k);
     Y = kr7 * r + kg7 * g + kb7 * b;
-    Cb = (b - Y) * (1.f / (2.f * (1.f - kb7)));
-    Cr = (r - Y) * (1.f / (2.f * (1.f - kr7)));
+    C = make_float2((b - Y) * (1.f / (2.f * (1.f - kb7))), (r - Y) * (1.f / (2.f * (1.f - kr7))));
 }
+
+__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)q8(__builtin_fmaf(219.f, Y, 16.f)); }
 
 } // namespace
 
 constexpr int kTmCRows = 8;                  // chroma rows per tile (16 luma rows)
 constexpr int kTmTiles = 8;                  // tiles per workgroup, walked top to bottom (one table load)
-constexpr int kTmLW = 130, kTmLH = 2 * kTmCRows + 2;   // luma tile + ring: 128 + 2 columns, 16 + 2 rows
+constexpr int kTmLH = 2 * kTmCRows + 2;      // luma rows of a tile + ring: 16 + 2
+constexpr int kTmLP = 132;                   // output-chroma row pitch: columns x0 - 1 .. x0 + 127 at 1 .. 129
 constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged: 64 + 2 columns, 8 + 2 rows
 
+// LDS: tables 16.4 KB + staged chroma 5.3 KB + output chroma 19 KB = 40.7 KB (four
+// workgroups per CU).  Tiles whose 128 x 16 luma block lies inside the picture (all
+// but the bottom / right edge tiles) take the block path: one 2 x 2 luma block per
+// thread, its chroma interpolated from the 3 x 2 staged samples it shares, two 4-byte
+// luma loads, 16-byte (Cb, Cr) x 2 LDS stores; edge tiles and the one-pixel ring take
+// the per-pixel path with the clamps.  The top ring row of tile t > 0 is the previous
+// tile's last luma row, carried in LDS rather than recomputed.
+template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
     __shared__ float2 tl[2 * (kTmLutN + 1)];
     __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
-    __shared__ float cb4[kTmLH][kTmLW], cr4[kTmLH][kTmLW];   // output Cb / Cr at full resolution
+    __shared__ __attribute__((aligned(16))) float2 cc[kTmLH][kTmLP];   // output (Cb, Cr) at full resolution
     const int t = threadIdx.x, f = blockIdx.z;
     const int cw = P.w >> 1, ch = P.h >> 1;
     const int cx0 = blockIdx.x * 64;
     const int x0 = 2 * cx0;
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
+    const bool a4 = ((P.src.data[0] + sf) & 3) == 0 && (P.src.pitch[0] & 3) == 0;
     for (int i = t; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
     for (int tile = 0; tile < kTmTiles; ++tile) {
     const int cy0 = (blockIdx.y * kTmTiles + tile) * kTmCRows, y0 = 2 * cy0;
     if (cy0 >= ch) break;
-    if (tile) __syncthreads();                      // the previous tile's chroma pass is done with cin / cb4
+    if (tile) __syncthreads();                      // the previous tile's chroma pass is done with cin / cc
     for (int i = t; i < kTmCH * kTmCW; i += 256) {
         const int r = i / kTmCW, c = i - r * kTmCW;
         const int sy = min(max(cy0 - 1 + r, 0), ch - 1), sx = min(max(cx0 - 1 + c, 0), cw - 1);
@@ -137,61 +155,103 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         cin[r][c] = make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f),
                                 (float)((int)(v >> 22) - 512) * (1.f / 896.f));
     }
+    if (tile)                                       // top ring row = the previous tile's luma row y0 - 1
+        for (int i = t; i < kTmLP; i += 256) cc[0][i] = cc[kTmLH - 2][i];
     __syncthreads();
     // one luma pixel (clamped into the picture): zimg bilinear up (chroma location left:
     // columns j, j + 1 at weights 1 - fx, fx; rows k, k2 at 3/4, 1/4) + the conversion
-    auto pix = [&](int xr, int yr, float &Yv, float &Cb, float &Cr) {
+    auto pix = [&](int xr, int yr, float &Yv, float2 &C) {
         const int x = min(max(xr, 0), P.w - 1), y = min(max(yr, 0), P.h - 1);
         const int ky = y >> 1, k = min(ky, ch - 1), k2 = min(max((y & 1) ? ky + 1 : ky - 1, 0), ch - 1);
         const int j = x >> 1, j1 = min(min(j + 1, cw - 1), cx0 + 64);   // (x even: j1 unused, fx = 0)
         const int lj = j - (cx0 - 1), lj1 = j1 - (cx0 - 1), lk = k - (cy0 - 1), lk2 = k2 - (cy0 - 1);
         const float fx = (x & 1) ? 0.5f : 0.f;
         const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
-        const float cb = 0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x));
-        const float cr = 0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y));
+        const float2 c = make_float2(0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x)),
+                                     0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y)));
         const int y10 = (int)(*reinterpret_cast<const uint16_t *>(P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0] +
                                                                   2 * x) >> 6);
-        pixel(P, tl, y10, cb, cr, Yv, Cb, Cr);
+        pixel<MODE, DESAT>(P, tl, (float)y10, c, Yv, C);
     };
-    // the tile's 2x2 blocks (luma written here) ...
-    for (int i = t; i < 64 * kTmCRows; i += 256) {
-        const int byl = i >> 6, bxl = i & 63;
-        float Yv[4], Cb[4], Cr[4];
+    if (a4 && x0 + 128 <= P.w && y0 + 16 <= P.h) {
+        // block path: the 2 x 2 luma block of chroma sample (cx0 + bxl, cy0 + byl); staged
+        // rows byl .. byl + 2 = chroma rows by - 1 .. by + 1, columns bxl + 1, bxl + 2 = bx, bx + 1
+        for (int i = t; i < 64 * kTmCRows; i += 256) {
+            const int byl = i >> 6, bxl = i & 63;
+            const float2 m0 = cin[byl][bxl + 1], m1 = cin[byl][bxl + 2];
+            const float2 a0 = cin[byl + 1][bxl + 1], a1 = cin[byl + 1][bxl + 2];
+            const float2 p0 = cin[byl + 2][bxl + 1], p1 = cin[byl + 2][bxl + 2];
+            const float2 ah = make_float2(a0.x + 0.5f * (a1.x - a0.x), a0.y + 0.5f * (a1.y - a0.y));
+            const float2 mh = make_float2(m0.x + 0.5f * (m1.x - m0.x), m0.y + 0.5f * (m1.y - m0.y));
+            const float2 ph = make_float2(p0.x + 0.5f * (p1.x - p0.x), p0.y + 0.5f * (p1.y - p0.y));
+            const float2 c[4] = {make_float2(0.75f * a0.x + 0.25f * m0.x, 0.75f * a0.y + 0.25f * m0.y),
+                                 make_float2(0.75f * ah.x + 0.25f * mh.x, 0.75f * ah.y + 0.25f * mh.y),
+                                 make_float2(0.75f * a0.x + 0.25f * p0.x, 0.75f * a0.y + 0.25f * p0.y),
+                                 make_float2(0.75f * ah.x + 0.25f * ph.x, 0.75f * ah.y + 0.25f * ph.y)};
+            const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
+            const uint64_t ys = P.src.data[0] + sf + (uint64_t)ya * P.src.pitch[0] + 2 * xa;
+            const uint32_t l0 = *reinterpret_cast<const uint32_t *>(ys);
+            const uint32_t l1 = *reinterpret_cast<const uint32_t *>(ys + P.src.pitch[0]);
+            const float y10[4] = {(float)__builtin_amdgcn_ubfe(l0, 6, 10), (float)(l0 >> 22),
+                                  (float)__builtin_amdgcn_ubfe(l1, 6, 10), (float)(l1 >> 22)};
+            float Yv[4];
+            float2 C[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pix(x0 + 2 * bxl + (q & 1), y0 + 2 * byl + (q >> 1), Yv[q], Cb[q], Cr[q]);
+            for (int q = 0; q < 4; ++q) pixel<MODE, DESAT>(P, tl, y10[q], c[q], Yv[q], C[q]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            cb4[1 + 2 * byl + (q >> 1)][1 + 2 * bxl + (q & 1)] = Cb[q];
-            cr4[1 + 2 * byl + (q >> 1)][1 + 2 * bxl + (q & 1)] = Cr[q];
-        }
-        const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
-        if (xa < P.w && ya < P.h) {                         // w, h even: the whole block is inside
+            for (int r = 0; r < 2; ++r)
+                *reinterpret_cast<float4 *>(&cc[1 + 2 * byl + r][2 + 2 * bxl]) =
+                    make_float4(C[2 * r].x, C[2 * r].y, C[2 * r + 1].x, C[2 * r + 1].y);
             const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
-            *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8(16.f + 219.f * Yv[0]) | (q8(16.f + 219.f * Yv[1]) << 8));
-            *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) =
-                (uint16_t)(q8(16.f + 219.f * Yv[2]) | (q8(16.f + 219.f * Yv[3]) << 8));
+            *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8));
+            *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) = (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8));
+        }
+    } else {
+        // per-pixel path (edge tiles): out-of-picture blocks keep the clamped values the
+        // 2:1 filter of the last chroma row / column reads
+        for (int i = t; i < 64 * kTmCRows; i += 256) {
+            const int byl = i >> 6, bxl = i & 63;
+            float Yv[4];
+            float2 C[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pix(x0 + 2 * bxl + (q & 1), y0 + 2 * byl + (q >> 1), Yv[q], C[q]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cc[1 + 2 * byl + (q >> 1)][2 + 2 * bxl + (q & 1)] = C[q];
+            const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
+            if (xa < P.w && ya < P.h) {                     // w, h even: the whole block is inside
+                const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
+                *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8));
+                *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) = (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8));
+            }
         }
     }
-    // ... and the one-pixel ring (chroma only): rows y0 - 1 and y0 + 16 (130 pixels
-    // each), columns x0 - 1 and x0 + 128 of the 16 rows between
-    for (int i = t; i < 2 * kTmLW + 2 * 2 * kTmCRows; i += 256) {
-        int lx, ly;
-        if (i < 2 * kTmLW) {
-            ly = i < kTmLW ? 0 : kTmLH - 1;
-            lx = i < kTmLW ? i : i - kTmLW;
-        } else {
-            const int k = i - 2 * kTmLW;
-            ly = 1 + (k >> 1);
-            lx = (k & 1) ? kTmLW - 1 : 0;
+    // ... and the ring the 2:1 filter reads (chroma only): rows y0 - 1 (first tile only)
+    // and y0 + 16, columns x0 - 1 .. x0 + 127, and column x0 - 1 of the 16 rows between
+    {
+        constexpr int kRow = 129;
+        const int top = tile ? 0 : kRow;
+        for (int i = t; i < top + kRow + 2 * kTmCRows; i += 256) {
+            int lx, ly;
+            if (i < top) {
+                ly = 0;
+                lx = i;
+            } else if (i < top + kRow) {
+                ly = kTmLH - 1;
+                lx = i - top;
+            } else {
+                ly = 1 + (i - top - kRow);
+                lx = 0;
+            }
+            float Yv;
+            float2 C;
+            pix(x0 - 1 + lx, y0 - 1 + ly, Yv, C);
+            cc[ly][1 + lx] = C;
         }
-        float Yv, Cb, Cr;
-        pix(x0 - 1 + lx, y0 - 1 + ly, Yv, Cb, Cr);
-        cb4[ly][lx] = Cb;
-        cr4[ly][lx] = Cr;
     }
     __syncthreads();
-    // chroma 2:1 (location left): columns 2 bx - 1 .. 2 bx + 1, rows 2 by - 1 .. 2 by + 2
-    constexpr float wx[3] = {0.25f, 0.5f, 0.25f}, wy[4] = {0.125f, 0.375f, 0.375f, 0.125f};
+    // chroma 2:1 (location left): columns 2 bx - 1 .. 2 bx + 1 (indices 2 rx + 1 .. 2 rx + 3),
+    // rows 2 by - 1 .. 2 by + 2 (ring row 0 = y0 - 1)
+    constexpr float wy[4] = {0.125f, 0.375f, 0.375f, 0.125f};
     for (int i = t; i < 64 * kTmCRows; i += 256) {
         const int ry = i >> 6, rx = i & 63;
         const int bx = cx0 + rx, by = cy0 + ry;
@@ -199,13 +259,10 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         float sb = 0.f, sr = 0.f;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            const int ly = 2 * ry + a;                   // luma row 2 by - 1 + a, ring row 0 = y0 - 1
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                const int lx = 2 * rx + b;               // luma column 2 bx - 1 + b, ring column 0 = x0 - 1
-                sb += wy[a] * wx[b] * cb4[ly][lx];
-                sr += wy[a] * wx[b] * cr4[ly][lx];
-            }
+            const float2 l = cc[2 * ry + a][2 * rx + 1];
+            const float4 mr = *reinterpret_cast<const float4 *>(&cc[2 * ry + a][2 * rx + 2]);
+            sb += wy[a] * (0.25f * l.x + 0.5f * mr.x + 0.25f * mr.z);
+            sr += wy[a] * (0.25f * l.y + 0.5f * mr.y + 0.25f * mr.w);
         }
         const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
         if (P.dst_fmt == DTS_FMT_NV12) {
@@ -223,7 +280,23 @@ hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s)
 {
     const int rows = kTmCRows * kTmTiles;
     const dim3 grid((unsigned)((p.w / 2 + 63) / 64), (unsigned)((p.h / 2 + rows - 1) / rows), (unsigned)p.nframes);
-    hipLaunchKernelGGL(k_tonemap, grid, dim3(256), 0, s, p);
+    const bool ds = p.desat > 0.f;
+#define DTS_TM_CASE(m)                                                                                               \
+    case m:                                                                                                          \
+        if (ds) hipLaunchKernelGGL((k_tonemap<m, true>), grid, dim3(256), 0, s, p);                                 \
+        else hipLaunchKernelGGL((k_tonemap<m, false>), grid, dim3(256), 0, s, p);                                   \
+        break;
+    switch (p.mode) {
+    DTS_TM_CASE(DTS_TM_NONE)
+    DTS_TM_CASE(DTS_TM_LINEAR)
+    DTS_TM_CASE(DTS_TM_GAMMA)
+    DTS_TM_CASE(DTS_TM_CLIP)
+    DTS_TM_CASE(DTS_TM_REINHARD)
+    DTS_TM_CASE(DTS_TM_HABLE)
+    DTS_TM_CASE(DTS_TM_MOBIUS)
+    default: return hipErrorInvalidValue;
+    }
+#undef DTS_TM_CASE
     return hipGetLastError();
 }
 
