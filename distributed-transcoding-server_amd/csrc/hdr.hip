@@ -22,6 +22,13 @@
 // tolerance.
 #include "dts_internal.h"
 
+#ifndef DTS_TM_OETF_POW
+#define DTS_TM_OETF_POW 0   // 1: BT.709 OETF by v_log / v_exp instead of the LDS table (A/B knob)
+#endif
+#ifndef DTS_TM_UNROLL
+#define DTS_TM_UNROLL 0     // 1: both block iterations of a lane unrolled (8 pixels in flight; A/B knob)
+#endif
+
 namespace dts {
 
 namespace {
@@ -41,6 +48,14 @@ __device__ __forceinline__ float lut(const float2 *t, float xn)
     const float x = __builtin_amdgcn_fmed3f(xn, 0.f, (float)kTmLutN);
     const float2 e = t[(int)x];
     return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
+}
+
+// BT.709 OETF on [0, 1] (the host table's curve, api.cpp tonemap_luts)
+__device__ __forceinline__ float oetf709(float v)
+{
+    const float x = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+    const float p = __builtin_fmaf(1.09929682680944f, pw(x, 0.45f), -0.09929682680944f);
+    return x < 0.018053968510807f ? 4.5f * x : p;
 }
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -105,10 +120,18 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
+#if DTS_TM_OETF_POW
+    (void)oetf;
+    const float k = sig * rcp(sig0);
+    r = oetf709(r * k);
+    g = oetf709(g * k);
+    b = oetf709(b * k);
+#else
     const float k = sig * N * rcp(sig0);
     r = lut(oetf, r * k);
     g = lut(oetf, g * k);
     b = lut(oetf, b * k);
+#endif
     Y = kr7 * r + kg7 * g + kb7 * b;
     C = make_float2((b - Y) * (1.f / (2.f * (1.f - kb7))), (r - Y) * (1.f / (2.f * (1.f - kr7))));
 }
@@ -120,11 +143,11 @@ __device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)q8(__builtin
 constexpr int kTmCRows = 8;                  // chroma rows per tile (16 luma rows)
 constexpr int kTmTiles = 8;                  // tiles per workgroup, walked top to bottom (one table load)
 constexpr int kTmLH = 2 * kTmCRows + 2;      // luma rows of a tile + ring: 16 + 2
-constexpr int kTmLP = 132;                   // output-chroma row pitch: columns x0 - 1 .. x0 + 127 at 1 .. 129
+constexpr int kTmLP = 130;                   // output-chroma row pitch (16-B rows): columns x0 - 1 .. x0 + 127 at 1 .. 129
 constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged: 64 + 2 columns, 8 + 2 rows
 
-// LDS: tables 16.4 KB + staged chroma 5.3 KB + output chroma 19 KB = 40.7 KB (four
-// workgroups per CU).  Tiles whose 128 x 16 luma block lies inside the picture (all
+// LDS: tables 16.4 KB + staged chroma 5.3 KB + output chroma 18.7 KB = 40.4 KB (four
+// workgroups per CU; 32.2 KB, five, with DTS_TM_OETF_POW).  Tiles whose 128 x 16 luma block lies inside the picture (all
 // but the bottom / right edge tiles) take the block path: one 2 x 2 luma block per
 // thread, its chroma interpolated from the 3 x 2 staged samples it shares, two 4-byte
 // luma loads, 16-byte (Cb, Cr) x 2 LDS stores; edge tiles and the one-pixel ring take
@@ -133,7 +156,8 @@ constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged:
 template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
-    __shared__ float2 tl[2 * (kTmLutN + 1)];
+    constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
+    __shared__ float2 tl[kTabs * (kTmLutN + 1)];
     __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
     __shared__ __attribute__((aligned(16))) float2 cc[kTmLH][kTmLP];   // output (Cb, Cr) at full resolution
     const int t = threadIdx.x, f = blockIdx.z;
@@ -142,7 +166,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     const int x0 = 2 * cx0;
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
     const bool a4 = ((P.src.data[0] + sf) & 3) == 0 && (P.src.pitch[0] & 3) == 0;
-    for (int i = t; i < 2 * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
+    for (int i = t; i < kTabs * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
     for (int tile = 0; tile < kTmTiles; ++tile) {
     const int cy0 = (blockIdx.y * kTmTiles + tile) * kTmCRows, y0 = 2 * cy0;
     if (cy0 >= ch) break;
@@ -176,7 +200,11 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     if (a4 && x0 + 128 <= P.w && y0 + 16 <= P.h) {
         // block path: the 2 x 2 luma block of chroma sample (cx0 + bxl, cy0 + byl); staged
         // rows byl .. byl + 2 = chroma rows by - 1 .. by + 1, columns bxl + 1, bxl + 2 = bx, bx + 1
-        for (int i = t; i < 64 * kTmCRows; i += 256) {
+#if DTS_TM_UNROLL
+#pragma unroll
+#endif
+        for (int kb = 0; kb < 64 * kTmCRows / 256; ++kb) {
+            const int i = t + 256 * kb;
             const int byl = i >> 6, bxl = i & 63;
             const float2 m0 = cin[byl][bxl + 1], m1 = cin[byl][bxl + 2];
             const float2 a0 = cin[byl + 1][bxl + 1], a1 = cin[byl + 1][bxl + 2];
