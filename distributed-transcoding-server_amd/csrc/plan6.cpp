@@ -304,16 +304,73 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         if (us.empty()) return false;
         // window start of a unit (its first tile's x0) orders the plane's units left to right;
         // by_rung: groups of one rendition each (their waves do the same work per granule)
+        // (diagnostic DTS_L7_SORT: 1 = by window centre, 2 = by window end)
+        const char *se = std::getenv("DTS_L7_SORT");
+        const int sort_key = se ? std::atoi(se) : 0;
+        auto wkey = [&](const Unit6 &w) {
+            if (!sort_key) return 2 * w.x0[0];
+            const int hkb = l6_hkb(w.variant), ct = l6_ct(w.variant);
+            int x1 = 0;
+            for (int c = 0; c < ct; ++c)
+                if (16 * c < w.ncols) x1 = std::max(x1, w.x0[c] + 64 * hkb);
+            return sort_key == 1 ? w.x0[0] + x1 : 2 * x1;
+        };
         std::stable_sort(us.begin(), us.end(), [&](const Unit6 &a, const Unit6 &b) {
             if (by_rung && a.rung != b.rung) return a.rung < b.rung;
-            return a.x0[0] < b.x0[0];
+            return wkey(a) < wkey(b);
         });
+        // window extent [wa, wz) of every unit (the source columns its tiles' K windows cover)
+        std::vector<int> wa(us.size()), wz(us.size());
+        for (size_t i = 0; i < us.size(); ++i) {
+            const Unit6 &w = us[i];
+            const int hkb = l6_hkb(w.variant), ct = l6_ct(w.variant);
+            wa[i] = 1 << 30;
+            wz[i] = 0;
+            for (int c = 0; c < ct; ++c)
+                if (16 * c < w.ncols) {
+                    wa[i] = std::min(wa[i], w.x0[c]);
+                    wz[i] = std::max(wz[i], w.x0[c] + 64 * hkb);
+                }
+        }
         // runs of units grouped together: the whole plane kind, or one rendition
         std::vector<std::pair<int, int>> runs;
+        const char *dpe = std::getenv("DTS_L7_DP");
+        const int dp_slack = dpe ? std::atoi(dpe) : 0;
         for (int a = 0, n = (int)us.size(); a < n;) {
             int z = a + 1;
             while (z < n && (!by_rung || us[z].rung == us[a].rung)) ++z;
             const int ng = (z - a + wmax - 1) / wmax;
+            if (dp_slack > 0 && ng > 1) {
+                // diagnostic (DTS_L7_DP=s): the same number of groups, sizes in [wmax - s, wmax],
+                // boundaries chosen to minimise the staged pieces (sum of npc) by dynamic programming
+                const int m = z - a, lo = std::max(1, wmax - dp_slack);
+                const int inf = 1 << 29;
+                std::vector<std::vector<int>> best(ng + 1, std::vector<int>(m + 1, inf)), from(ng + 1, std::vector<int>(m + 1, -1));
+                best[0][0] = 0;
+                for (int g = 1; g <= ng; ++g)
+                    for (int e = 1; e <= m; ++e)
+                        for (int sz = lo; sz <= std::min(wmax, e); ++sz) {
+                            const int b0 = e - sz;
+                            if (best[g - 1][b0] >= inf) continue;
+                            int x0 = 1 << 30, x1 = 0;
+                            for (int i = b0; i < e; ++i) {
+                                x0 = std::min(x0, wa[a + i]);
+                                x1 = std::max(x1, wz[a + i]);
+                            }
+                            const int cost = best[g - 1][b0] + (x1 - (x0 & ~15) + 63) / 64;
+                            if (cost < best[g][e]) {
+                                best[g][e] = cost;
+                                from[g][e] = b0;
+                            }
+                        }
+                if (best[ng][m] < inf) {
+                    std::vector<int> sizes;
+                    for (int g = ng, e = m; g > 0; e = from[g][e], --g) sizes.push_back(e - from[g][e]);
+                    for (int gi = ng - 1; gi >= 0; --gi) runs.push_back({sizes[gi], 0});
+                    a = z;
+                    continue;
+                }
+            }
             for (int gi = 0; gi < ng; ++gi) runs.push_back({(z - a) / ng + (gi < (z - a) % ng ? 1 : 0), 0});
             a = z;
         }
