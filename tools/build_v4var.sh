@@ -1,0 +1,14 @@
+#!/bin/bash
+# Diagnostic builds of libdts with k_ladder4 knobs -> lib/libdts_<name>.so, for
+# tools/ab_libs.sh.  Args: name=DEFINES.  Never used by tests or bench defaults.
+set -e
+cd "$(dirname "$0")/../distributed-transcoding-server_amd"
+make -s lib/libdts.so
+OBJS="build/api.o build/filters.o build/plan5.o build/plan6.o build/kernels.o build/ladder5.o build/ladder6.o build/ladder7.o build/hdr.o build/deint.o"
+for a in "$@"; do
+  n=${a%%=*}; d=${a#*=}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $d -c csrc/ladder4.hip -o build/ladder4_$n.o \
+      -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "VGPRs:|Occupancy|Spill" | head -4 | sed "s/^.*remark: */$n: /"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libdts_$n.so $OBJS build/ladder4_$n.o \
+      -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdts.so
+done
