@@ -19,6 +19,9 @@ namespace dts {
 #define DTS_YADIF_ROWS 16
 #endif
 constexpr int kYadifRows = DTS_YADIF_ROWS;     // output rows per workgroup tile
+#ifndef DTS_YADIF_SLIDE
+#define DTS_YADIF_SLIDE 1   // interior tiles: sliding row window (0: every row loads its whole neighbourhood)
+#endif
 
 namespace {
 
@@ -174,6 +177,102 @@ __device__ __forceinline__ void yadif_quad(const YadifParams &P, int p, int w, i
     }
 }
 
+// A lane's 4 columns over the rows [y0, y1) of a tile whose interpolated rows all
+// lie in 2 <= y <= h - 3 (no reflected references, no forced mode 2): the rows an
+// interpolated row reads slide down by two rows per step, so after the first one
+// each step loads only the new rows -- cur / prev / next row y + 3 and prev2 /
+// next2 row y + 4 (or y + 2) for the next step, issued before this row's
+// arithmetic -- 7 dwords instead of 12 or 16, and the kept rows are stored from
+// the window's cur rows (no load).
+__device__ __forceinline__ void yadif_tile_slide(const YadifParams &P, int p, int y0, int y1, int x0, int o, int i,
+                                                 int ip, int in, int is_second)
+{
+    const int64_t pitch = P.seq.pitch[p], dpitch = P.dst.pitch[p];
+    const uint64_t col = P.seq.data[p] + x0;
+    const uint8_t *cur = reinterpret_cast<const uint8_t *>(col + (uint64_t)i * P.seq.fstride);
+    const uint8_t *prev = reinterpret_cast<const uint8_t *>(col + (uint64_t)ip * P.seq.fstride);
+    const uint8_t *next = reinterpret_cast<const uint8_t *>(col + (uint64_t)in * P.seq.fstride);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(P.dst.data[p] + (uint64_t)o * P.dst.fstride + x0);
+    const int td_parity = P.tff ^ !is_second;
+    const int parity = td_parity ^ P.tff;
+    const uint8_t *prev2 = parity ? prev : cur, *next2 = parity ? cur : next;
+    const int mode = P.mode;
+    const bool far = !(mode & 2);
+    // interpolated rows y = ya, ya + 2, ...; the kept rows between them are the
+    // window's cur rows (y - 1 / y + 1), stored from registers
+    int y = y0 + (((y0 ^ td_parity) & 1) ? 0 : 1);
+    AtReg a;
+    a.p2m = a.p2p = a.n2m = a.n2p = 0;
+    {
+        const int64_t r = (int64_t)y * pitch;
+        a.cm[0] = ld32(cur + r - pitch - 4);
+        a.cm[1] = ld32(cur + r - pitch);
+        a.cm[2] = ld32(cur + r - pitch + 4);
+        a.cp[0] = ld32(cur + r + pitch - 4);
+        a.cp[1] = ld32(cur + r + pitch);
+        a.cp[2] = ld32(cur + r + pitch + 4);
+        a.pm = ld32(prev + r - pitch);
+        a.pp = ld32(prev + r + pitch);
+        a.nm = ld32(next + r - pitch);
+        a.np = ld32(next + r + pitch);
+        a.p2 = ld32(prev2 + r);
+        a.n2 = ld32(next2 + r);
+        if (far) {
+            a.p2m = ld32(prev2 + r - 2 * pitch);
+            a.p2p = ld32(prev2 + r + 2 * pitch);
+            a.n2m = ld32(next2 + r - 2 * pitch);
+            a.n2p = ld32(next2 + r + 2 * pitch);
+        }
+    }
+    if (y > y0) *reinterpret_cast<uint32_t *>(dst + (int64_t)y0 * dpitch) = a.cm[1];
+    for (; y < y1; y += 2) {
+        // the next step's new rows are in flight while this row is computed
+        const bool more = y + 2 < y1;
+        uint32_t c0 = 0, c1 = 0, c2 = 0, pq = 0, nq = 0, p2q = 0, n2q = 0;
+        if (more) {
+            const int64_t r3 = (int64_t)(y + 3) * pitch, r4 = (int64_t)(far ? y + 4 : y + 2) * pitch;
+            c0 = ld32(cur + r3 - 4);
+            c1 = ld32(cur + r3);
+            c2 = ld32(cur + r3 + 4);
+            pq = ld32(prev + r3);
+            nq = ld32(next + r3);
+            p2q = ld32(prev2 + r4);
+            n2q = ld32(next2 + r4);
+        }
+        uint32_t out = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                      // 4 <= x < w - 4: never an edge pixel
+            a.i = k;
+            out |= (uint32_t)yadif_px(a, mode, true) << (8 * k);
+        }
+        *reinterpret_cast<uint32_t *>(dst + (int64_t)y * dpitch) = out;
+        if (y + 1 < y1) *reinterpret_cast<uint32_t *>(dst + (int64_t)(y + 1) * dpitch) = a.cp[1];
+        if (more) {                                        // slide by two rows
+            a.cm[0] = a.cp[0];
+            a.cm[1] = a.cp[1];
+            a.cm[2] = a.cp[2];
+            a.cp[0] = c0;
+            a.cp[1] = c1;
+            a.cp[2] = c2;
+            a.pm = a.pp;
+            a.pp = pq;
+            a.nm = a.np;
+            a.np = nq;
+            if (far) {
+                a.p2m = a.p2;
+                a.p2 = a.p2p;
+                a.p2p = p2q;
+                a.n2m = a.n2;
+                a.n2 = a.n2p;
+                a.n2p = n2q;
+            } else {
+                a.p2 = p2q;
+                a.n2 = n2q;
+            }
+        }
+    }
+}
+
 // One workgroup = a 1024-pixel x kYadifRows tile of one plane of one output
 // frame, walked row by row: the 5-row neighbourhoods of consecutive rows
 // overlap, so the tile's input rows come from HBM once and are re-read from
@@ -197,8 +296,14 @@ __global__ void __launch_bounds__(256) k_yadif(const YadifParams P)
     const int w = p ? cw : P.w, h = p ? ch : P.h;
     const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x);
     if (x0 >= w) return;
-    const int y1 = min(h, (rb + 1) * kYadifRows);
-    for (int y = rb * kYadifRows; y < y1; ++y) yadif_quad(P, p, w, h, y, x0, o, i, ip, in, is_second);
+    const int y0 = rb * kYadifRows, y1 = min(h, y0 + kYadifRows);
+#if DTS_YADIF_SLIDE
+    if (P.aligned && x0 >= 4 && x0 + 8 <= w && y0 >= 2 && y1 <= h - 2) {
+        yadif_tile_slide(P, p, y0, y1, x0, o, i, ip, in, is_second);
+        return;
+    }
+#endif
+    for (int y = y0; y < y1; ++y) yadif_quad(P, p, w, h, y, x0, o, i, ip, in, is_second);
 }
 
 hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s)
