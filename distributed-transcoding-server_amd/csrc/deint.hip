@@ -111,7 +111,12 @@ struct AtReg {
     }
 };
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+// global (not flat) loads / stores: the pointers are built from integers, so the
+// compiler cannot infer the address space itself
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *(g_cu32 *)(uintptr_t)p; }
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *(g_u32 *)(uintptr_t)p = v; }
 
 } // namespace
 
@@ -128,7 +133,7 @@ __device__ __forceinline__ void yadif_quad(const YadifParams &P, int p, int w, i
     const bool fast = P.aligned && x0 >= 4 && x0 + 8 <= w;
     if (!((y ^ td_parity) & 1)) {                          // the kept field: copy
         if (P.aligned && x0 + 4 <= w) {
-            *reinterpret_cast<uint32_t *>(dst) = ld32(cur);
+            st32(dst, ld32(cur));
         } else {
             for (int k = 0; k < 4 && x0 + k < w; ++k) dst[k] = cur[k];
         }
@@ -167,7 +172,7 @@ __device__ __forceinline__ void yadif_quad(const YadifParams &P, int p, int w, i
             a.i = k;
             out |= (uint32_t)yadif_px(a, mode, true) << (8 * k);
         }
-        *reinterpret_cast<uint32_t *>(dst) = out;
+        st32(dst, out);
         return;
     }
     for (int k = 0; k < 4 && x0 + k < w; ++k) {
@@ -224,7 +229,7 @@ __device__ __forceinline__ void yadif_tile_slide(const YadifParams &P, int p, in
             a.n2p = ld32(next2 + r + 2 * pitch);
         }
     }
-    if (y > y0) *reinterpret_cast<uint32_t *>(dst + (int64_t)y0 * dpitch) = a.cm[1];
+    if (y > y0) st32(dst + (int64_t)y0 * dpitch, a.cm[1]);
     for (; y < y1; y += 2) {
         // the next step's new rows are in flight while this row is computed
         const bool more = y + 2 < y1;
@@ -245,8 +250,8 @@ __device__ __forceinline__ void yadif_tile_slide(const YadifParams &P, int p, in
             a.i = k;
             out |= (uint32_t)yadif_px(a, mode, true) << (8 * k);
         }
-        *reinterpret_cast<uint32_t *>(dst + (int64_t)y * dpitch) = out;
-        if (y + 1 < y1) *reinterpret_cast<uint32_t *>(dst + (int64_t)(y + 1) * dpitch) = a.cp[1];
+        st32(dst + (int64_t)y * dpitch, out);
+        if (y + 1 < y1) st32(dst + (int64_t)(y + 1) * dpitch, a.cp[1]);
         if (more) {                                        // slide by two rows
             a.cm[0] = a.cp[0];
             a.cm[1] = a.cp[1];

@@ -50,6 +50,7 @@ __device__ __forceinline__ float lut(const float2 *t, float xn)
     return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
 }
 
+#if DTS_TM_OETF_POW
 // BT.709 OETF on [0, 1] (the host table's curve, api.cpp tonemap_luts)
 __device__ __forceinline__ float oetf709(float v)
 {
@@ -57,6 +58,11 @@ __device__ __forceinline__ float oetf709(float v)
     const float p = __builtin_fmaf(1.09929682680944f, pw(x, 0.45f), -0.09929682680944f);
     return x < 0.018053968510807f ? 4.5f * x : p;
 }
+#endif
+
+// global (not flat) loads / stores at integer addresses
+template <class T> __device__ __forceinline__ T gld(uint64_t a) { return *(__attribute__((address_space(1))) const T *)a; }
+template <class T> __device__ __forceinline__ void gst(uint64_t a, T v) { *(__attribute__((address_space(1))) T *)a = v; }
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
@@ -174,7 +180,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     for (int i = t; i < kTmCH * kTmCW; i += 256) {
         const int r = i / kTmCW, c = i - r * kTmCW;
         const int sy = min(max(cy0 - 1 + r, 0), ch - 1), sx = min(max(cx0 - 1 + c, 0), cw - 1);
-        const uint32_t v = *reinterpret_cast<const uint32_t *>(P.src.data[1] + sf + (uint64_t)sy * P.src.pitch[1] +
+        const uint32_t v = gld<uint32_t>(P.src.data[1] + sf + (uint64_t)sy * P.src.pitch[1] +
                                                                 4 * sx);
         cin[r][c] = make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f),
                                 (float)((int)(v >> 22) - 512) * (1.f / 896.f));
@@ -193,7 +199,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
         const float2 c = make_float2(0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x)),
                                      0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y)));
-        const int y10 = (int)(*reinterpret_cast<const uint16_t *>(P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0] +
+        const int y10 = (int)(gld<uint16_t>(P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0] +
                                                                   2 * x) >> 6);
         pixel<MODE, DESAT>(P, tl, (float)y10, c, Yv, C);
     };
@@ -218,8 +224,8 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
                                  make_float2(0.75f * ah.x + 0.25f * ph.x, 0.75f * ah.y + 0.25f * ph.y)};
             const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
             const uint64_t ys = P.src.data[0] + sf + (uint64_t)ya * P.src.pitch[0] + 2 * xa;
-            const uint32_t l0 = *reinterpret_cast<const uint32_t *>(ys);
-            const uint32_t l1 = *reinterpret_cast<const uint32_t *>(ys + P.src.pitch[0]);
+            const uint32_t l0 = gld<uint32_t>(ys);
+            const uint32_t l1 = gld<uint32_t>(ys + P.src.pitch[0]);
             const float y10[4] = {(float)__builtin_amdgcn_ubfe(l0, 6, 10), (float)(l0 >> 22),
                                   (float)__builtin_amdgcn_ubfe(l1, 6, 10), (float)(l1 >> 22)};
             float Yv[4];
@@ -231,8 +237,8 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
                 *reinterpret_cast<float4 *>(&cc[1 + 2 * byl + r][2 + 2 * bxl]) =
                     make_float4(C[2 * r].x, C[2 * r].y, C[2 * r + 1].x, C[2 * r + 1].y);
             const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
-            *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8));
-            *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) = (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8));
+            gst<uint16_t>(yd, (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)));
+            gst<uint16_t>(yd + P.dst.pitch[0], (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8)));
         }
     } else {
         // per-pixel path (edge tiles): out-of-picture blocks keep the clamped values the
@@ -248,8 +254,8 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
             if (xa < P.w && ya < P.h) {                     // w, h even: the whole block is inside
                 const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
-                *reinterpret_cast<uint16_t *>(yd) = (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8));
-                *reinterpret_cast<uint16_t *>(yd + P.dst.pitch[0]) = (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8));
+                gst<uint16_t>(yd, (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)));
+                gst<uint16_t>(yd + P.dst.pitch[0], (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8)));
             }
         }
     }
@@ -294,11 +300,10 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         }
         const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
         if (P.dst_fmt == DTS_FMT_NV12) {
-            *reinterpret_cast<uint16_t *>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx) =
-                (uint16_t)(u | (v << 8));
+            gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx, (uint16_t)(u | (v << 8)));
         } else {
-            *reinterpret_cast<uint8_t *>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + bx) = (uint8_t)u;
-            *reinterpret_cast<uint8_t *>(P.dst.data[2] + df + (uint64_t)by * P.dst.pitch[2] + bx) = (uint8_t)v;
+            gst<uint8_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + bx, (uint8_t)u);
+            gst<uint8_t>(P.dst.data[2] + df + (uint64_t)by * P.dst.pitch[2] + bx, (uint8_t)v);
         }
     }
     }
