@@ -58,7 +58,7 @@ WORKLOADS = {
              "desc": "cfg2: 4K60 8-bit yuv420p -> 1080p/720p/854x480 nv12 ABR ladder, bicubic "
                      "(SWS_BITEXACT|ACCURATE_RND semantics), one fused launch per batch"},
     "cfg3": {"src": (SRC_W, SRC_H, D.FMT_P010LE), "outs": [(1920, 1080, D.FMT_YUV420P, D.SCALE_BICUBIC)],
-             "tonemap": {"mode": D.TM_HABLE, "desat": 0.0, "peak": 0.0, "npl": 100.0}, "quality": False,
+             "tonemap": {"mode": D.TM_HABLE, "desat": 2.0, "peak": 0.0, "npl": 100.0}, "quality": False,
              "desc": "cfg3: 4K60 10-bit p010 HDR10 (PQ, bt2020nc) -> SDR bt709 8-bit 1080p yuv420p: bit-exact "
                      "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB)"},
     "cfg4": {"src": (7680, 4320, D.FMT_YUV420P), "outs": [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)],

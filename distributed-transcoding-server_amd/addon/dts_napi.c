@@ -198,7 +198,7 @@ static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
             s->hdr_to_sdr = 1;
             if (get_i32(env, tm, "mode", DTS_TM_HABLE, &s->tonemap.mode) ||
                 get_f64(env, tm, "param", NAN, &s->tonemap.param) ||
-                get_f64(env, tm, "desat", 0.0, &s->tonemap.desat) ||
+                get_f64(env, tm, "desat", 2.0, &s->tonemap.desat) /* vf_tonemap default */ ||
                 get_f64(env, tm, "peak", 0.0, &s->tonemap.peak) || get_f64(env, tm, "npl", 100.0, &s->tonemap.npl))
                 return -1;
         }

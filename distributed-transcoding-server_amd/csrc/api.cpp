@@ -50,6 +50,10 @@ struct dts_ctx {
     int last_hip = 0;
     hipStream_t stream[2] = {nullptr, nullptr};
     QScratch qs;                               // dts_quality_run_device
+    // dts_quality_run_host: one batch of both frame sets + its records, kept across calls
+    // (the worker scores every segment of every rendition: no allocation per call)
+    uint8_t *hq = nullptr;
+    size_t hq_bytes = 0;
     // graphs hold a reference: the context outlives every graph made on it,
     // whichever of dts_ctx_destroy / dts_graph_destroy runs first
     std::atomic<int> refs{1};
@@ -507,12 +511,30 @@ int l7_waves()
     return std::min(std::max(w, 1), kL7MaxWaves);
 }
 
-// source stages per k_ladder7 group (DTS_L7_NS: diagnostic kernel builds compiled with
-// another DTS_L7_NS; the default build's kernel stages kL7Stages granules)
+// Staging batches per k_ladder7 group and granules per batch: what the linked kernel was
+// compiled with (ladder7.hip NS7 / PB7; diagnostic builds change them with -DDTS_L7_NS /
+// -DDTS_L7_PAIR).  The planner sizes the stage buffers and the V fragment slots from these,
+// so DTS_L7_NS / DTS_L7_PB may only restate them: a graph asked for any other value is
+// refused (l7_knobs_ok), never planned for a kernel that would overrun its slots.
 int l7_stages()
 {
-    const char *f = std::getenv("DTS_L7_NS");
-    return f ? std::atoi(f) : kL7Stages;
+    int ns, pb;
+    ladder7_compiled(&ns, &pb);
+    return ns;
+}
+
+// granules per k_ladder7 staging batch (see l7_stages)
+int l7_pb()
+{
+    int ns, pb;
+    ladder7_compiled(&ns, &pb);
+    return pb;
+}
+
+bool l7_knobs_ok()
+{
+    const char *ns = std::getenv("DTS_L7_NS"), *pb = std::getenv("DTS_L7_PB");
+    return (!ns || std::atoi(ns) == l7_stages()) && (!pb || std::atoi(pb) == l7_pb());
 }
 
 // k_ladder7 groups: one rendition per group (DTS_L7_GROUP=r) or every rendition of a
@@ -521,13 +543,6 @@ bool l7_by_rung()
 {
     const char *f = std::getenv("DTS_L7_GROUP");
     return f ? f[0] == 'r' : false;
-}
-
-// granules per k_ladder7 staging batch (DTS_L7_PB; a kernel built with DTS_L7_PAIR=1 stages 2)
-int l7_pb()
-{
-    const char *f = std::getenv("DTS_L7_PB");
-    return f ? std::atoi(f) : kL7Batch;
 }
 
 // a staging-only wave in every k_ladder7 group (DTS_L7_STAGER=1; plan groups of W - 1 units)
@@ -595,6 +610,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 {
     int e = validate_spec(s);
     if (e) return e;
+    if (!l7_knobs_ok()) return DTS_E_INVAL;      // DTS_L7_NS / DTS_L7_PB differ from the linked kernel
     gp.src_kind = s.src_fmt == DTS_FMT_P010LE ? kSrcP010 : (s.src_fmt == DTS_FMT_NV12 ? kSrcNV12 : kSrcPlanar8);
     const bool p010 = s.src_fmt == DTS_FMT_P010LE;
     const bool use4 = v4_enabled();
@@ -782,6 +798,7 @@ static void ctx_release(dts_ctx *c)
     if (c->refs.fetch_sub(1) != 1) return;
     hipSetDevice(c->device);
     qscratch_free(c->qs);
+    if (c->hq) hipFree(c->hq);
     for (auto &s : c->stream)
         if (s) hipStreamDestroy(s);
     delete c;
@@ -1532,7 +1549,11 @@ int dts_quality_run_device(dts_ctx *ctx, int w, int h, int fmt, const dts_dev_fr
 
 // Host frames -> device batches -> k_quality -> finished statistics (the Node worker's
 // per-rendition vf_psnr / vf_ssim against a reference rendition).  Synchronous on the
-// ctx's stream 0; device buffers live for the call only.
+// ctx's stream 0.  Frames go through in batches of kQHostBatch into a device buffer the
+// ctx keeps (grown once, reused by every later call): a 600-frame 4K segment needs one
+// batch of scratch, not 2 x 600 frames.
+constexpr int kQHostBatch = 32;
+
 int dts_quality_run_host(dts_ctx *ctx, int w, int h, int fmt, const dts_frame *a, const dts_frame *b, int nframes,
                          dts_qstat *out)
 {
@@ -1548,42 +1569,85 @@ int dts_quality_run_host(dts_ctx *ctx, int w, int h, int fmt, const dts_frame *a
     hipSetDevice(ctx->device);
     DevLayout lay;
     lay.init(w, h, fmt);
-    const size_t fb = (size_t)lay.fstride, n = (size_t)nframes;
-    uint8_t *dev = nullptr;
-    dts_qraw *qd = nullptr;
-    std::vector<dts_qraw> qh(n);
+    const size_t fb = (size_t)lay.fstride, nb = (size_t)std::min(nframes, kQHostBatch);
+    const size_t qoff = align_up((int64_t)(2 * fb * nb), 256), need = qoff + nb * sizeof(dts_qraw);
     hipStream_t st = ctx->stream[0];
-    auto run = [&]() -> int {
-        HIPCHK(ctx, hipMalloc(&dev, 2 * fb * n));
-        HIPCHK(ctx, hipMalloc(&qd, n * sizeof(dts_qraw)));
-        for (size_t f = 0; f < n; ++f)
+    if (ctx->hq_bytes < need) {
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        if (ctx->hq) hipFree(ctx->hq);
+        ctx->hq = nullptr;
+        ctx->hq_bytes = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->hq, need));
+        ctx->hq_bytes = need;
+    }
+    uint8_t *dev = ctx->hq;
+    dts_qraw *qd = reinterpret_cast<dts_qraw *>(dev + qoff);
+    std::vector<dts_qraw> qh((size_t)nframes);
+    dts_dev_frames da{}, db{};
+    for (int p = 0; p < 3; ++p) {
+        const int pp = rowb[p] ? p : 1;
+        da.data[p] = dev + lay.off[pp];
+        db.data[p] = dev + nb * fb + lay.off[pp];
+        da.pitch[p] = db.pitch[p] = lay.pitch[pp];
+    }
+    da.frame_stride = db.frame_stride = (int64_t)fb;
+    for (int f0 = 0; f0 < nframes; f0 += (int)nb) {
+        const int m = std::min((int)nb, nframes - f0);
+        for (int i = 0; i < m; ++i)
             for (int p = 0; p < 3; ++p) {
                 if (!rowb[p]) continue;
-                HIPCHK(ctx, hipMemcpy2DAsync(dev + f * fb + lay.off[p], (size_t)lay.pitch[p], a[f].data[p],
-                                             (size_t)a[f].pitch[p], (size_t)rowb[p], (size_t)rows[p],
+                const dts_frame &fa = a[f0 + i], &fbh = b[f0 + i];
+                HIPCHK(ctx, hipMemcpy2DAsync(dev + i * fb + lay.off[p], (size_t)lay.pitch[p], fa.data[p],
+                                             (size_t)fa.pitch[p], (size_t)rowb[p], (size_t)rows[p],
                                              hipMemcpyHostToDevice, st));
-                HIPCHK(ctx, hipMemcpy2DAsync(dev + (n + f) * fb + lay.off[p], (size_t)lay.pitch[p], b[f].data[p],
-                                             (size_t)b[f].pitch[p], (size_t)rowb[p], (size_t)rows[p],
+                HIPCHK(ctx, hipMemcpy2DAsync(dev + (nb + i) * fb + lay.off[p], (size_t)lay.pitch[p], fbh.data[p],
+                                             (size_t)fbh.pitch[p], (size_t)rowb[p], (size_t)rows[p],
                                              hipMemcpyHostToDevice, st));
             }
-        dts_dev_frames da{}, db{};
-        for (int p = 0; p < 3; ++p) {
-            const int pp = rowb[p] ? p : 1;
-            da.data[p] = dev + lay.off[pp];
-            db.data[p] = dev + n * fb + lay.off[pp];
-            da.pitch[p] = db.pitch[p] = lay.pitch[pp];
-        }
-        da.frame_stride = db.frame_stride = (int64_t)fb;
-        int e = quality_enqueue(ctx, ctx->qs, w, h, fmt, da, db, nframes, qd, st);
+        int e = quality_enqueue(ctx, ctx->qs, w, h, fmt, da, db, m, qd, st);
         if (e) return e;
-        HIPCHK(ctx, hipMemcpyAsync(qh.data(), qd, n * sizeof(dts_qraw), hipMemcpyDeviceToHost, st));
-        HIPCHK(ctx, hipStreamSynchronize(st));
-        return dts_qstat_finalize(w, h, qh.data(), nframes, out);
-    };
-    const int e = run();
-    if (dev) hipFree(dev);
-    if (qd) hipFree(qd);
-    return e;
+        HIPCHK(ctx, hipMemcpyAsync(qh.data() + f0, qd, (size_t)m * sizeof(dts_qraw), hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));      // the batch buffer is reused by the next batch
+    }
+    return dts_qstat_finalize(w, h, qh.data(), nframes, out);
+}
+
+int dts_qraw_sum_device(dts_ctx *ctx, const dts_qraw *raw_dev, int n, dts_qraw *sum_dev, void *stream)
+{
+    if (!ctx || !raw_dev || !sum_dev || n < 0) return DTS_E_INVAL;
+    hipSetDevice(ctx->device);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
+    HIPCHK(ctx, launch_qsum(raw_dev, n, sum_dev, st));
+    return DTS_OK;
+}
+
+int dts_qstat_stream(int w, int h, const dts_qraw *sum, int64_t nframes, dts_qstat *out)
+{
+    if (!sum || !out || nframes < 1 || w < 1 || h < 1) return DTS_E_INVAL;
+    // vf_psnr uninit: psnr(mse_comp[c] / nb_frames), psnr(mse / nb_frames) with mse the
+    // area-weighted per-frame average; vf_ssim uninit: ssim[c] / nb_frames and
+    // ssim_total / nb_frames.  Plane sizes are fixed, so both are the per-frame
+    // formulas (dts_qstat_finalize) on the summed record with every count x nframes.
+    const int pw[3] = {w, (w + 1) >> 1, (w + 1) >> 1}, ph[3] = {h, (h + 1) >> 1, (h + 1) >> 1};
+    double area = 0;
+    for (int c = 0; c < 3; ++c) area += (double)pw[c] * ph[c];
+    double mse = 0, ssim = 0;
+    const double n = (double)nframes;
+    for (int c = 0; c < 3; ++c) {
+        const double wgt = (double)pw[c] * ph[c] / area;
+        out->sse[c] = sum->sse[c];
+        out->mse[c] = sum->sse[c] / ((double)((int64_t)pw[c] * ph[c]) * n);
+        out->psnr[c] = 10.0 * std::log10(255.0 * 255.0 / out->mse[c]);
+        mse += out->mse[c] * wgt;
+        const int nw = ((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1);
+        out->ssim[c] = sum->ssim_sum[c] / ((double)nw * n);
+        ssim += wgt * out->ssim[c];
+    }
+    out->mse_avg = mse;
+    out->psnr_avg = 10.0 * std::log10(255.0 * 255.0 / mse);
+    out->ssim_all = ssim;
+    out->ssim_db = 10.0 * std::log10(1.0 / (1.0 - ssim));
+    return DTS_OK;
 }
 
 int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dts_dev_frames *seq, int nseq,

@@ -336,6 +336,7 @@ struct Group7 {                     // one workgroup's strip of one frame
     int32_t u0;                     // first unit
     int32_t ngran, srcH;
     int32_t scr;                    // LDS offset of the per-wave store exchange (1 KB per wave)
+    int32_t xown;                   // the next strip's X0 (plane width for the last): diagnostics only
 };
 
 struct Ladder7Params {
@@ -349,6 +350,7 @@ struct Ladder7Params {
 };
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s);
+void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
@@ -468,6 +470,7 @@ __host__ __device__ inline int synth_sample(int pattern, uint32_t seed, int x, i
 hipError_t launch_ladder(const LadderParams &p, int ndmax, int lds_bytes, int grid, hipStream_t s);
 int ladder_blocks_per_cu(int src_kind, int ndmax, int lds_bytes);   // occupancy for the persistent grid
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s);
+hipError_t launch_qsum(const dts_qraw *raw, int n, dts_qraw *sum, hipStream_t s);
 hipError_t launch_synth(int w, int h, int fmt, int pattern, uint32_t seed, int64_t first,
                         const DevPlanes &dst, int nframes, hipStream_t s);
 int ladder_ndmax_for(int nd);       // template bucket for a required nd (0 = unsupported)

@@ -806,6 +806,49 @@ __global__ void __launch_bounds__(kThreads) k_qreduce(const QualityParams P)
     }
 }
 
+// One segment's record: the n per-frame records summed (u64 SSE exact; the f64 SSIM
+// window sums in a fixed order: thread t takes frames t, t + kThreads, ... in order,
+// then the tree; the same n always gives the same bits).  One workgroup per record
+// field: 3 SSE + 3 SSIM sums.  vf_psnr / vf_ssim keep exactly these running sums
+// across a stream (uninit: mse_comp / nb_frames, ssim / nb_frames).
+__global__ void __launch_bounds__(kThreads) k_qsum(const dts_qraw *raw, int n, dts_qraw *sum)
+{
+    __shared__ double rs[kThreads];
+    __shared__ unsigned long long re[kThreads];
+    const int c = blockIdx.x % 3, t = threadIdx.x;
+    const bool ssim = blockIdx.x >= 3;
+    double s = 0;
+    unsigned long long e = 0;
+    for (int i = t; i < n; i += kThreads) {
+        if (ssim)
+            s += raw[i].ssim_sum[c];
+        else
+            e += raw[i].sse[c];
+    }
+    rs[t] = s;
+    re[t] = e;
+    __syncthreads();
+    for (int o = kThreads / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            rs[t] += rs[t + o];
+            re[t] += re[t + o];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (ssim)
+            sum->ssim_sum[c] = rs[0];
+        else
+            sum->sse[c] = re[0];
+    }
+}
+
+hipError_t launch_qsum(const dts_qraw *raw, int n, dts_qraw *sum, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_qsum, dim3(6), dim3(kThreads), 0, s, raw, n, sum);
+    return hipGetLastError();
+}
+
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s)
 {
     hipLaunchKernelGGL(k_quality, dim3((unsigned)(total_tiles * p.nframes)), dim3(kThreads), 0, s, p);

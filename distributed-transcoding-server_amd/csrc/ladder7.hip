@@ -39,7 +39,8 @@
 #include "ladder_mfma.h"
 
 #ifndef DTS_L7_ABLATE
-#define DTS_L7_ABLATE 0     // diagnostic builds only (wrong results): 1 no group barrier, 2 no A xor
+#define DTS_L7_ABLATE 0     // diagnostic builds only (wrong results): 1 no group barrier, 2 no A xor,
+                            // 4 stage only the pieces left of the next strip's X0 (no halo re-reads)
 #endif
 #ifndef DTS_L7_DEFER
 #define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
@@ -125,7 +126,7 @@ __device__ __forceinline__ void group_barrier7()
 struct Stage7 {
     uint64_t sb[2];                 // plane bases of this frame (chroma: U, V)
     uint32_t sp[2];                 // plane pitches
-    int np, npc, npieces, w, nw, srcH1, ngran, stage_bytes;
+    int np, npc, npieces, w, nw, srcH1, ngran, stage_bytes, nown;
     uint32_t lcol;                  // this lane's byte in a piece row: X0 + 16 chunk
     int dr;                         // this lane's row in a piece
     int ops, e[NS7 - 1];
@@ -139,6 +140,7 @@ struct Stage7 {
         }
         npc = G.npc;
         npieces = np * npc;
+        nown = min(npc, (G.xown - G.X0 + 63) >> 6);
         // the waves beyond the group's units (if any) stage every piece; else all deal them
         const int stagers = waves - G.nwaves;
         w = stagers > 0 ? (wave >= G.nwaves ? wave - G.nwaves : npieces) : wave;
@@ -163,6 +165,7 @@ struct Stage7 {
         uint8_t *dst = lds + at;
         for (int k = w; k < npieces; k += nw) {
             const int p = k >= npc ? 1 : 0, i = k - p * npc;
+            if ((DTS_L7_ABLATE & 4) && i >= nown) continue;
             const uint64_t src = (p ? sb[1] : sb[0]) + (uint64_t)(row * (p ? sp[1] : sp[0])) + lcol + 64u * (uint32_t)i;
             __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)src,
                                              (__attribute__((address_space(3))) void *)(dst + 1024 * k), 16, 0,
@@ -640,6 +643,14 @@ int ladder7_stamps(unsigned long long *out, bool reset)
     return (kL7Variants + 1) * 8;
 }
 #endif
+
+// the staging geometry this build of k_ladder7 was compiled with: the planner sizes the
+// stage buffers and the V fragment slots for exactly these, and refuses any other
+void ladder7_compiled(int *stages, int *batch)
+{
+    *stages = NS7;
+    *batch = PB7;
+}
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s)
 {

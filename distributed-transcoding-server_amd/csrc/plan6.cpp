@@ -447,6 +447,11 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             u += cnt;
         }
     }
+    for (size_t i = 0; i < out.groups.size(); ++i) {       // (ladder7.hip DTS_L7_ABLATE & 4)
+        Group7 &g = out.groups[i];
+        const bool last = i + 1 == out.groups.size() || out.groups[i + 1].kind != g.kind;
+        g.xown = last ? kinds[g.kind].srcW : std::max(out.groups[i + 1].X0, g.X0 + 64);
+    }
     if (std::getenv("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
         for (const Group7 &g : out.groups)
             std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d\n", g.kind, g.X0, g.npc, g.nwaves);

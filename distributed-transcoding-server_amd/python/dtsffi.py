@@ -93,7 +93,8 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_ctx_last_hip_error", "dts_graph_create", "dts_graph_destroy", "dts_graph_info_get",
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
-           "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device", "dts_quality_run_host"]
+           "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device", "dts_quality_run_host",
+           "dts_qraw_sum_device", "dts_qstat_stream"]
 
 _lib = None
 
@@ -128,6 +129,8 @@ def lib():
     L.dts_quality_run_device.argtypes = [vp, i32, i32, i32, ctypes.POINTER(DevFrames),
                                          ctypes.POINTER(DevFrames), i32, vp, vp]
     L.dts_qstat_finalize.argtypes = [i32, i32, ctypes.POINTER(QRaw), i32, ctypes.POINTER(QStat)]
+    L.dts_qraw_sum_device.argtypes = [vp, vp, i32, vp, vp]
+    L.dts_qstat_stream.argtypes = [i32, i32, ctypes.POINTER(QRaw), i64, ctypes.POINTER(QStat)]
     L.dts_quality_run_host.argtypes = [vp, i32, i32, i32, ctypes.POINTER(Frame), ctypes.POINTER(Frame), i32,
                                        ctypes.POINTER(QStat)]
     L.dts_synth_host.argtypes = [i32, i32, i32, i32, u32, i64, ctypes.POINTER(Frame)]
@@ -224,6 +227,24 @@ def qstat_finalize(w, h, raws):
     return [out[i].as_dict() for i in range(n)]
 
 
+def qstat_stream(w, h, raw_sum, nframes):
+    """dts_qstat_stream: vf_psnr / vf_ssim end-of-stream averages of nframes frames
+    from their summed record (a QRaw)."""
+    out = QStat()
+    check(lib().dts_qstat_stream(w, h, ctypes.byref(raw_sum), nframes, ctypes.byref(out)), "qstat_stream")
+    return out.as_dict()
+
+
+def qraw_sum_host(raws):
+    """The sum of QRaw records (u64 SSE, f64 SSIM sums) on the host, in list order."""
+    s = QRaw()
+    for r in raws:
+        for c in range(3):
+            s.sse[c] += r.sse[c]
+            s.ssim_sum[c] += r.ssim_sum[c]
+    return s
+
+
 def graph_plan(spec):
     """dts_graph_plan: the graph's info (filter sizes, kernel choice) without a device."""
     info = GraphInfo()
@@ -249,7 +270,7 @@ def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max
         s.hdr_to_sdr = 1
         s.tonemap.mode = tonemap.get("mode", TM_HABLE)
         s.tonemap.param = tonemap.get("param", float("nan"))
-        s.tonemap.desat = tonemap.get("desat", 0.0)
+        s.tonemap.desat = tonemap.get("desat", 2.0)          # vf_tonemap's default (FFmpeg 4.4)
         s.tonemap.peak = tonemap.get("peak", 0.0)
         s.tonemap.npl = tonemap.get("npl", 100.0)
     if deint is not None:
@@ -288,6 +309,10 @@ class Context:
         check(lib().dts_quality_run_device(self.h, w, h, fmt, ctypes.byref(a), ctypes.byref(b), nframes,
                                            ctypes.c_void_p(qraw_ptr), ctypes.c_void_p(stream or 0)),
               "quality_run_device")
+
+    def qraw_sum_device(self, raw_ptr, n, sum_ptr, stream=None):
+        check(lib().dts_qraw_sum_device(self.h, ctypes.c_void_p(raw_ptr), n, ctypes.c_void_p(sum_ptr),
+                                        ctypes.c_void_p(stream or 0)), "qraw_sum_device")
 
     def quality_host(self, w, h, fmt, a_frames, b_frames):
         """vf_psnr + vf_ssim of host frames a[i] vs b[i] (plane lists) -> [qstat dict]."""

@@ -89,7 +89,9 @@ typedef struct dts_tonemap_spec {
     int32_t mode;       /* DTS_TM_* (vf_tonemap tonemap=) */
     int32_t pad_;
     double param;       /* vf_tonemap param; NaN = the curve's default (init()) */
-    double desat;       /* vf_tonemap desat; <= 0 = off */
+    double desat;       /* vf_tonemap desat; <= 0 = off.  vf_tonemap's default is 2.0
+                           (FFmpeg 4.4 tonemap_options): the bindings (N-API addon,
+                           dtsffi, node/ladder.js) default to it */
     double peak;        /* vf_tonemap peak (units of npl); <= 0 = its fallback for
                            linear input without HDR side data: 10 */
     double npl;         /* zscale npl, cd/m^2 mapped to 1.0; <= 0 = 100 */
@@ -250,6 +252,16 @@ int dts_yadif_run_device(dts_ctx *ctx, int w, int h, int mode, int tff, const dt
 
 /* vf_psnr get_psnr / vf_ssim ssim_db finishing of raw records (host). */
 int dts_qstat_finalize(int w, int h, const dts_qraw *raw, int n, dts_qstat *out);
+/* A segment's quality record: the n device records at raw_dev summed into one
+ * record at sum_dev (u64 SSE exact, f64 SSIM window sums in a fixed order), on
+ * `stream`.  These are the running sums vf_psnr / vf_ssim keep over a stream;
+ * records of several segments (gathered from several GPUs) add up the same way. */
+int dts_qraw_sum_device(dts_ctx *ctx, const dts_qraw *raw_dev, int n, dts_qraw *sum_dev, void *stream);
+/* End-of-stream averages of nframes frames from their summed record, as vf_psnr /
+ * vf_ssim print them at uninit: psnr[c] / psnr_avg from the mean MSE (not the mean
+ * dB), ssim[c] / ssim_all the mean SSIM.  Replaces reading the "PSNR y:.. average:"
+ * and "SSIM Y:.. All:" lines from an ffmpeg worker's log. */
+int dts_qstat_stream(int w, int h, const dts_qraw *sum, int64_t nframes, dts_qstat *out);
 
 /* Synthetic deterministic source (testsrc2-like): pattern 0 = gradient +
  * moving bars + seeded noise (limited range), 1 = uniform random full range. */

@@ -136,7 +136,7 @@ def fps_map(nb_in, in_rate, out_rate, cap=1 << 20):
 TM_MODES = {"none": 0, "linear": 1, "gamma": 2, "clip": 3, "reinhard": 4, "hable": 5, "mobius": 6}
 
 
-def hdr_to_sdr(src_planes, w, h, dst_fmt, mode=5, param=float("nan"), desat=0.0, peak=0.0, npl=0.0):
+def hdr_to_sdr(src_planes, w, h, dst_fmt, mode=5, param=float("nan"), desat=2.0, peak=0.0, npl=0.0):
     """HDR10 p010 -> SDR bt709 8-bit (zscale + vf_tonemap restated, double precision)."""
     dst = _alloc(w, h, dst_fmt)
     sd, sp = _ptrs(src_planes)

@@ -10,7 +10,14 @@ def oracle_frame(src, sw, sh, sfmt, w, h, fmt, method, param=(D.PARAM_DEFAULT, D
 
 
 def planes_equal(a, b):
+    """Plane lists equal: same plane count (None where a format has no plane) and
+    every plane bit-exact."""
+    a, b = list(a), list(b)
+    if len(a) != len(b):
+        return False
     for pa, pb in zip(a, b):
+        if (pa is None) != (pb is None):
+            return False
         if pa is None and pb is None:
             continue
         if not np.array_equal(np.asarray(pa), np.asarray(pb)):
@@ -19,7 +26,12 @@ def planes_equal(a, b):
 
 
 def first_diff(a, b):
+    a, b = list(a), list(b)
+    if len(a) != len(b):
+        return f"plane count {len(a)} vs {len(b)}"
     for i, (pa, pb) in enumerate(zip(a, b)):
+        if (pa is None) != (pb is None):
+            return f"plane {i} present in one frame only"
         if pa is None:
             continue
         d = np.argwhere(np.asarray(pa) != np.asarray(pb))

@@ -60,7 +60,7 @@ def main():
     # HDR10 -> SDR (float path, double oracle) and yadif
     src = D.synth_host(64, 36, D.FMT_P010LE, 0, 5, 0)
     d = planes_dict("src", src)
-    d.update(planes_dict("out", orc.hdr_to_sdr(src, 64, 36, D.FMT_YUV420P, D.TM_HABLE)))
+    d.update(planes_dict("out", orc.hdr_to_sdr(src, 64, 36, D.FMT_YUV420P, D.TM_HABLE, desat=0.0)))
     np.savez_compressed(os.path.join(HERE, "hdr_hable_64x36.npz"), **d)
     fr = [D.synth_host(48, 20, D.FMT_YUV420P, 1, 9, i) for i in range(3)]
     d = {}

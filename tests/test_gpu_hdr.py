@@ -61,8 +61,11 @@ def test_p010_identity_passthrough(ctx):
 
 
 def _check_tol(got, want, what):
+    got, want = list(got), list(want)
+    assert len(got) == len(want), f"{what}: {len(got)} planes vs {len(want)}"
     n = bad = 0
     for a, b in zip(got, want):
+        assert (a is None) == (b is None), f"{what}: plane present in one frame only"
         if a is None:
             continue
         d = np.abs(np.asarray(a).astype(np.int16) - np.asarray(b).astype(np.int16))
@@ -79,7 +82,7 @@ def _hdr_case(ctx, sw, sh, outs, frames, tm):
         for k, (w, h, fmt, m) in enumerate(outs):
             mid = orc.scale_frame(src, sw, sh, D.FMT_P010LE, w, h, D.FMT_P010LE, m)
             want = orc.hdr_to_sdr(mid, w, h, fmt, tm.get("mode", D.TM_HABLE), tm.get("param", float("nan")),
-                                  tm.get("desat", 0.0), tm.get("peak", 0.0), tm.get("npl", 100.0))
+                                  tm.get("desat", 2.0), tm.get("peak", 0.0), tm.get("npl", 100.0))
             _check_tol(got[f][k], want, f"frame {f} out {k} tm {tm}")
     g.close()
 
@@ -103,7 +106,9 @@ def test_hdr_to_sdr_params(ctx, tm):
 
 
 def test_hdr_4k_to_1080p_one_frame(ctx):
-    """The config-3 geometry itself, one frame (host path)."""
+    """The config-3 geometry itself, one frame (host path), with vf_tonemap's
+    defaults (hable, desat 2.0, peak from the fallback): the graph a CPU worker's
+    `tonemap=hable` runs."""
     frames = [D.synth_host(3840, 2160, D.FMT_P010LE, 0, 0x5EED, 0)]
     _hdr_case(ctx, 3840, 2160, [(1920, 1080, D.FMT_YUV420P, BIC)], frames, {"mode": D.TM_HABLE})
 

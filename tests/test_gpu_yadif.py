@@ -6,7 +6,7 @@ import pytest
 
 import dtsffi as D
 import orc
-from _util import random_frame
+from _util import random_frame, planes_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -88,7 +88,7 @@ def test_yadif_subrange_and_validation(ctx):
         i = 3 + j
         want = orc.yadif_frame(hp[i - 1], hp[i], hp[min(i + 1, n - 1)], w, h, 0, 1, 0)
         got = _from_dev(out_t[j].cpu().numpy(), w, h)
-        assert all(np.array_equal(a, b) for a, b in zip(got, want))
+        assert planes_equal(got, want)
     with pytest.raises(D.DtsError):
         ctx.yadif_device(w, h, 0, 1, seq, n, 5, 2, _dev(out_t, w, h))
     with pytest.raises(D.DtsError):
@@ -114,7 +114,7 @@ def test_graph_yadif_then_ladder(ctx, mode, tff):
         de = orc.yadif_frame(seq[i - 1], seq[i], seq[i + 1], sw, sh, mode, tff, 0)
         for k, (w, h, fmt, m) in enumerate(outs):
             want = orc.scale_frame(de, sw, sh, Dm.FMT_YUV420P, w, h, fmt, m)
-            assert all(np.array_equal(a, b) for a, b in zip(got[j][k], want)), (mode, tff, j, k)
+            assert planes_equal(got[j][k], want), (mode, tff, j, k)
     g.close()
     with pytest.raises(Dm.DtsError):                   # frame-rate modes only; 8-bit planar sources only
         Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_YUV420P, outs, deint=(1, 1)))

@@ -205,3 +205,57 @@ def test_plan_range_conversion(monkeypatch):
     with pytest.raises(D.DtsError):
         D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1))
     assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1, dst_range=1)).ladder_v5 == 2
+
+
+@pytest.mark.parametrize("knob", [("DTS_L7_PB", "1"), ("DTS_L7_NS", "3"), ("DTS_L7_NS", "4")])
+def test_l7_staging_knobs_must_match_the_kernel(monkeypatch, knob):
+    """DTS_L7_PB / DTS_L7_NS may only restate the staging geometry the linked
+    k_ladder7 was compiled with (a planner sized for one
+    granule per batch let the kernel overrun its V fragment slots).  Any other
+    value is refused at planning time instead of miscomputed."""
+    spec = D.make_spec(3840, 2160, D.FMT_YUV420P, [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC)], max_batch=64)
+    assert D.graph_plan(spec).ladder_v5 == 3          # k_ladder7 without the knob
+    monkeypatch.setenv(*knob)
+    with pytest.raises(D.DtsError) as e:
+        D.graph_plan(spec)
+    assert e.value.code == D.E_INVAL
+
+
+def test_l7_staging_knobs_restating_the_build_are_accepted(monkeypatch):
+    spec = D.make_spec(3840, 2160, D.FMT_YUV420P, [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC)], max_batch=64)
+    monkeypatch.setenv("DTS_L7_PB", "2")
+    monkeypatch.setenv("DTS_L7_NS", "2")
+    assert D.graph_plan(spec).ladder_v5 == 3
+
+
+def test_qstat_stream_is_vf_psnr_ssim_end_of_stream():
+    """dts_qstat_stream on summed records = vf_psnr's mean-MSE PSNR and vf_ssim's mean
+    SSIM over the frames (and the same as bench.job_quality, cfg5's gather side)."""
+    import bench
+    import torch
+    rng = np.random.default_rng(7)
+    w, h, n = 854, 480, 9
+    pw, ph = [w, 427, 427], [h, 240, 240]
+    nw = [((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1) for c in range(3)]
+    raws = []
+    for _ in range(n):
+        r = D.QRaw()
+        for c in range(3):
+            r.sse[c] = int(rng.integers(0, 50 * pw[c] * ph[c]))
+            r.ssim_sum[c] = float(rng.uniform(0.8, 1.0)) * nw[c]
+        raws.append(r)
+    per = D.qstat_finalize(w, h, raws)
+    got = D.qstat_stream(w, h, D.qraw_sum_host(raws), n)
+    mse = [np.mean([p["mse"][c] for p in per]) for c in range(3)]
+    assert got["mse"] == pytest.approx(mse, rel=1e-12)
+    assert got["mse_avg"] == pytest.approx(np.mean([p["mse_avg"] for p in per]), rel=1e-12)
+    assert got["psnr_avg"] == pytest.approx(10 * np.log10(255 * 255 / got["mse_avg"]), rel=1e-12)
+    assert got["ssim"] == pytest.approx([np.mean([p["ssim"][c] for p in per]) for c in range(3)], rel=1e-12)
+    assert got["ssim_all"] == pytest.approx(np.mean([p["ssim_all"] for p in per]), rel=1e-12)
+    sse = torch.tensor([[list(r.sse) for r in raws]], dtype=torch.int64).sum(1, keepdim=True)
+    ssim = torch.tensor([[list(r.ssim_sum) for r in raws]], dtype=torch.float64).sum(1, keepdim=True)
+    jq = bench.job_quality([(w, h, D.FMT_NV12, 0)], sse, ssim, n)[0]
+    assert jq["psnr_avg"] == pytest.approx(got["psnr_avg"], abs=1e-4)
+    assert jq["ssim_all"] == pytest.approx(got["ssim_all"], abs=1e-6)
+    with pytest.raises(D.DtsError):
+        D.qstat_stream(w, h, raws[0], 0)

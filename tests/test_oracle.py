@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import orc
+from _util import planes_equal
 
 BIL, BIC, LAN, POINT, AREA, GAUSS = 0x2, 0x4, 0x200, 0x10, 0x20, 0x80
 
@@ -62,10 +63,10 @@ def test_identity_and_nv12_roundtrip():
     rng = np.random.default_rng(0)
     src = _frame(64, 36, rng)
     same = orc.scale_frame(src, 64, 36, 0, 64, 36, 0, BIC)
-    assert all(np.array_equal(a, b) for a, b in zip(src, same))
+    assert planes_equal(src, same)
     nv = orc.scale_frame(src, 64, 36, 0, 64, 36, 1, BIC)
     back = orc.nv12_to_planar(nv)
-    assert all(np.array_equal(a, b) for a, b in zip(src, back))
+    assert planes_equal(src, back)
 
 
 @pytest.mark.parametrize("method", [BIL, BIC])
@@ -126,7 +127,7 @@ def test_yadif_oracle_properties():
     c = [np.tile(np.arange(p.shape[1], dtype=np.uint8)[None, :] * 3, (p.shape[0], 1)) for p in f]
     for mode in range(4):
         oc = orc.yadif_frame(c, c, c, w, h, mode, 1, 0)
-        assert all(np.array_equal(a, b) for a, b in zip(oc, c))
+        assert planes_equal(oc, c)
 
 
 @pytest.mark.parametrize("v,src_range,dst_range,luma,chroma", [
@@ -142,4 +143,4 @@ def test_range_conversion_known_answers(v, src_range, dst_range, luma, chroma):
     assert set(np.unique(out[0])) == {luma}
     assert set(np.unique(out[1])) == {chroma} and set(np.unique(out[2])) == {chroma}
     same = orc.scale_frame(f, w, h, 0, w, h, 0, BIC, src_range=src_range, dst_range=src_range)
-    assert all(np.array_equal(a, b) for a, b in zip(same, f))      # equal ranges: no conversion
+    assert planes_equal(same, f)      # equal ranges: no conversion
