@@ -199,7 +199,7 @@ struct dts_graph {
     const Unit7 *dev_units7 = nullptr;
     const uint32_t *dev_frag7 = nullptr;
     const int32_t *dev_fire7 = nullptr;
-    int ngroups7 = 0, lds7 = 0, waves7 = 0;
+    int ngroups7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -1028,6 +1028,7 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
     g->waves7 = gp.p7.waves;
+    g->hsplit7 = gp.p7.hsplit;
     g->v7 = true;
     return DTS_OK;
 }
@@ -1359,7 +1360,8 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.fire = g->dev_fire7;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
-            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1), st));
+            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
+                                       g->hsplit7, st));
             continue;
         }
         bool aligned6 = g->v6 && planes_aligned6(pp.src);

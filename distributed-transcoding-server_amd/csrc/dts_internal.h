@@ -349,7 +349,8 @@ struct Ladder7Params {
     const int32_t *fire;
 };
 
-hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s);
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
+                          hipStream_t s);
 void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
 
 // ---------------------------------------------------------------------------

@@ -122,8 +122,10 @@ struct Plan6 {
 // 16 for k_ladder7, whose A operands are 16-B LDS reads); sort: heaviest units first.
 // narrow (k_ladder7): the one-K-block walks get 2 tiles per plane (luma) / 1 (chroma), not 4 / 2
 // fs_window: granules whose firing row blocks share the V fragment slots
+// hsplit: the H taps as hsplit * hi + lo (256: lo a signed byte, k_ladder6; 128: lo in
+// [0, 127], k_ladder7's one-shift epilogue; false if a tap does not split)
 bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align = 4, bool sort = true, bool narrow = false,
-                 int fs_window = kL6Stages);
+                 int fs_window = kL6Stages, int hsplit = 256);
 
 // v7 ladder plan: the v6 units (align 16) in groups of at most wmax waves over one
 // source strip (Group7, Unit7).  false: the graph does not fit k_ladder7 (plane widths
@@ -134,6 +136,7 @@ struct Plan7 {
     std::vector<uint32_t> frag;
     std::vector<int32_t> fire;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
+    int hsplit = 256;                // H tap split of the fragments (ladder7.hip walk7 HS)
 };
 // stager: one more wave per workgroup that only stages (groups of wmax units then have it too)
 bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, bool stager,

@@ -339,7 +339,14 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
     L7_STAMP_DONE(kL7Variants, G.ngran);
 }
 
-template <int VAR, bool RC>
+// HS: the H taps' split in the fragments (plan6.cpp put6).  256: c = 256 hi + lo (signed
+// bytes), the epilogue FFMIN(((hi << 8) + lo) >> 7, 32767).  128: c = 128 hi + lo, lo in
+// [0, 127]; with x = src - 128, sum(src c) = 128 (sum(x hi) + 16384) + sum(x lo), so
+//   y = sum(src c) >> 7 = sum(x hi) + ((sum(x lo) + (128 << 14)) >> 7)
+// exactly (128 (...) is a multiple of 128): the lo MFMAs run first from the bias, one
+// shift, and the hi MFMAs accumulate onto it -- y comes out of the matrix core and the
+// epilogue is the saturating pack (FFMIN(y, 32767), y >= -32768 for 8-bit sources).
+template <int VAR, bool RC, int HS>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -535,16 +542,42 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     ah[t] = zero;
                     al[t] = hbias;
                 }
+                if (HS == 128) {
+                    v4i x[T][HKB];
 #pragma unroll
-                for (int kb = 0; kb < HKB; ++kb)
+                    for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t) {
+                            x[t][kb] = a[t][kb] ^ ((DTS_L7_ABLATE & 2) ? 0 : (int)0x80808080u);
+                            al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+                        }
+#pragma unroll
+                    for (int t = 0; t < T; ++t) ah[t] = al[t] >> 7;
+#pragma unroll
+                    for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t)
+                            ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[t][kb], bh[t % CT][kb], ah[t], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t) {
+                            const v4i x = a[t][kb] ^ ((DTS_L7_ABLATE & 2) ? 0 : (int)0x80808080u);
+                            ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bh[t % CT][kb], ah[t], 0, 0, 0);
+                            al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bl[t % CT][kb], al[t], 0, 0, 0);
+                        }
+                }
+                const int rs = s % R;
+                if (HS == 128 && !RC) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
-                        const v4i x = a[t][kb] ^ ((DTS_L7_ABLATE & 2) ? 0 : (int)0x80808080u);
-                        ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bh[t % CT][kb], ah[t], 0, 0, 0);
-                        al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, bl[t % CT][kb], al[t], 0, 0, 0);
+                        const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(ah[t].x, ah[t].y));
+                        const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(ah[t].z, ah[t].w));
+                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
+                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                     }
-                const int rs = s % R;
-                if (!RC) {
+                } else if (!RC) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
                         const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
@@ -560,7 +593,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         int y[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const int v = min(((ah[t][i] << 8) + al[t][i]) >> 7, 32767);
+                            const int v = min(HS == 128 ? ah[t][i] : ((ah[t][i] << 8) + al[t][i]) >> 7, 32767);
                             y[i] = (min(v, U.rc_cap) * U.rc_mul + U.rc_add) >> U.rc_sh;
                         }
                         const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)y[1], (uint32_t)y[0], 0x05040100u);
@@ -591,7 +624,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 
 // RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
 // the common kernel keeps its register allocation)
-template <bool RC>
+template <bool RC, int HS>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -613,20 +646,20 @@ void k_ladder7(Ladder7Params P)
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
-    walk7<DTS_L7_ONLYVAR, RC>(P, G, U, S, f, wave, waves);
+    walk7<DTS_L7_ONLYVAR, RC, HS>(P, G, U, S, f, wave, waves);
     return;
 #endif
     switch (U.variant) {
-    case 0: walk7<0, RC>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1, RC>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2, RC>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3, RC>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4, RC>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5, RC>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6, RC>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7, RC>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8, RC>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12, RC>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC, HS>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC, HS>(P, G, U, S, f, wave, waves); break;
     }
 }
 
@@ -652,13 +685,19 @@ void ladder7_compiled(int *stages, int *batch)
     *batch = PB7;
 }
 
-hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, hipStream_t s)
+hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
+                          hipStream_t s)
 {
-    if (waves < 1 || waves > kL7MaxWaves) return hipErrorInvalidValue;
-    if (range_conv)
-        hipLaunchKernelGGL(k_ladder7<true>, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
+    if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
+    const dim3 g(grid), b(64 * waves);
+    if (range_conv && hsplit == 128)
+        hipLaunchKernelGGL((k_ladder7<true, 128>), g, b, lds_bytes, s, p);
+    else if (range_conv)
+        hipLaunchKernelGGL((k_ladder7<true, 256>), g, b, lds_bytes, s, p);
+    else if (hsplit == 128)
+        hipLaunchKernelGGL((k_ladder7<false, 128>), g, b, lds_bytes, s, p);
     else
-        hipLaunchKernelGGL(k_ladder7<false>, dim3(grid), dim3(64 * waves), lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<false, 256>), g, b, lds_bytes, s, p);
     return hipGetLastError();
 }
 

@@ -54,16 +54,17 @@ int vtap6(const VTable &v, int y, int row)
 }
 
 // one fragment pair from tapf(lane, j) (j = byte of the lane's 16): c = 256 hi + lo,
-// hi and lo signed bytes; false if a tap does not split
+// hi and lo signed bytes (split 256), or c = 128 hi + lo with lo in [0, 127] (split 128);
+// false if a tap does not split
 template <class F>
-bool put6(std::vector<uint32_t> &bf, uint32_t frag, F tapf)
+bool put6(std::vector<uint32_t> &bf, uint32_t frag, F tapf, int split = 256)
 {
     uint8_t *hi = reinterpret_cast<uint8_t *>(bf.data() + (size_t)frag * 512);
     uint8_t *lo = hi + 1024;
     for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 16; ++j) {
             const int c = tapf(lane, j);
-            const int l = (int8_t)(c & 0xff), h = (c - l) >> 8;
+            const int l = split == 128 ? (c & 127) : (int8_t)(c & 0xff), h = split == 128 ? (c >> 7) : (c - l) >> 8;
             if (h < -128 || h > 127) return false;
             hi[lane * 16 + j] = (uint8_t)h;
             lo[lane * 16 + j] = (uint8_t)l;
@@ -146,7 +147,7 @@ bool plan_v6(const VTable &v, int srcH, int dstH, Rend6 &r)
 
 } // namespace
 
-bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool narrow, int fs_window)
+bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool narrow, int fs_window, int hsplit)
 {
     out = Plan6{};
     struct Cost { Unit6 u; int64_t cost; };
@@ -218,7 +219,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
                 if (!put6(out.frag, p.hfrag + (uint32_t)(t * p.r.hkb + kb), [&](int lane, int j) {
                         const int o = 16 * t + (lane & 15);
                         return o < R.dstW ? htap6(f, o, base + 16 * (lane >> 4) + j) : 0;
-                    }))
+                    }, hsplit))
                     return false;
             }
         const int R4 = 4 * p.r.vkb;
@@ -292,7 +293,18 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     // granules (the batches in flight + the one-granule V deferral; ladder7.hip)
     if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages > 4 || pb < 1 || pb > 2) return false;
     Plan6 p6;
-    if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1))) return false;
+    // H taps split 128 (one shift in the H epilogue, walk7 HS = 128) where every tap fits
+    // (|c| < 16384: not a 1:1 tap of exactly 1 << 14), else 256
+    out.hsplit = 128;
+    if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 128)) {
+        out.hsplit = 256;
+        if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
+    }
+    if (const char *hs = std::getenv("DTS_L7_HSPLIT"))    // diagnostic A/B: force the 256 split
+        if (std::atoi(hs) == 256 && out.hsplit == 128) {
+            out.hsplit = 256;
+            if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
+        }
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
     for (int kind = 0; kind < 2; ++kind) {
@@ -374,6 +386,22 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             for (int gi = 0; gi < ng; ++gi) runs.push_back({(z - a) / ng + (gi < (z - a) % ng ? 1 : 0), 0});
             a = z;
         }
+        // Waves w and w + 4 of a workgroup share a SIMD (waves are dealt to the CU's four
+        // SIMDs in turn).  Within each group the heaviest units (MFMAs per granule: the
+        // 1080p walks) take waves 0..3 and the lightest 4..7, so no SIMD carries two heavy
+        // walks of one group (the heavy waves set the group's pace at every barrier).
+        const char *bal = std::getenv("DTS_L7_BAL");
+        if (!bal || std::atoi(bal) != 0)
+            for (int gi = 0, u = 0; gi < (int)runs.size(); u += runs[gi].first, ++gi) {
+                const int cnt = runs[gi].first;
+                auto cost = [](const Unit6 &w) {
+                    const int t = l6_ct(w.variant) * l6_np(w.variant);
+                    return (int64_t)w.ngran * t * l6_hkb(w.variant) * 2 + (int64_t)w.nrb * t * l6_vkb(w.variant) * 4;
+                };
+                std::vector<Unit6> part(us.begin() + u, us.begin() + u + cnt);
+                std::stable_sort(part.begin(), part.end(), [&](const Unit6 &a, const Unit6 &b) { return cost(a) > cost(b); });
+                for (int i = 0; i < cnt; ++i) us[u + i] = part[i];
+            }
         for (int gi = 0, u = 0; gi < (int)runs.size(); ++gi) {
             const int cnt = runs[gi].first;                 // groups as even as possible
             Group7 g{};

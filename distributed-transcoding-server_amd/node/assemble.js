@@ -25,17 +25,22 @@ function storeBlock(blockDir, buf) {
     return id;
 }
 
-// files: segment paths in playback order -> {size, chunk: [block ids]}
-function assembleFiles(files, blockDir) {
+// files: segment paths in playback order -> {size, chunk: [block ids]}.
+// skip(i): bytes at the start of file i that are not part of the stream (Y4M segments:
+// every segment file carries its own header line, the assembled stream one -- the
+// first segment's; ADVICE r02: concatenated headers made an invalid Y4M stream).
+function assembleFiles(files, blockDir, skip) {
     fs.mkdirSync(blockDir, { recursive: true });
     const block = Buffer.alloc(BLOCK);
     let fill = 0, size = 0;
     const chunk = [];
-    files.forEach(function (f) {
+    files.forEach(function (f, fi) {
         const fd = fs.openSync(f, "r");
+        let pos = skip ? skip(fi, f) : 0;
         try {
             for (;;) {
-                const n = fs.readSync(fd, block, fill, BLOCK - fill, null);
+                const n = fs.readSync(fd, block, fill, BLOCK - fill, pos);
+                pos += Math.max(n, 0);
                 if (n <= 0) break;
                 fill += n;
                 size += n;
@@ -65,4 +70,11 @@ function readRange(assembled, blockDir, first, last) {
     return Buffer.concat(out);
 }
 
-module.exports = { BLOCK: BLOCK, assembleFiles: assembleFiles, readRange: readRange };
+// Y4M rendition segments -> one YUV4MPEG2 stream: the first file whole, the header
+// line of every later one dropped (all segments of a rendition share it)
+function assembleY4M(files, blockDir) {
+    const y4m = require("./y4m");
+    return assembleFiles(files, blockDir, function (i, f) { return i ? y4m.headerBytes(f) : 0; });
+}
+
+module.exports = { BLOCK: BLOCK, assembleFiles: assembleFiles, assembleY4M: assembleY4M, readRange: readRange };

@@ -173,6 +173,62 @@ function fpsFrames(addon, n, srcFps, outFps) {
     return addon.fpsMap(n, srcFps[0], srcFps[1], r[0], r[1]);
 }
 
+// A segment's summed quality record from per-frame statistics (the addon's qstat
+// objects): {frames, sse: [y, u, v], ssimSum: [y, u, v]} -- the running sums vf_psnr /
+// vf_ssim keep (SSE exact; SSIM as the per-plane window sums), which add across segments.
+function rawQuality(stats, w, h) {
+    const pw = [w, (w + 1) >> 1, (w + 1) >> 1], ph = [h, (h + 1) >> 1, (h + 1) >> 1];
+    const nw = [0, 1, 2].map(function (c) { return ((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1); });
+    const comp = ["y", "u", "v"], raw = { frames: stats.length, sse: [0, 0, 0], ssimSum: [0, 0, 0] };
+    stats.forEach(function (q) {
+        comp.forEach(function (c, i) {
+            raw.sse[i] += q.sse[c];
+            raw.ssimSum[i] += q.ssim[c] * nw[i];
+        });
+    });
+    return raw;
+}
+
+function addRaw(list) {
+    const r = { frames: 0, sse: [0, 0, 0], ssimSum: [0, 0, 0] };
+    list.forEach(function (x) {
+        r.frames += x.frames;
+        for (let i = 0; i < 3; ++i) {
+            r.sse[i] += x.sse[i];
+            r.ssimSum[i] += x.ssimSum[i];
+        }
+    });
+    return r;
+}
+
+// vf_psnr / vf_ssim end-of-stream averages of a summed record: PSNR from the mean MSE
+// (per plane and area-weighted overall), mean SSIM (as dts_qstat_stream)
+function summarizeRaw(raw, w, h) {
+    const pw = [w, (w + 1) >> 1, (w + 1) >> 1], ph = [h, (h + 1) >> 1, (h + 1) >> 1];
+    const area = pw[0] * ph[0] + pw[1] * ph[1] + pw[2] * ph[2], n = raw.frames;
+    const psnr = function (m) { return m === 0 ? "inf" : 10 * Math.log10(255 * 255 / m); };   // JSON has no Infinity
+    const comp = ["y", "u", "v"], r = { frames: n, psnr: {}, ssim: {} };
+    let mseAvg = 0, ssimAll = 0;
+    comp.forEach(function (c, i) {
+        const mse = raw.sse[i] / (n * pw[i] * ph[i]);
+        const nw = ((pw[i] >> 2) - 1) * ((ph[i] >> 2) - 1);
+        r.psnr[c] = psnr(mse);
+        r.ssim[c] = raw.ssimSum[i] / (n * nw);
+        mseAvg += mse * pw[i] * ph[i] / area;
+        ssimAll += r.ssim[c] * pw[i] * ph[i] / area;
+    });
+    r.psnr.avg = psnr(mseAvg);
+    r.ssim.all = ssimAll;
+    return r;
+}
+
+// the same from the addon's qstatStream() object
+function summaryOfStat(q, raw) {
+    const f = function (x) { return x === Infinity ? "inf" : x; };
+    return { frames: raw.frames, psnr: { y: f(q.psnr.y), u: f(q.psnr.u), v: f(q.psnr.v), avg: f(q.psnrAvg) },
+             ssim: { y: q.ssim.y, u: q.ssim.u, v: q.ssim.v, all: q.ssimAll } };
+}
+
 // Segment summary of per-frame statistics, as vf_psnr / vf_ssim print at the end of
 // a stream: PSNR from the mean MSE (per plane and area-weighted overall), mean SSIM.
 function summarizeQuality(stats, w, h) {
@@ -203,4 +259,5 @@ function summarizeQuality(stats, w, h) {
 module.exports = { FMT: FMT, METHOD: METHOD, TONEMAP: TONEMAP, MAX_OUTPUTS: MAX_OUTPUTS, parseSettings: parseSettings,
                    outputOf: outputOf, tonemapOf: tonemapOf, qualityOf: qualityOf, deintOf: deintOf, rangeOf: rangeOf,
                    planLadders: planLadders,
-                   rateOf: rateOf, fpsFrames: fpsFrames, summarizeQuality: summarizeQuality };
+                   rateOf: rateOf, fpsFrames: fpsFrames, summarizeQuality: summarizeQuality, rawQuality: rawQuality,
+                   addRaw: addRaw, summarizeRaw: summarizeRaw, summaryOfStat: summaryOfStat };

@@ -56,6 +56,9 @@ function allocFrame(w, h, fmt) {
     return { data: data, pitch: pitch };
 }
 
+// A source maps (plan, frame indices) to host frames, each carrying its source index
+// (`frame.index`); indices past the end of the stream are dropped (the last segment of
+// a job is usually short).
 // default source: the deterministic testsrc2-like generator of libdts (the
 // segment's frames are its global frame indices); a real deployment passes a
 // decoder here (host libavcodec, out of the GPU path)
@@ -65,19 +68,35 @@ function synthSource(addon, seed) {
         return frameIdx.map(function (i) {
             const f = allocFrame(s.w, s.h, s.fmt);
             addon.synthFrame(s.w, s.h, s.fmt, 0, seed >>> 0, i, f);
+            f.index = i;
             return f;
         });
     };
 }
 
-// Y4M source: frame indices past the end of the file are dropped (the last segment
-// of a job is usually short)
+// Y4M source (a file read at random, or a pipe read in order: y4m.js Y4MReader).  Each
+// index is read once per request (vf_fps may repeat a frame); a stream reader keeps the
+// frames it has read until the scheduler releases them (release(sourceID, below)).
 function y4mSource(readers) {
-    return function (plan, frameIdx) {
+    const src = function (plan, frameIdx) {
         const r = readers[plan.sourceID];
         if (!r) throw new Error("source " + plan.sourceID + " has no Y4M path");
-        return frameIdx.filter(function (i) { return i < r.frames; }).map(function (i) { return r.read(i); });
+        const got = new Map();
+        frameIdx.forEach(function (i) {
+            if (got.has(i) || i >= r.frames) return;
+            const f = r.read(i);
+            if (f) {
+                f.index = i;
+                got.set(i, f);
+            }
+        });
+        return frameIdx.filter(function (i) { return got.has(i); }).map(function (i) { return got.get(i); });
     };
+    src.release = function (sourceID, below) {
+        const r = readers[sourceID];
+        if (r && r.release) r.release(below);
+    };
+    return src;
 }
 
 class GpuSegmentScheduler extends EventEmitter {
@@ -147,30 +166,33 @@ class GpuSegmentScheduler extends EventEmitter {
         return { dst: dst, per: per };
     }
 
-    // source frames a stream holds (Y4M file), Infinity for the synthetic source
-    _sourceFrames(plan) {
-        const r = this.readers[plan.sourceID];
-        return r ? r.frames : Infinity;
-    }
-
     async _runSegment(slot, task) {
         const self = this;
         const plan = task.plan;
         const t0 = Date.now();
         const g = this._graph(slot, plan);
-        let idx = this._frames(plan, task.chunkOffset, plan.srcFps);
-        let sel = null;
+        const idx = this._frames(plan, task.chunkOffset, plan.srcFps);
+        let sel = null, src;
         if (plan.spec.deint) {
             // yadif needs each frame's neighbours in the source stream: the graph runs on the
-            // segment's contiguous frames plus one context frame each side (clamped: yadif's
-            // clone at the stream ends); the vf_fps selection is applied to its outputs
-            const base = task.chunkOffset * this.segmentFrames, total = this._sourceFrames(plan);
-            const n = Math.max(0, Math.min(this.segmentFrames, total - base));
-            sel = idx.filter(function (i) { return i < base + n; }).map(function (i) { return i - base; });
-            idx = n ? [Math.max(base - 1, 0)].concat(Array.from({ length: n }, function (_, i) { return base + i; }),
-                                                      [Math.min(base + n, total - 1)]) : [];
+            // segment's contiguous frames plus one context frame each side (yadif's clone of
+            // the first / last frame at the stream ends); the vf_fps selection is applied to
+            // its outputs.  The stream's length need not be known up front (a pipe).
+            const segN = this.segmentFrames, base = task.chunkOffset * segN;
+            const want = (base > 0 ? [base - 1] : []).concat(Array.from({ length: segN + 1 }, function (_, i) { return base + i; }));
+            const got = await this.source(plan, want);
+            const real = got.filter(function (f) { return f.index >= base && f.index < base + segN; });
+            const n = real.length;
+            sel = idx.map(function (i) { return i - base; }).filter(function (i) { return i < n; });
+            src = [];
+            if (n) {
+                const prev = got.find(function (f) { return f.index === base - 1; }) || real[0];
+                const next = got.find(function (f) { return f.index === base + n; }) || real[n - 1];
+                src = [prev].concat(real, [next]);
+            }
+        } else {
+            src = await this.source(plan, idx);
         }
-        const src = await this.source(plan, idx);
         const t1 = Date.now();
         const outs = plan.spec.outputs;
         const nout = plan.spec.deint ? Math.max(0, src.length - 2) : src.length;
@@ -188,7 +210,7 @@ class GpuSegmentScheduler extends EventEmitter {
                 if (!plan.quality.rows[k]) continue;
                 const st = await this.addon.quality(this._ctx(slot), outs[k].w, outs[k].h, outs[k].fmt, o.per[k],
                                                     ref.per[k]);
-                const sum = ladder.summarizeQuality(st, outs[k].w, outs[k].h);
+                const sum = this._qsummary(ladder.rawQuality(st, outs[k].w, outs[k].h), outs[k].w, outs[k].h);
                 if (!(plan.quality.rows[k] & 1)) delete sum.psnr;
                 if (!(plan.quality.rows[k] & 2)) delete sum.ssim;
                 quality[k] = sum;
@@ -227,18 +249,59 @@ class GpuSegmentScheduler extends EventEmitter {
         });
     }
 
-    // every chunk of a job done -> its segments assembled into 1 MiB blocks
+    // vf_psnr / vf_ssim end-of-stream averages of a summed record (the addon's
+    // dts_qstat_stream when it has it, else the same formulas in ladder.js)
+    _qsummary(raw, w, h) {
+        const r = this.addon.qstatStream ? ladder.summaryOfStat(this.addon.qstatStream(w, h, raw.sse, raw.ssimSum, raw.frames), raw)
+                                         : ladder.summarizeRaw(raw, w, h);
+        r.raw = raw;
+        return r;
+    }
+
+    // A job whose chunks are all here and done: chunkOffsets exactly 0 .. Jobs.chunks - 1
+    // (database.js:79).  A worker that was given only some of a job's chunks -- the usual
+    // case in a pool -- leaves the job alone (ADVICE r02: it used to publish a truncated
+    // output as finished); the worker the job names in Jobs.assemble gets every row.
+    _completeJob(job, chunks) {
+        const mine = chunks.filter(function (c) { return c.mainJob === job.id; });
+        if (!mine.length || mine.some(function (c) { return c.status !== "done"; })) return null;
+        mine.sort(function (a, b) { return a.chunkOffset - b.chunkOffset; });
+        const n = typeof job.chunks === "number" ? job.chunks : NaN;
+        if (mine.length !== n || mine.some(function (c, i) { return c.chunkOffset !== i; })) return null;
+        return mine;
+    }
+
+    // every chunk of a job done -> the job's quality (every segment's summed record,
+    // combined as vf_psnr / vf_ssim average a whole stream) and, with outDir, its
+    // segments assembled into 1 MiB blocks of one Y4M stream
     _assembleJobs(jobs, chunks) {
         const self = this;
-        if (!this.outDir || this.sink) return;
         jobs.forEach(function (job) {
-            const mine = chunks.filter(function (c) { return c.mainJob === job.id; });
-            if (!mine.length || mine.some(function (c) { return c.status !== "done"; })) return;
-            mine.sort(function (a, b) { return a.chunkOffset - b.chunkOffset; });
-            const files = mine.map(function (c) { return self._segmentPath(job.id, c.chunkOffset); });
+            const mine = self._completeJob(job, chunks);
+            if (!mine) return;
             try {
-                const a = assemble.assembleFiles(files, path.join(self.outDir, "blocks"));
-                const fields = { assembledData: JSON.stringify(a), finished: true };
+                const fields = {};
+                const recs = mine.map(function (c) {
+                    try {
+                        return JSON.parse(c.result || "{}");
+                    } catch (e) {
+                        return {};
+                    }
+                });
+                if (recs.every(function (r) { return r.quality && r.quality.raw; })) {
+                    const raw = ladder.addRaw(recs.map(function (r) { return r.quality.raw; }));
+                    const q = self._qsummary(raw, recs[0].width, recs[0].height);
+                    delete q.raw;
+                    q.segments = mine.length;
+                    fields.quality = JSON.stringify(q);
+                }
+                if (self.outDir && !self.sink) {
+                    const files = mine.map(function (c, i) { return recs[i].file || self._segmentPath(job.id, c.chunkOffset); });
+                    const a = assemble.assembleY4M(files, path.join(self.outDir, "blocks"));
+                    fields.assembledData = JSON.stringify(a);
+                    fields.finished = true;
+                }
+                if (!Object.keys(fields).length) return;
                 Object.keys(fields).forEach(function (k) { job[k] = fields[k]; });
                 self.onJobUpdate(job, fields);
                 self.emit("jobUpdate", job, fields);
@@ -246,6 +309,25 @@ class GpuSegmentScheduler extends EventEmitter {
                 self.emit("updateError", e, job, null);
             }
         });
+    }
+
+    // a stream source keeps frames until no pending segment can ask for them again
+    _releaseFrames(queue, inflight) {
+        if (!this.source.release) return;
+        const self = this, low = new Map();
+        queue.concat(inflight).forEach(function (t) {
+            const sid = String(t.plan.sourceID), b = t.chunkOffset * self.segmentFrames - 1;
+            low.set(sid, low.has(sid) ? Math.min(low.get(sid), b) : b);
+        });
+        Object.keys(this.readers).forEach(function (sid) {
+            self.source.release(sid, low.has(sid) ? low.get(sid) : Infinity);
+        });
+    }
+
+    _closeReaders() {
+        const self = this;
+        Object.keys(this.readers).forEach(function (sid) { self.readers[sid].close(); });
+        this.readers = {};
     }
 
     // jobs: Jobs rows of one or more ladders; chunks: their JobChunks rows;
@@ -262,7 +344,7 @@ class GpuSegmentScheduler extends EventEmitter {
                 self.readers[sid] = r;
                 s.w = s.w || r.hdr.w;
                 s.h = s.h || r.hdr.h;
-                s.fmt = s.fmt || 0;
+                s.fmt = s.fmt === undefined ? r.hdr.fmt : s.fmt;
                 s.fps = s.fps || r.hdr.fps;
             });
             if (Object.keys(this.readers).length && !this._userSource) this.source = y4mSource(this.readers);
@@ -286,6 +368,8 @@ class GpuSegmentScheduler extends EventEmitter {
                 queue.push({ plan: plan, chunkOffset: off, rows: rows, tries: 0, lastGpu: -1 });
             });
         });
+        // segments in stream order across ladders (a pipe source is read once, front to back)
+        queue.sort(function (a, b) { return a.chunkOffset - b.chunkOffset; });
         const total = queue.length;
         let finished = 0;
         function safeUpdate(r, fields) {
@@ -295,11 +379,14 @@ class GpuSegmentScheduler extends EventEmitter {
                 self.emit("updateError", e, r, fields);
             }
         }
+        const inflight = [];
         return new Promise(function (resolve) {
-            if (!total) {
+            function finish() {
                 self._assembleJobs(jobs, chunks);
-                return resolve(self._summary(0));
+                self._closeReaders();
+                resolve(self._summary(total));
             }
+            if (!total) return finish();
             function pull(slot) {
                 if (slot.busy) return;
                 // prefer a task that did not just fail on this GPU
@@ -307,6 +394,7 @@ class GpuSegmentScheduler extends EventEmitter {
                 if (i < 0 && queue.length && self.slots.length === 1) i = 0;
                 if (i < 0) return;
                 const task = queue.splice(i, 1)[0];
+                inflight.push(task);
                 slot.busy = true;
                 task.rows.forEach(function (r) {
                     if (r) safeUpdate(r, { assignedTo: self.workerId, status: "assigned" });
@@ -349,10 +437,13 @@ class GpuSegmentScheduler extends EventEmitter {
                     self.emit("updateError", e, null, null);
                 }).then(function () {
                     slot.busy = false;
-                    if (finished === total) {
-                        self._assembleJobs(jobs, chunks);
-                        return resolve(self._summary(total));
+                    inflight.splice(inflight.indexOf(task), 1);
+                    try {
+                        self._releaseFrames(queue, inflight);
+                    } catch (e) {
+                        self.emit("updateError", e, null, null);
                     }
+                    if (finished === total) return finish();
                     self.slots.forEach(pull);
                 });
             }

@@ -192,7 +192,7 @@ function testY4MRoundTrip() {
     assert.strictEqual(f3.data[0][3], 7);
     assert.strictEqual(f3.data[1][cw * ch - 1], 103);
     assert.strictEqual(f3.data[2][0], 203);
-    assert.throws(function () { r.read(5); }, /out of range/);
+    assert.strictEqual(r.read(5), null);                                  // past the end
     r.close();
     // nv12 rendition -> planar Y4M record (de-interleaved chroma)
     const nv = { data: [Buffer.alloc(w * h, 1), Buffer.alloc(ch * 2 * cw), null], pitch: [w, 2 * cw, 0] };
@@ -249,8 +249,8 @@ async function testY4MJobAssembled() {
         return { data: [Buffer.alloc(W * H, i), Buffer.alloc(32 * 18, 128), Buffer.alloc(32 * 18, 128)], pitch: [W, 32, 32] };
     });
     const addon = fakeAddon({ devices: 2 });
-    const jobs = [{ id: 21, sourceID: 3, width: 32, height: 18, framerate: 60, codecSettings: '{"quality": "both"}' },
-                  { id: 22, sourceID: 3, width: 16, height: 10, framerate: 60, codecSettings: null }];
+    const jobs = [{ id: 21, sourceID: 3, width: 32, height: 18, framerate: 60, chunks: 3, codecSettings: '{"quality": "both"}' },
+                  { id: 22, sourceID: 3, width: 16, height: 10, framerate: 60, chunks: 3, codecSettings: null }];
     const chunks = [];
     let id = 1;
     jobs.forEach(function (j) { for (let o = 0; o < 3; o++) chunks.push({ id: id++, mainJob: j.id, chunkOffset: o, status: null }); });
@@ -276,12 +276,27 @@ async function testY4MJobAssembled() {
         assert.strictEqual(j.finished, true);
         const a = JSON.parse(j.assembledData);
         const files = chunks.filter(function (c) { return c.mainJob === j.id; })
+            .sort(function (x, y) { return x.chunkOffset - y.chunkOffset; })
             .map(function (c) { return JSON.parse(c.result).file; });
-        const total = files.reduce(function (x, f) { return x + fs.statSync(f).size; }, 0);
+        // one YUV4MPEG2 stream: the first segment's header, every segment's FRAME records
+        const hb = y4m.headerBytes(files[0]);
+        const total = files.reduce(function (x, f) { return x + fs.statSync(f).size; }, 0) - (files.length - 1) * hb;
         assert.strictEqual(a.size, total);
         assert.strictEqual(a.chunk.length, Math.ceil(total / 1048576));
+        const whole = path.join(d, "whole" + j.id + ".y4m");
+        fs.writeFileSync(whole, assemble.readRange(a, path.join(d, "blocks"), 0, a.size - 1));
+        const rd = new y4m.Y4MReader(whole);
+        assert.strictEqual(rd.frames, 14);
+        for (let i = 0; i < 14; ++i) assert.strictEqual(rd.read(i).data[0][0], i);
+        rd.close();
     });
     assert.deepStrictEqual(updates.sort(), [[21, true], [22, true]]);
+    // job-level quality on the row that asked for it: the summed segment records
+    const q21 = JSON.parse(jobs[0].quality);
+    assert.strictEqual(q21.frames, 14);
+    assert.strictEqual(q21.segments, 3);
+    assert.ok(q21.psnr.avg === "inf" && q21.ssim.all > 0.99, JSON.stringify(q21));   // stand-in: identical
+    assert.strictEqual(jobs[1].quality, undefined);
     assert.ok(addon.stats.quality >= 3);
 }
 
@@ -313,6 +328,7 @@ async function testDeinterlaceWithRateChange() {
         const r = JSON.parse(c.result);
         const rd = new y4m.Y4MReader(r.file);
         const got = Array.from({ length: rd.frames }, function (_, i) { return rd.read(i).data[0][0]; });
+        assert.strictEqual(jobs[0].finished, undefined);            // Jobs.chunks unknown: not assembled
         rd.close();
         const want = { 0: [0, 2, 4], 1: [6, 8, 10], 2: [12] }[c.chunkOffset];
         assert.deepStrictEqual(got, want, "chunk " + c.chunkOffset);
@@ -321,6 +337,88 @@ async function testDeinterlaceWithRateChange() {
         ladder.planLadders([{ id: 1, sourceID: 1, width: 8, height: 8, codecSettings: '{"deinterlace": {"mode": 1}}' }],
                            { 1: { w: 16, h: 16, fmt: 0 } });
     }, /frame-rate modes/);
+}
+
+function testY4M10BitAndHeaders() {
+    // C420p10 <-> p010 host frames; a long header line; FRAME parameters on a stream
+    const d = tmpdir(), p = path.join(d, "p10.y4m");
+    const w = 6, h = 4, cw = 3, ch = 2;
+    const f = { data: [Buffer.alloc(2 * w * h), Buffer.alloc(4 * cw * ch), null], pitch: [2 * w, 4 * cw, 0] };
+    for (let i = 0; i < w * h; ++i) f.data[0].writeUInt16LE(((i * 37) & 1023) << 6, 2 * i);
+    for (let i = 0; i < cw * ch; ++i) {
+        f.data[1].writeUInt16LE(((i * 91 + 5) & 1023) << 6, 4 * i);
+        f.data[1].writeUInt16LE(((i * 13 + 700) & 1023) << 6, 4 * i + 2);
+    }
+    const wr = new y4m.Y4MWriter(p, w, h, [24, 1], y4m.FMT_P010LE);
+    wr.write(f);
+    wr.write(f);
+    assert.strictEqual(wr.close(), fs.statSync(p).size);
+    const r = new y4m.Y4MReader(p);
+    assert.deepStrictEqual([r.hdr.bits, r.hdr.fmt, r.frames], [10, y4m.FMT_P010LE, 2]);
+    const g = r.read(1);
+    assert.ok(g.data[0].equals(f.data[0]) && g.data[1].equals(f.data[1]));
+    r.close();
+    // record layout: planar 10-bit little-endian samples
+    const raw = fs.readFileSync(p);
+    const o = y4m.headerBytes(p) + 6;
+    assert.strictEqual(raw.readUInt16LE(o + 2), 37);
+    assert.strictEqual(raw.readUInt16LE(o + 2 * w * h + 2), 96);                  // U[1]
+    assert.strictEqual(raw.readUInt16LE(o + 2 * (w * h + cw * ch)), 700);         // V[0]
+    // a header with many tags (> 512 bytes) and FRAME parameters, read as a stream
+    const q = path.join(d, "long.y4m");
+    const tags = Array.from({ length: 80 }, function (_, i) { return "XTAG" + i + "=abcdef"; }).join(" ");
+    const rec = Buffer.alloc(w * h + 2 * cw * ch, 9);
+    fs.writeFileSync(q, Buffer.concat([Buffer.from("YUV4MPEG2 W6 H4 F30:1 C420jpeg " + tags + "\n"),
+                                       Buffer.from("FRAME Ixyz\n"), rec, Buffer.from("FRAME\n"), rec]));
+    assert.ok(y4m.headerBytes(q) > 512);
+    const fd = fs.openSync(q, "r");
+    const st = new y4m.Y4MReader(fd);
+    st.seekable = false;                     // (a regular file read as a stream: past its header)
+    fs.readSync(fd, Buffer.alloc(st.hdr.headerBytes), 0, st.hdr.headerBytes, null);
+    st.frames = Infinity;
+    st.next = 0;
+    st.kept = new Map();
+    assert.strictEqual(st.read(1).data[0][0], 9);
+    assert.strictEqual(st.read(0).data[2][0], 9);                 // kept until released
+    st.release(2);
+    assert.throws(function () { st.read(0); }, /released/);
+    assert.strictEqual(st.read(2), null);
+    assert.strictEqual(st.frames, 2);
+    fs.closeSync(fd);
+}
+
+async function testPipeSourceAndPartialJob() {
+    // a FIFO source (read in order, never seeked) through the scheduler; a job whose
+    // Jobs.chunks exceeds the rows this worker got is left unassembled (ADVICE r02)
+    const d = tmpdir(), src = path.join(d, "src.y4m"), fifo = path.join(d, "src.fifo");
+    y4m.writeFile(src, 32, 18, [60, 1], 10, function (i) {
+        return { data: [Buffer.alloc(32 * 18, i), Buffer.alloc(16 * 9, 128), Buffer.alloc(16 * 9, 128)], pitch: [32, 16, 16] };
+    });
+    require("child_process").execFileSync("mkfifo", [fifo]);
+    const feeder = require("child_process").spawn("sh", ["-c", "cat \"$0\" > \"$1\"", src, fifo]);
+    const addon = fakeAddon({ devices: 2 });
+    const jobs = [{ id: 51, sourceID: 4, width: 16, height: 10, framerate: 30, chunks: 3, codecSettings: null },
+                  { id: 52, sourceID: 4, width: 8, height: 6, framerate: 60, chunks: 4, codecSettings: null }];
+    const chunks = [];
+    [0, 1, 2].forEach(function (o) { chunks.push({ id: 60 + o, mainJob: 51, chunkOffset: o, status: null }); });
+    [0, 1, 2].forEach(function (o) { chunks.push({ id: 70 + o, mainJob: 52, chunkOffset: o, status: null }); });
+    const s = new GpuSegmentScheduler({ addon: addon, segmentFrames: 4, outDir: d });
+    await s.runJobs(jobs, chunks, { 4: { path: fifo } });
+    await new Promise(function (res) { feeder.on("exit", res); if (feeder.exitCode !== null) res(); });
+    chunks.forEach(function (c) {
+        assert.strictEqual(c.status, "done", c.result);
+        const r = JSON.parse(c.result);
+        const rd = new y4m.Y4MReader(r.file);
+        const got = Array.from({ length: rd.frames }, function (_, i) { return rd.read(i).data[0][0]; });
+        rd.close();
+        const base = 4 * c.chunkOffset;
+        const want = (c.mainJob === 51 ? [0, 2] : [0, 1, 2, 3]).map(function (i) { return base + i; })
+            .filter(function (i) { return i < 10; });
+        assert.deepStrictEqual(got, want, "job " + c.mainJob + " chunk " + c.chunkOffset);
+    });
+    assert.strictEqual(jobs[0].finished, true);
+    assert.strictEqual(jobs[1].finished, undefined);             // 3 of 4 chunks here: not this worker's to assemble
+    assert.deepStrictEqual(Object.keys(s.readers), []);          // readers closed
 }
 
 function testNoDevicesIsLoud() {
@@ -340,5 +438,7 @@ function testNoDevicesIsLoud() {
     testQualitySummary();
     await testY4MJobAssembled();
     await testDeinterlaceWithRateChange();
+    testY4M10BitAndHeaders();
+    await testPipeSourceAndPartialJob();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });
