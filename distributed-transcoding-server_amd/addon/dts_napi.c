@@ -149,6 +149,10 @@ static int parse_spec(napi_env env, napi_value o, dts_graph_spec *s)
         if (get_i32(env, oi, "w", 0, &os->w) || get_i32(env, oi, "h", 0, &os->h) ||
             get_i32(env, oi, "fmt", DTS_FMT_NV12, &os->fmt) || get_i32(env, oi, "method", DTS_SCALE_BICUBIC, &os->method))
             return -1;
+        /* rendition quality: {quality: DTS_Q_*, qrefMethod: DTS_SCALE_*} (dts_output_spec, ABI 6) */
+        if (get_i32(env, oi, "quality", 0, &os->quality) ||
+            get_i32(env, oi, "qrefMethod", DTS_SCALE_LANCZOS, &os->qref_method))
+            return -1;
         os->param[0] = os->param[1] = DTS_PARAM_DEFAULT;
         napi_has_named_property(env, oi, "param", &has);
         if (has) {
@@ -342,7 +346,9 @@ typedef struct {
     dts_graph *g;
     dts_frame *src, *dst, *qref;
     dts_qstat *q;
-    int n, status;
+    int n, nq, status;           /* nq: statistics per frame (rendition quality: nout) */
+    int rq[DTS_MAX_OUTPUTS];     /* output k carries rendition quality */
+    int nout;
 } run_job;
 
 static void free_job(run_job *j)
@@ -399,7 +405,22 @@ static void run_complete(napi_env env, napi_status st, void *data)
         napi_reject_deferred(env, j->deferred, err);
     } else {
         napi_value res;
-        if (j->q) {
+        if (j->q && j->nq > 1) {        /* rendition quality: res[f][k] (null for outputs without it) */
+            napi_create_array_with_length(env, (size_t)j->n, &res);
+            for (int i = 0; i < j->n; ++i) {
+                napi_value row;
+                napi_create_array_with_length(env, (size_t)j->nout, &row);
+                for (int k = 0; k < j->nout; ++k) {
+                    napi_value v;
+                    if (j->rq[k])
+                        v = qstat_obj(env, &j->q[(size_t)i * j->nout + k]);
+                    else
+                        napi_get_null(env, &v);
+                    napi_set_element(env, row, (uint32_t)k, v);
+                }
+                napi_set_element(env, res, (uint32_t)i, row);
+            }
+        } else if (j->q) {
             napi_create_array_with_length(env, (size_t)j->n, &res);
             for (int i = 0; i < j->n; ++i) napi_set_element(env, res, (uint32_t)i, qstat_obj(env, &j->q[i]));
         } else {
@@ -443,9 +464,20 @@ static napi_value js_run(napi_env env, napi_callback_info info)
         return throw_dts(env, DTS_E_INVAL, "run: dst must hold (src.length - context) * outputs frames (frame-major)");
     }
     j->n = (int)(ns - cf);
+    j->nout = s->nout;
+    int any_rq = 0;
+    for (int k = 0; k < s->nout; ++k) any_rq |= j->rq[k] = s->out[k].quality != 0;
+    if (any_rq) {                                 /* rendition quality: nout statistics per frame */
+        j->nq = s->nout;
+        j->q = (dts_qstat *)calloc(j->n ? (size_t)j->n * s->nout : 1, sizeof(dts_qstat));
+        if (!j->q) {
+            free_job(j);
+            return throw_dts(env, DTS_E_NOMEM, "run");
+        }
+    }
     napi_valuetype qt = napi_undefined;
     if (argc >= 4) napi_typeof(env, argv[3], &qt);
-    if (qt == napi_object) {
+    if (qt == napi_object && !any_rq) {
         const int qo = s->quality_out;
         if (!s->quality || parse_frames(env, argv[3], &j->qref, &nq, &ow[qo], &oh[qo], &of[qo], 1) ||
             nq != (uint32_t)j->n) {
@@ -567,6 +599,36 @@ static napi_value js_quality(napi_env env, napi_callback_info info)
 }
 
 /* ---- synthFrame(w, h, fmt, pattern, seed, index, frame) ---------------- */
+/* ---- qstatStream(w, h, sse[3], ssimSum[3], frames) -> qstat ---------------- */
+/* vf_psnr / vf_ssim end-of-stream averages from a summed record (dts_qstat_stream) */
+static napi_value js_qstat_stream(napi_env env, napi_callback_info info)
+{
+    size_t argc = 5;
+    napi_value argv[5];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 5) return throw_dts(env, DTS_E_INVAL, "qstatStream(w, h, sse, ssimSum, frames)");
+    int32_t w = 0, h = 0;
+    int64_t n = 0;
+    napi_get_value_int32(env, argv[0], &w);
+    napi_get_value_int32(env, argv[1], &h);
+    napi_get_value_int64(env, argv[4], &n);
+    dts_qraw r;
+    memset(&r, 0, sizeof r);
+    for (uint32_t c = 0; c < 3; ++c) {
+        napi_value v;
+        double d = 0;
+        if (napi_get_element(env, argv[2], c, &v) != napi_ok || napi_get_value_double(env, v, &d) != napi_ok)
+            return throw_dts(env, DTS_E_INVAL, "qstatStream: sse");
+        r.sse[c] = (uint64_t)d;
+        if (napi_get_element(env, argv[3], c, &v) != napi_ok || napi_get_value_double(env, v, &r.ssim_sum[c]) != napi_ok)
+            return throw_dts(env, DTS_E_INVAL, "qstatStream: ssimSum");
+    }
+    dts_qstat q;
+    const int e = dts_qstat_stream(w, h, &r, n, &q);
+    if (e) return throw_dts(env, e, "dts_qstat_stream");
+    return qstat_obj(env, &q);
+}
+
 static napi_value js_synth_frame(napi_env env, napi_callback_info info)
 {
     size_t argc = 7;
@@ -667,6 +729,7 @@ static napi_value init(napi_env env, napi_value exports)
         {"frameLayout", NULL, js_frame_layout, NULL, NULL, NULL, napi_default, NULL},
         {"fpsMap", NULL, js_fps_map, NULL, NULL, NULL, napi_default, NULL},
         {"quality", NULL, js_quality, NULL, NULL, NULL, napi_default, NULL},
+        {"qstatStream", NULL, js_qstat_stream, NULL, NULL, NULL, napi_default, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

@@ -43,6 +43,10 @@ struct QScratch {
     void *dp = nullptr;
     size_t dbytes = 0;
     hipEvent_t dev = nullptr;
+    // the reference renditions of rendition quality (one batch of each), ordered the same way
+    void *rp = nullptr;
+    size_t rbytes = 0;
+    hipEvent_t rev = nullptr;
 };
 
 struct dts_ctx {
@@ -227,6 +231,11 @@ struct dts_graph {
     unsigned hdr_next = 0;
     TonemapParams tm{};
     float *dev_tm_lut = nullptr;          // the transfer-curve tables of tm (TonemapParams::lut)
+    // rendition quality (dts_output_spec.quality): a graph of the reference renditions
+    // (output j of ref = this graph's output rq_out[j], scaled with its qref_method)
+    dts_graph *ref = nullptr;
+    int nrq = 0;
+    int rq_out[DTS_MAX_OUTPUTS] = {};
 };
 
 // ---------------------------------------------------------------------------
@@ -461,6 +470,13 @@ int validate_spec(const dts_graph_spec &s)
     if ((s.range & 1) != ((s.range >> 4) & 1) && (s.hdr_to_sdr || s.src_fmt != DTS_FMT_YUV420P))
         return DTS_E_UNSUPPORTED;                                // range conversion: k_ladder7 sources only
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
+    for (int k = 0; k < s.nout; ++k) {                  // rendition quality (ABI 6)
+        const dts_output_spec &o = s.out[k];
+        if (o.quality < 0 || o.quality > DTS_Q_BOTH) return DTS_E_INVAL;
+        if (!o.quality) continue;
+        if (!method_ok(o.qref_method)) return DTS_E_UNSUPPORTED;
+        if (s.quality || s.hdr_to_sdr || !fmt_8bit(o.fmt)) return DTS_E_UNSUPPORTED;
+    }
     if (s.quality && !fmt_8bit(s.out[s.quality_out].fmt)) return DTS_E_UNSUPPORTED;   // vf_psnr/vf_ssim: 8-bit
     if (s.deint) {                                        // yadif ahead of the ladder: 8-bit yuv420p, frame modes
         if (s.deint != 1 || s.src_fmt != DTS_FMT_YUV420P || s.hdr_to_sdr) return DTS_E_UNSUPPORTED;
@@ -733,7 +749,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.5 (gfx950; abi 5)"; }
+const char *dts_version(void) { return "dts-mi355x 0.6 (gfx950; abi 6)"; }
 
 const char *dts_strerror(int err)
 {
@@ -788,8 +804,13 @@ static void qscratch_free(QScratch &q)
         hipEventSynchronize(q.dev);
         hipEventDestroy(q.dev);
     }
+    if (q.rev) {
+        hipEventSynchronize(q.rev);
+        hipEventDestroy(q.rev);
+    }
     if (q.p) hipFree(q.p);
     if (q.dp) hipFree(q.dp);
+    if (q.rp) hipFree(q.rp);
     q = QScratch{};
 }
 
@@ -1098,6 +1119,31 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
             }
         }
         if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt);
+        // rendition quality: the reference renditions are a graph of their own over the same
+        // source (deinterlaced first when the graph deinterlaces: it runs on our yadif output)
+        dts_graph_spec rs = s;
+        rs.nout = 0;
+        rs.quality = 0;
+        rs.deint = 0;
+        rs.max_batch = g->batch;
+        for (int k = 0; k < s.nout; ++k)
+            if (s.out[k].quality) {
+                dts_output_spec &o = rs.out[rs.nout];
+                o = s.out[k];
+                o.method = s.out[k].qref_method;
+                o.param[0] = o.param[1] = DTS_PARAM_DEFAULT;
+                o.quality = 0;
+                g->rq_out[rs.nout++] = k;
+            }
+        if (rs.nout) {
+            for (int k = rs.nout; k < DTS_MAX_OUTPUTS; ++k) rs.out[k] = dts_output_spec{};
+            e = dts_graph_create(ctx, &rs, &g->ref);
+            if (e) {
+                dts_graph_destroy(g);
+                return e;
+            }
+            g->nrq = rs.nout;
+        }
         *out = g;
         return DTS_OK;
     } catch (const std::bad_alloc &) {
@@ -1141,6 +1187,7 @@ void dts_graph_destroy(dts_graph *g)
             if (g->hdr_mid[sl][k]) hipFree(g->hdr_mid[sl][k]);
     }
     if (g->dev_tm_lut) hipFree(g->dev_tm_lut);
+    if (g->ref) dts_graph_destroy(g->ref);
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_tables5) hipFree(g->dev_tables5);
@@ -1464,6 +1511,72 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
     return DTS_OK;
 }
 
+// the reference-rendition buffer of a QScratch (same reuse rule as the quality partials)
+static int ensure_rscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
+{
+    if (!q.rev) HIPCHK(ctx, hipEventCreateWithFlags(&q.rev, hipEventDisableTiming));
+    if (q.rbytes >= bytes) return DTS_OK;
+    if (q.rp) {
+        HIPCHK(ctx, hipEventSynchronize(q.rev));
+        hipFree(q.rp);
+        q.rp = nullptr;
+        q.rbytes = 0;
+    }
+    HIPCHK(ctx, hipMalloc(&q.rp, bytes));
+    q.rbytes = bytes;
+    return DTS_OK;
+}
+
+// Rendition quality of frames f0 .. f0 + n - 1 of a call over `ntot` frames: per batch
+// the reference graph scales the same source frames (src, already deinterlaced) into a
+// scratch batch, then k_quality scores each rendition that asked for it against its
+// reference; records go to qraw[k * ntot + f] (vf_psnr / vf_ssim per frame, exactly as
+// the dts_quality_run_device path).
+static int rung_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, int f0, int n,
+                        int ntot, dts_qraw *qraw, hipStream_t st)
+{
+    dts_ctx *ctx = g->ctx;
+    const dts_graph_spec &s = g->spec;
+    dts_graph *r = g->ref;
+    const int B = g->batch;
+    size_t off[DTS_MAX_OUTPUTS], total = 0;
+    for (int j = 0; j < g->nrq; ++j) {
+        off[j] = total;
+        total += (size_t)B * (size_t)r->lay_out[j].fstride;
+    }
+    int e = ensure_rscratch(ctx, qs, total);
+    if (e) return e;
+    for (int c0 = 0; c0 < n; c0 += B) {
+        const int m = std::min(B, n - c0);
+        HIPCHK(ctx, hipStreamWaitEvent(st, qs.rev, 0));   // the buffer's previous user
+        DevPlanes sc = src, rd[DTS_MAX_OUTPUTS];
+        int rf[DTS_MAX_OUTPUTS];
+        for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src.fstride);
+        for (int j = 0; j < g->nrq; ++j) {
+            rd[j] = r->lay_out[j].planes(static_cast<uint8_t *>(qs.rp) + off[j]);
+            rf[j] = r->spec.out[j].fmt;
+        }
+        e = enqueue_ladder(r, sc, rd, rf, m, st);
+        if (e) return e;
+        for (int j = 0; j < g->nrq; ++j) {
+            const int k = g->rq_out[j];
+            const dts_output_spec &o = s.out[k];
+            dts_dev_frames a{}, b = dev_frames(static_cast<uint8_t *>(qs.rp) + off[j], r->lay_out[j]);
+            for (int pl = 0; pl < 3; ++pl) {
+                a.data[pl] = dst[k].data[pl] ? reinterpret_cast<void *>(dst[k].data[pl] +
+                                                                        (uint64_t)((int64_t)(c0 + 0) * dst[k].fstride))
+                                             : nullptr;
+                a.pitch[pl] = dst[k].pitch[pl];
+            }
+            a.frame_stride = dst[k].fstride;
+            e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, m, qraw + (int64_t)k * ntot + f0 + c0, st);
+            if (e) return e;
+        }
+        HIPCHK(ctx, hipEventRecord(qs.rev, st));
+    }
+    return DTS_OK;
+}
+
 static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
                       const dts_dev_frames *qref, dts_qraw *qraw_dev, void *stream)
 {
@@ -1506,6 +1619,10 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
             }
             e = enqueue_ladder(g, to_dev(dbuf, s.src_fmt), dd, dfmt, m, st);
             if (e) return e;
+            if (g->ref && qraw_dev) {
+                e = rung_quality(g, qs, to_dev(dbuf, s.src_fmt), dd, c0, m, nframes, qraw_dev, st);
+                if (e) return e;
+            }
             if (want_q) {
                 const dts_output_spec &o = s.out[s.quality_out];
                 dts_dev_frames qa = dst[s.quality_out], qb = *qref;
@@ -1521,8 +1638,12 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
         return DTS_OK;
     }
     const DevPlanes dsrc = to_dev(*src, s.src_fmt);
-    const int e = g->hdr ? enqueue_hdr(g, dsrc, ddst, nframes, st) : enqueue_ladder(g, dsrc, ddst, dfmt, nframes, st);
+    int e = g->hdr ? enqueue_hdr(g, dsrc, ddst, nframes, st) : enqueue_ladder(g, dsrc, ddst, dfmt, nframes, st);
     if (e) return e;
+    if (g->ref && qraw_dev) {
+        e = rung_quality(g, qs, dsrc, ddst, 0, nframes, nframes, qraw_dev, st);
+        if (e) return e;
+    }
     if (want_q) {
         const dts_output_spec &o = s.out[s.quality_out];
         return quality_enqueue(ctx, qs, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
@@ -1753,6 +1874,12 @@ static int alloc_host_path(dts_graph *g)
             HIPCHK(ctx, hipMalloc(&g->dev_qraw[sl], (size_t)B * sizeof(dts_qraw)));
             HIPCHK(ctx, hipHostMalloc(&g->pin_qraw[sl], (size_t)B * sizeof(dts_qraw), hipHostMallocDefault));
         }
+        if (g->ref) {                                    // rendition quality: B x nout records per slot
+            const size_t nb = (size_t)B * (size_t)s.nout * sizeof(dts_qraw);
+            HIPCHK(ctx, hipMalloc(&g->dev_qraw[sl], nb));
+            HIPCHK(ctx, hipMemset(g->dev_qraw[sl], 0, nb));
+            HIPCHK(ctx, hipHostMalloc(&g->pin_qraw[sl], nb, hipHostMallocDefault));
+        }
         HIPCHK(ctx, hipHostMalloc(&g->pin_in[sl], (size_t)g->pin_in_bytes, hipHostMallocDefault));
         HIPCHK(ctx, hipHostMalloc(&g->pin_out[sl], (size_t)g->pin_out_bytes, hipHostMallocDefault));
         HIPCHK(ctx, hipEventCreateWithFlags(&g->done[sl], hipEventDisableTiming));
@@ -1819,6 +1946,15 @@ static int finish_slot(dts_graph *g, int sl)
         const dts_output_spec &o = s.out[s.quality_out];
         dts_qstat_finalize(o.w, o.h, g->pin_qraw[sl], n, g->p_q + f0);
     }
+    if (g->ref && g->p_q) {                    // records [k][n] -> q[(f0 + f) * nout + k]
+        std::vector<dts_qstat> tmp((size_t)n);
+        for (int k = 0; k < s.nout; ++k) {
+            if (s.out[k].quality)
+                dts_qstat_finalize(s.out[k].w, s.out[k].h, g->pin_qraw[sl] + (int64_t)k * n, n, tmp.data());
+            for (int f = 0; f < n; ++f)
+                g->p_q[(int64_t)(f0 + f) * s.nout + k] = s.out[k].quality ? tmp[(size_t)f] : dts_qstat{};
+        }
+    }
     g->p_chunk_first[sl] = -1;
     return DTS_OK;
 }
@@ -1864,15 +2000,16 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             for (int k = 0; k < s.nout; ++k) ddst[k] = dev_frames(g->dev_out[sl][k], g->lay_out[k]);
             dts_dev_frames dq = s.quality ? dev_frames(g->dev_q[sl], g->lay_q) : dts_dev_frames{};
             e = run_device(g, g->hqs[sl], &dsrc, n, ddst, s.quality ? &dq : nullptr,
-                           s.quality ? g->dev_qraw[sl] : nullptr, st);
+                           (s.quality || g->ref) ? g->dev_qraw[sl] : nullptr, st);
             if (e) return e;
             uint8_t *op = g->pin_out[sl];
             for (int k = 0; k < s.nout; ++k) {
                 HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
                 op += (int64_t)B * g->info.out_frame_bytes[k];
             }
-            if (s.quality)
-                HIPCHK(ctx, hipMemcpyAsync(g->pin_qraw[sl], g->dev_qraw[sl], (size_t)n * sizeof(dts_qraw),
+            if (s.quality || g->ref)
+                HIPCHK(ctx, hipMemcpyAsync(g->pin_qraw[sl], g->dev_qraw[sl],
+                                           (size_t)n * (g->ref ? s.nout : 1) * sizeof(dts_qraw),
                                            hipMemcpyDeviceToHost, st));
             HIPCHK(ctx, hipEventRecord(g->done[sl], st));
             g->p_chunk_first[sl] = f0;

@@ -142,17 +142,17 @@ function planLadders(jobs, sources) {
                     throw new Error("jobs " + part[0].id + "/" + r.id + ": one graph needs one range setting");
             });
             if (rg.src || rg.dst) { spec.srcRange = rg.src; spec.dstRange = rg.dst; }
-            // per-rendition quality (codecSettings.quality): run by the scheduler after the
-            // ladder, each requesting row against its reference rendition
+            // per-rendition quality (codecSettings.quality): each requesting row against its
+            // reference rendition, made and scored inside the same graph on the GPU
+            // (dts_output_spec.quality / qref_method): no rendition crosses PCIe twice
             const q = part.map(qualityOf);
-            const quality = q.some(function (x) { return x; }) ? {
-                rows: q.map(function (x) { return x ? x.mode : 0; }),
-                refSpec: { src: spec.src, quality: 0, maxBatch: spec.maxBatch, deint: spec.deint,
-                           srcRange: spec.srcRange, dstRange: spec.dstRange,
-                           outputs: spec.outputs.map(function (o, k) {
-                               return { w: o.w, h: o.h, fmt: o.fmt, method: q[k] ? q[k].ref : o.method };
-                           }) }
-            } : null;
+            const quality = q.some(function (x) { return x; }) ? { rows: q.map(function (x) { return x ? x.mode : 0; }) } : null;
+            if (quality) spec.outputs.forEach(function (o, k) {
+                if (q[k]) {
+                    o.quality = q[k].mode;
+                    o.qrefMethod = q[k].ref;
+                }
+            });
             if (quality && tm) throw new Error("job " + part[0].id + ": quality with tonemap is not supported");
             plans.push({ sourceID: sid, framerate: part[0].framerate || 0, jobs: part, spec: spec, quality: quality });
         }

@@ -25,7 +25,9 @@
 //     ids]} (assemble.js) and reported through `onJobUpdate(job, fields)`;
 //   * `result` carries per-phase timings (readMs, gpuMs, qualityMs, writeMs) and,
 //     for rows whose codecSettings ask for it, the segment's PSNR / SSIM against
-//     the reference rendition (ladder.js qualityOf).
+//     the reference rendition (ladder.js qualityOf) with its summed record (`raw`);
+//     a job whose chunks are all done gets the whole stream's averages (Jobs row
+//     field `quality`, from the summed records: vf_psnr / vf_ssim end of stream).
 //
 // The addon's run() executes on the libuv thread pool: set UV_THREADPOOL_SIZE
 // >= the GPU count before the first async call (worker.js does).
@@ -130,11 +132,9 @@ class GpuSegmentScheduler extends EventEmitter {
         return slot.ctx;
     }
 
-    _graph(slot, plan, ref) {
-        const key = ref ? plan.key + ":ref" : plan.key;
-        if (!slot.graphs.has(key))
-            slot.graphs.set(key, this.addon.createGraph(this._ctx(slot), ref ? plan.quality.refSpec : plan.spec));
-        return slot.graphs.get(key);
+    _graph(slot, plan) {
+        if (!slot.graphs.has(plan.key)) slot.graphs.set(plan.key, this.addon.createGraph(this._ctx(slot), plan.spec));
+        return slot.graphs.get(plan.key);
     }
 
     _segmentPath(jobId, off) {
@@ -197,19 +197,19 @@ class GpuSegmentScheduler extends EventEmitter {
         const outs = plan.spec.outputs;
         const nout = plan.spec.deint ? Math.max(0, src.length - 2) : src.length;
         const o = this._allocOutputs(outs, nout);
-        if (nout) await this.addon.run(g, src, o.dst, null);
-        if (sel) o.per = o.per.map(function (fr) { return sel.map(function (j) { return fr[j]; }); });
+        // with rendition quality the graph also returns, per frame, each rendition's vf_psnr /
+        // vf_ssim against its reference rendition (made and scored on the GPU: qs[f][k])
+        let qs = nout ? await this.addon.run(g, src, o.dst, null) : null;
+        if (sel) {
+            o.per = o.per.map(function (fr) { return sel.map(function (j) { return fr[j]; }); });
+            if (qs) qs = sel.map(function (j) { return qs[j]; });
+        }
         const t2 = Date.now();
-        // per-rendition PSNR / SSIM against the reference rendition of the same source frames
         const quality = outs.map(function () { return null; });
-        if (plan.quality && nout) {
-            const ref = this._allocOutputs(plan.quality.refSpec.outputs, nout);
-            await this.addon.run(this._graph(slot, plan, true), src, ref.dst, null);
-            if (sel) ref.per = ref.per.map(function (fr) { return sel.map(function (j) { return fr[j]; }); });
+        if (plan.quality && qs && qs.length) {
             for (let k = 0; k < outs.length; ++k) {
                 if (!plan.quality.rows[k]) continue;
-                const st = await this.addon.quality(this._ctx(slot), outs[k].w, outs[k].h, outs[k].fmt, o.per[k],
-                                                    ref.per[k]);
+                const st = qs.map(function (fq) { return fq[k]; });
                 const sum = this._qsummary(ladder.rawQuality(st, outs[k].w, outs[k].h), outs[k].w, outs[k].h);
                 if (!(plan.quality.rows[k] & 1)) delete sum.psnr;
                 if (!(plan.quality.rows[k] & 2)) delete sum.ssim;

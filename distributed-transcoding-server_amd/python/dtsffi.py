@@ -37,7 +37,8 @@ E_INVAL, E_NOMEM, E_RANGE, E_UNSUPPORTED, E_BUSY, E_NODEV, E_HIP = -22, -12, -34
 
 class OutputSpec(ctypes.Structure):
     _fields_ = [("w", ctypes.c_int32), ("h", ctypes.c_int32), ("fmt", ctypes.c_int32),
-                ("method", ctypes.c_int32), ("param", ctypes.c_double * 2)]
+                ("method", ctypes.c_int32), ("param", ctypes.c_double * 2),
+                ("quality", ctypes.c_int32), ("qref_method", ctypes.c_int32)]
 
 
 class TonemapSpec(ctypes.Structure):
@@ -254,7 +255,8 @@ def graph_plan(spec):
 
 def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max_batch=0, tonemap=None,
               deint=None, src_range=0, dst_range=0):
-    """outputs: list of (w, h, fmt, method[, (p0, p1)]).  tonemap: None, or a dict
+    """outputs: list of (w, h, fmt, method[, (p0, p1)[, (quality, qref_method)]]): the last
+    turns on rendition quality (dts_output_spec.quality / qref_method).  tonemap: None, or a dict
     {mode, param, desat, peak, npl} turning on HDR10 -> SDR (dts_tonemap_spec).
     deint: None, or (mode, tff) for yadif ahead of the ladder (sources then carry one
     context frame on each side: dts_graph_spec.deint)."""
@@ -263,8 +265,10 @@ def make_spec(src_w, src_h, src_fmt, outputs, quality=Q_NONE, quality_out=0, max
     s.nout = len(outputs)
     for i, o in enumerate(outputs):
         s.out[i].w, s.out[i].h, s.out[i].fmt, s.out[i].method = o[0], o[1], o[2], o[3]
-        par = o[4] if len(o) > 4 else (PARAM_DEFAULT, PARAM_DEFAULT)
+        par = o[4] if len(o) > 4 and o[4] is not None else (PARAM_DEFAULT, PARAM_DEFAULT)
         s.out[i].param[0], s.out[i].param[1] = par
+        if len(o) > 5 and o[5] is not None:
+            s.out[i].quality, s.out[i].qref_method = o[5]
     s.quality, s.quality_out, s.max_batch = quality, quality_out, max_batch
     if tonemap is not None:
         s.hdr_to_sdr = 1
@@ -362,6 +366,13 @@ class Graph:
         src = (Frame * ns)(*[frame_struct(f) for f in frames])
         outs = [[alloc_frame(s.out[k].w, s.out[k].h, s.out[k].fmt) for k in range(s.nout)] for _ in range(n)]
         dst = (Frame * (n * s.nout))(*[frame_struct(outs[f][k]) for f in range(n) for k in range(s.nout)])
+        rq = any(s.out[k].quality for k in range(s.nout))
+        if rq:                      # rendition quality: q[f * nout + k]
+            qs = (QStat * (n * s.nout))()
+            check(lib().dts_graph_submit(self.h, src, n, dst, None, qs), "graph_submit")
+            check(lib().dts_graph_wait(self.h), "graph_wait")
+            return outs, [[qs[f * s.nout + k].as_dict() if s.out[k].quality else None for k in range(s.nout)]
+                          for f in range(n)]
         qr = (Frame * n)(*[frame_struct(q) for q in qref]) if qref is not None else None
         qs = (QStat * n)() if qref is not None else None
         check(lib().dts_graph_submit(self.h, src, n, dst, qr, qs), "graph_submit")

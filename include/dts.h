@@ -103,6 +103,14 @@ typedef struct dts_output_spec {
                            (output.c yuv2p010lX_c / yuv2p010cX_c) */
     int32_t method;     /* DTS_SCALE_*; always run as method|ACCURATE_RND|BITEXACT */
     double param[2];    /* sws param[0..1]; DTS_PARAM_DEFAULT for defaults */
+    /* Rendition quality (ABI 6): `[rendition][reference]psnr` / `ssim` of this output
+     * against a reference rendition of the same size and format that the graph makes
+     * from the same source frames with qref_method (e.g. DTS_SCALE_LANCZOS), all on the
+     * device -- the quality a CPU worker gets from a second scale branch of its
+     * filtergraph.  DTS_Q_* (0 = off); 8-bit outputs, no HDR graph, and not together
+     * with dts_graph_spec.quality (an external reference). */
+    int32_t quality;
+    int32_t qref_method;
 } dts_output_spec;
 
 typedef struct dts_graph_spec {
@@ -215,7 +223,9 @@ int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info);
 
 /* Host-memory path (the Node worker's path).  dst holds nframes*nout frames,
  * frame-major (dst[f*nout + k]); src holds nframes (+ 2 with deint: see above).
- * qref/q may be NULL when quality is off.
+ * qref/q may be NULL when quality is off.  With rendition quality (dts_output_spec
+ * quality) q, if not NULL, holds nframes*nout statistics, frame-major like dst
+ * (entries of outputs without quality are zeroed) and qref is not used.
  * The caller keeps every buffer alive until dts_graph_wait returns. */
 int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes,
                      const dts_frame *dst, const dts_frame *qref, dts_qstat *q);
@@ -224,7 +234,9 @@ int dts_graph_wait(dts_graph *g);
 /* Device-resident path: enqueue one batch on `stream` (a hipStream_t, NULL =
  * the ctx's stream).  dst[k] is the batch of output k.  When the graph has
  * quality on, qref is the reference batch for output quality_out and qraw
- * receives nframes device-side dts_qraw records (device pointer). */
+ * receives nframes device-side dts_qraw records (device pointer).  With rendition
+ * quality qref is not used and qraw receives nframes*nout records, output-major
+ * (record k*nframes + f; those of outputs without quality are left as they were). */
 int dts_graph_run_device(dts_graph *g, const dts_dev_frames *src, int nframes,
                          const dts_dev_frames *dst, const dts_dev_frames *qref,
                          dts_qraw *qraw_dev, void *stream);

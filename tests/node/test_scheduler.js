@@ -47,7 +47,17 @@ function fakeAddon(opts) {
                 setTimeout(function () {
                     if (opts.fail && opts.fail(g.ctx.dev, stats.runs)) return reject(new Error("dts run: HIP error (-1000)"));
                     dst.forEach(function (f, i) { f.data[0][0] = src[cf + Math.floor(i / g.spec.outputs.length)].data[0][0]; });
-                    resolve(null);
+                    // rendition quality: stats[f][k] (stand-in vf_psnr: odd frames differ by one luma level)
+                    const rq = g.spec.outputs.some(function (o) { return o.quality; });
+                    if (!rq) return resolve(null);
+                    stats.quality = (stats.quality || 0) + 1;
+                    resolve(Array.from({ length: src.length - 2 * cf }, function (_, fi) {
+                        return g.spec.outputs.map(function (o) {
+                            if (!o.quality) return null;
+                            const d = src[cf + fi].data[0][0] & 1;
+                            return { sse: { y: d, u: 0, v: 0 }, psnr: {}, ssim: { y: 1 - d / 2, u: 1, v: 1 }, ssimAll: 1 - d / 4 };
+                        });
+                    }));
                 }, opts.delay === undefined ? 2 : opts.delay);
             });
         },
@@ -295,9 +305,12 @@ async function testY4MJobAssembled() {
     const q21 = JSON.parse(jobs[0].quality);
     assert.strictEqual(q21.frames, 14);
     assert.strictEqual(q21.segments, 3);
-    assert.ok(q21.psnr.avg === "inf" && q21.ssim.all > 0.99, JSON.stringify(q21));   // stand-in: identical
+    // stand-in: odd source frames (7 of 14) carry luma SSE 1 over 32x18 -> mean MSE 0.5 / 576
+    assert.ok(Math.abs(q21.psnr.y - 10 * Math.log10(255 * 255 / (0.5 / 576))) < 1e-9, JSON.stringify(q21));
+    assert.ok(q21.ssim.y < 1 && q21.ssim.u === 1, JSON.stringify(q21));
     assert.strictEqual(jobs[1].quality, undefined);
     assert.ok(addon.stats.quality >= 3);
+    assert.strictEqual(addon.stats.graphs, 2);          // one graph per GPU: the references are inside it
 }
 
 async function testDeinterlaceWithRateChange() {

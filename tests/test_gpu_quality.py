@@ -155,3 +155,73 @@ def test_quality_host_entry_vs_oracle(ctx, fmt):
         return [p[0], np.ascontiguousarray(p[1][:, 0::2]), np.ascontiguousarray(p[1][:, 1::2])]
     for i in range(3):
         check_q(got[i], orc.quality_frame(w, h, planar(a[i]), planar(b[i])))
+
+
+@pytest.mark.parametrize("deint", [None, (0, 1)])
+def test_graph_rendition_quality_host_path(ctx, deint):
+    """Rendition quality (dts_output_spec.quality, ABI 6): the graph scales every rendition
+    and, for the ones that ask, a lanczos reference of the same size from the same source
+    frames, and scores them on the device -- the Node worker's per-segment quality with no
+    rendition crossing PCIe twice.  More frames than max_batch (both host slots), mixed
+    formats, one output without quality; with deint the references are made from the
+    deinterlaced frames.  Every frame: SSE exact, SSIM 1e-4 vs the oracle."""
+    sw, sh, n, batch = 384, 216, 7, 3
+    src = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 21, f) for f in range(n + (2 if deint else 0))]
+    outs = [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS)),
+            (128, 72, D.FMT_YUV420P, D.SCALE_BILINEAR),
+            (96, 54, D.FMT_YUV420P, D.SCALE_BICUBIC, None, (D.Q_PSNR, D.SCALE_BILINEAR))]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, outs, max_batch=batch, deint=deint))
+    got, qs = g.run_host(src)
+    assert len(qs) == n and all(len(row) == 3 for row in qs)
+    for f in range(n):
+        frame = src[f + 1] if deint else src[f]
+        if deint:
+            frame = orc.yadif_frame(src[f], src[f + 1], src[f + 2], sw, sh, deint[0], deint[1], 0)
+        for k, o in enumerate(outs):
+            want = orc.scale_frame(frame, sw, sh, D.FMT_YUV420P, o[0], o[1], o[2], o[3])
+            assert planes_equal(got[f][k], want), (f, k)
+            if len(o) < 6:
+                assert qs[f][k] is None
+                continue
+            ref = orc.scale_frame(frame, sw, sh, D.FMT_YUV420P, o[0], o[1], o[2], o[5][1])
+            pl = (lambda p: [p[0], np.ascontiguousarray(p[1][:, 0::2]), np.ascontiguousarray(p[1][:, 1::2])]) \
+                if o[2] == D.FMT_NV12 else (lambda p: p)
+            check_q(qs[f][k], orc.quality_frame(o[0], o[1], pl(want), pl(ref)))
+    g.close()
+
+
+def test_graph_rendition_quality_device_path(ctx):
+    """The same on the device path: qraw receives nframes x nout records, output-major."""
+    import torch
+    from bench import dev_batch, frame_bytes
+    sw, sh, n = 512, 288, 5
+    outs = [(256, 144, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS)),
+            (170, 96, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS))]
+    st = torch.cuda.current_stream().cuda_stream
+    t = torch.empty((n, frame_bytes(sw, sh, D.FMT_YUV420P)), dtype=torch.uint8, device="cuda")
+    sd, _ = dev_batch(t, sw, sh, D.FMT_YUV420P)
+    ctx.synth_device(sw, sh, D.FMT_YUV420P, 0, 33, 0, sd, n, st)
+    dts = []
+    for o in outs:
+        ot = torch.empty((n, frame_bytes(o[0], o[1], o[2])), dtype=torch.uint8, device="cuda")
+        dts.append((ot, dev_batch(ot, o[0], o[1], o[2])[0]))
+    raw = torch.zeros((len(outs) * n, 6), dtype=torch.float64, device="cuda")
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, outs, max_batch=2))
+    g.run_device(sd, n, [d for (_t, d) in dts], qraw_ptr=raw.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    import ctypes
+    host = raw.cpu().numpy()
+    for k, o in enumerate(outs):
+        recs = []
+        for f in range(n):
+            r = D.QRaw()
+            ctypes.memmove(ctypes.addressof(r), host[k * n + f].tobytes(), ctypes.sizeof(r))
+            recs.append(r)
+        got = D.qstat_finalize(o[0], o[1], recs)
+        for f in range(n):
+            frame = D.synth_host(sw, sh, D.FMT_YUV420P, 0, 33, f)
+            a = orc.scale_frame(frame, sw, sh, 0, o[0], o[1], o[2], o[3])
+            b = orc.scale_frame(frame, sw, sh, 0, o[0], o[1], o[2], D.SCALE_LANCZOS)
+            pl = lambda p: [p[0], np.ascontiguousarray(p[1][:, 0::2]), np.ascontiguousarray(p[1][:, 1::2])]
+            check_q(got[f], orc.quality_frame(o[0], o[1], pl(a), pl(b)))
+    g.close()

@@ -259,3 +259,23 @@ def test_qstat_stream_is_vf_psnr_ssim_end_of_stream():
     assert jq["ssim_all"] == pytest.approx(got["ssim_all"], abs=1e-6)
     with pytest.raises(D.DtsError):
         D.qstat_stream(w, h, raws[0], 0)
+
+
+def test_rendition_quality_spec_validation():
+    """dts_output_spec.quality: bad modes / reference methods and the combinations the
+    graph does not run (external reference quality, HDR, p010 renditions) are refused."""
+    ok = D.make_spec(256, 144, D.FMT_YUV420P, [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS))])
+    D.graph_plan(ok)
+    bad = [
+        (D.make_spec(256, 144, D.FMT_YUV420P, [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC, None, (7, D.SCALE_LANCZOS))]), D.E_INVAL),
+        (D.make_spec(256, 144, D.FMT_YUV420P, [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, 12345))]), D.E_UNSUPPORTED),
+        (D.make_spec(256, 144, D.FMT_YUV420P, [(128, 72, D.FMT_P010LE, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS))]), D.E_UNSUPPORTED),
+        (D.make_spec(256, 144, D.FMT_YUV420P, [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS))],
+                     quality=D.Q_BOTH), D.E_UNSUPPORTED),
+        (D.make_spec(256, 144, D.FMT_P010LE, [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC, None, (D.Q_BOTH, D.SCALE_LANCZOS))],
+                     tonemap={"mode": D.TM_HABLE}), D.E_UNSUPPORTED),
+    ]
+    for spec, code in bad:
+        with pytest.raises(D.DtsError) as e:
+            D.graph_plan(spec)
+        assert e.value.code == code
