@@ -320,6 +320,54 @@ def gather_records(frames, checksum, wall, world, dev):
     return sum(r[0] for r in records), float(wall_t.item()), records
 
 
+def run_e2e(args, wl, ctx, sptr):
+    """The host-memory path end to end (dts_graph_submit / dts_graph_wait, the Node worker's
+    path): source frames in pageable host memory -> pinned rings (host threads) -> H2D ->
+    ladder -> D2H -> the caller's output frames, two slots / streams in flight.  PCIe and
+    host copies included: the rate a worker sees, not the kernel's."""
+    import numpy as np
+    sw, sh, sfmt = wl["src"]
+    chunk = args.e2e_batch
+    g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, wl["outs"], max_batch=chunk, tonemap=wl["tonemap"]))
+    nsrc = args.e2e_frames                   # distinct host source frames, cycled
+    srcs = [D.synth_host(sw, sh, sfmt, 0, 0x5EED, i) for i in range(nsrc)]
+    per = args.e2e_submit                    # frames per submit (several chunks: both slots busy)
+    outs = [[D.alloc_frame(w, h, fmt) for (w, h, fmt, _m) in wl["outs"]] for _ in range(per)]
+    nout = len(wl["outs"])
+    dst = (D.Frame * (per * nout))(*[D.frame_struct(outs[f][k]) for f in range(per) for k in range(nout)])
+    src_arr = [(D.Frame * per)(*[D.frame_struct(srcs[(i * per + f) % nsrc]) for f in range(per)])
+               for i in range(max(1, nsrc // per))]
+    L = D.lib()
+
+    def step(i):
+        D.check(L.dts_graph_submit(g.h, src_arr[i % len(src_arr)], per, dst, None, None), "submit")
+        D.check(L.dts_graph_wait(g.h), "wait")
+    for i in range(args.warmup):
+        step(i)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    wall = time.perf_counter() - t0
+    fps = args.steps * per / wall
+    io = g.info.src_frame_bytes + sum(g.info.out_frame_bytes[k] for k in range(nout))
+    ok = True
+    if not args.no_verify:                   # the last submit's first frame vs the oracle
+        want, _ = oracle_outputs(wl, srcs[((args.warmup + args.steps - 1) % len(src_arr)) * per % nsrc])
+        for k in range(nout):
+            for a, b in zip(outs[0][k], want[k]):
+                if a is not None and not np.array_equal(a, b):
+                    ok = False
+    g.close()
+    return {"metric": f"frames/s end to end (host memory -> GPU -> host memory), {args.workload}",
+            "value": round(fps, 1), "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": f"{nsrc} synthetic host frames, cycled",
+            "config": {"workload": wl["desc"], "frames_per_submit": per, "chunk_frames": chunk,
+                       "host_threads": os.environ.get("DTS_HOST_THREADS", "hardware threads (<= 16)")},
+            "pcie_bytes_per_frame": io, "host_io_GBps": round(fps * io / 1e9, 2),
+            "verified_vs_oracle": ok if not args.no_verify else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -331,6 +379,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="time the host-memory path (dts_graph_submit / wait) instead of device-resident batches")
+    ap.add_argument("--e2e-batch", type=int, default=32, help="--e2e: frames per device chunk (max_batch)")
+    ap.add_argument("--e2e-submit", type=int, default=128, help="--e2e: frames per submit")
+    ap.add_argument("--e2e-frames", type=int, default=128, help="--e2e: distinct host source frames")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS),
                     help="cfg2 = the BASELINE metric's workload (default line); cfg3 / cfg4 = extra lines")
     args = ap.parse_args()
@@ -358,6 +411,12 @@ def main():
     runtimes = hip_runtimes()
     if len(runtimes) != 1:
         print(f"WARNING: {len(runtimes)} HIP runtimes mapped: {runtimes}", file=sys.stderr)
+    if args.e2e:
+        line = run_e2e(args, wl, ctx, sptr)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        ctx.close()
+        return
     B, R = args.batch, max(args.ring, 2 * args.batch)
     if "ring" in wl and args.ring == ap.get_default("ring"):
         R = max(wl["ring"], B)                 # cfg5: one segment resident (7.4 GB), re-read every step

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "dts_internal.h"
@@ -125,14 +126,17 @@ void plane_geom(int w, int h, int fmt, int64_t rowb[3], int64_t rows[3])
 struct DevLayout {
     int64_t pitch[3] = {0, 0, 0}, off[3] = {0, 0, 0}, rows[3] = {0, 0, 0}, rowb[3] = {0, 0, 0};
     int64_t fstride = 0;
-    void init(int w, int h, int fmt)
+    // tight: pitches rounded to 16 B and planes to 256 B (the host path's batches: the
+    // pinned rings hold the same image, so a batch crosses PCIe as one contiguous copy
+    // with almost no padding); else pitches + 16 rounded to 256 B, planes to 4 KiB
+    void init(int w, int h, int fmt, bool tight = false)
     {
         plane_geom(w, h, fmt, rowb, rows);
         int64_t o = 0;
         for (int p = 0; p < 3; ++p) {
-            pitch[p] = rowb[p] ? align_up(rowb[p] + 16, 256) : 0;
+            pitch[p] = rowb[p] ? (tight ? align_up(rowb[p], 16) : align_up(rowb[p] + 16, 256)) : 0;
             off[p] = o;
-            o += align_up(pitch[p] * rows[p], 4096);
+            o += align_up(pitch[p] * rows[p], tight ? 256 : 4096);
         }
         fstride = o;
     }
@@ -1091,8 +1095,8 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
             dts_graph_destroy(g);
             return e;
         }
-        g->lay_src.init(s.src_w, s.src_h, s.src_fmt);
-        for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt);
+        g->lay_src.init(s.src_w, s.src_h, s.src_fmt, true);
+        for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt, true);
         if (s.hdr_to_sdr) {
             g->hdr = true;
             g->tm = tonemap_params(s.tonemap);
@@ -1118,7 +1122,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
                 return e;
             }
         }
-        if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt);
+        if (s.quality) g->lay_q.init(s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, true);
         // rendition quality: the reference renditions are a graph of their own over the same
         // source (deinterlaced first when the graph deinterlaces: it runs on our yadif output)
         dts_graph_spec rs = s;
@@ -1862,10 +1866,11 @@ static int alloc_host_path(dts_graph *g)
     const dts_graph_spec &s = g->spec;
     const int B = g->batch;
     const int cf = s.deint ? 2 : 0;                      // deint: one context frame each side
-    g->pin_in_bytes = (int64_t)(B + cf) * g->info.src_frame_bytes;
-    if (s.quality) g->pin_in_bytes += (int64_t)B * g->info.out_frame_bytes[s.quality_out];
+    // the pinned rings hold batches in the device layout (lay_*): one DMA per batch and plane set
+    g->pin_in_bytes = (int64_t)(B + cf) * g->lay_src.fstride;
+    if (s.quality) g->pin_in_bytes += (int64_t)B * g->lay_q.fstride;
     g->pin_out_bytes = 0;
-    for (int k = 0; k < s.nout; ++k) g->pin_out_bytes += (int64_t)B * g->info.out_frame_bytes[k];
+    for (int k = 0; k < s.nout; ++k) g->pin_out_bytes += (int64_t)B * g->lay_out[k].fstride;
     for (int sl = 0; sl < 2; ++sl) {
         HIPCHK(ctx, hipMalloc(&g->dev_src[sl], (size_t)(B + cf) * g->lay_src.fstride));
         for (int k = 0; k < s.nout; ++k) HIPCHK(ctx, hipMalloc(&g->dev_out[sl][k], (size_t)B * g->lay_out[k].fstride));
@@ -1887,46 +1892,62 @@ static int alloc_host_path(dts_graph *g)
     return DTS_OK;
 }
 
-// copy rows of a caller frame into/out of a packed pinned image
-static void pack_frame(uint8_t *dst, const dts_frame &f, int w, int h, int fmt)
+// Host threads that pack / unpack the caller's frames (DTS_HOST_THREADS, default: the
+// hardware threads, at most 16).  The host path's bound is this copy, not PCIe: one
+// thread moves ~8 GB/s, a 4K cfg2 frame is 17.5 MB in + out of the pinned rings.
+static int host_threads()
 {
-    int64_t rowb[3], rows[3];
-    plane_geom(w, h, fmt, rowb, rows);
-    for (int p = 0; p < 3; ++p)
-        for (int64_t y = 0; y < rows[p]; ++y) {
-            std::memcpy(dst, static_cast<const uint8_t *>(f.data[p]) + y * f.pitch[p], (size_t)rowb[p]);
-            dst += rowb[p];
-        }
+    static const int n = [] {
+        const char *e = std::getenv("DTS_HOST_THREADS");
+        int v = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::min(std::max(v, 1), 16);
+    }();
+    return n;
 }
 
-static void unpack_frame(const uint8_t *src, const dts_frame &f, int w, int h, int fmt)
+// f(i) for i in [0, n) over up to host_threads() threads (the caller's among them)
+extern "C++" template <class F>
+static void parallel_for(int n, F f)
 {
-    int64_t rowb[3], rows[3];
-    plane_geom(w, h, fmt, rowb, rows);
-    for (int p = 0; p < 3; ++p)
-        for (int64_t y = 0; y < rows[p]; ++y) {
-            std::memcpy(static_cast<uint8_t *>(f.data[p]) + y * f.pitch[p], src, (size_t)rowb[p]);
-            src += rowb[p];
-        }
+    const int nt = std::min(n, host_threads());
+    if (nt <= 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    for (int t = 1; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int i = t; i < n; i += nt) f(i);
+        });
+    for (int i = 0; i < n; i += nt) f(i);
+    for (auto &x : th) x.join();
 }
 
-// packed pinned image <-> device batch with our pitch: one 2D copy per plane per frame
+// rows of a caller frame into / out of one frame of a pinned batch in layout `lay`
+static void pack_frame(uint8_t *dst, const dts_frame &f, const DevLayout &lay)
+{
+    for (int p = 0; p < 3; ++p)
+        for (int64_t y = 0; y < lay.rows[p]; ++y)
+            std::memcpy(dst + lay.off[p] + y * lay.pitch[p], static_cast<const uint8_t *>(f.data[p]) + y * f.pitch[p],
+                        (size_t)lay.rowb[p]);
+}
+
+static void unpack_frame(const uint8_t *src, const dts_frame &f, const DevLayout &lay)
+{
+    for (int p = 0; p < 3; ++p)
+        for (int64_t y = 0; y < lay.rows[p]; ++y)
+            std::memcpy(static_cast<uint8_t *>(f.data[p]) + y * f.pitch[p], src + lay.off[p] + y * lay.pitch[p],
+                        (size_t)lay.rowb[p]);
+}
+
+// a pinned batch <-> the device batch: the same image, one contiguous copy
 static hipError_t copy_frames(uint8_t *dev, const DevLayout &lay, uint8_t *host, int n, bool h2d, hipStream_t st)
 {
-    for (int f = 0; f < n; ++f)
-        for (int p = 0; p < 3; ++p) {
-            if (!lay.rowb[p]) continue;
-            uint8_t *d = dev + (int64_t)f * lay.fstride + lay.off[p];
-            hipError_t e = h2d ? hipMemcpy2DAsync(d, lay.pitch[p], host, lay.rowb[p], lay.rowb[p], lay.rows[p],
-                                                  hipMemcpyHostToDevice, st)
-                               : hipMemcpy2DAsync(host, lay.rowb[p], d, lay.pitch[p], lay.rowb[p], lay.rows[p],
-                                                  hipMemcpyDeviceToHost, st);
-            if (e != hipSuccess) return e;
-            host += lay.rowb[p] * lay.rows[p];
-        }
-    return hipSuccess;
+    const size_t nb = (size_t)n * (size_t)lay.fstride;
+    return h2d ? hipMemcpyAsync(dev, host, nb, hipMemcpyHostToDevice, st)
+               : hipMemcpyAsync(host, dev, nb, hipMemcpyDeviceToHost, st);
 }
-
 
 static int finish_slot(dts_graph *g, int sl)
 {
@@ -1935,13 +1956,13 @@ static int finish_slot(dts_graph *g, int sl)
     const dts_graph_spec &s = g->spec;
     HIPCHK(ctx, hipEventSynchronize(g->done[sl]));
     const int f0 = g->p_chunk_first[sl], n = g->p_chunk_n[sl];
-    const uint8_t *hp = g->pin_out[sl];          // per output: a region of `batch` packed frames
-    for (int k = 0; k < s.nout; ++k) {
-        for (int f = 0; f < n; ++f)
-            unpack_frame(hp + (int64_t)f * g->info.out_frame_bytes[k], g->p_dst[(int64_t)(f0 + f) * s.nout + k],
-                         s.out[k].w, s.out[k].h, s.out[k].fmt);
-        hp += (int64_t)g->batch * g->info.out_frame_bytes[k];
-    }
+    const uint8_t *hp0 = g->pin_out[sl];         // per output: a region of `batch` packed frames
+    parallel_for(n * s.nout, [&](int i) {
+        const int f = i / s.nout, k = i % s.nout;
+        const uint8_t *hp = hp0;
+        for (int kk = 0; kk < k; ++kk) hp += (int64_t)g->batch * g->lay_out[kk].fstride;
+        unpack_frame(hp + (int64_t)f * g->lay_out[k].fstride, g->p_dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
+    });
     if (s.quality && g->p_q) {
         const dts_output_spec &o = s.out[s.quality_out];
         dts_qstat_finalize(o.w, o.h, g->pin_qraw[sl], n, g->p_q + f0);
@@ -1984,15 +2005,15 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             hipStream_t st = ctx->stream[sl];
             uint8_t *hp = g->pin_in[sl];
             const int cf = s.deint ? 2 : 0;              // deint: src[f0 .. f0 + n + 1] (context frames)
-            for (int f = 0; f < n + cf; ++f) {
-                pack_frame(hp + (int64_t)f * g->info.src_frame_bytes, src[f0 + f], s.src_w, s.src_h, s.src_fmt);
-            }
+            parallel_for(n + cf, [&](int f) {
+                pack_frame(hp + (int64_t)f * g->lay_src.fstride, src[f0 + f], g->lay_src);
+            });
             HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n + cf, true, st));
-            uint8_t *qhp = hp + (int64_t)(B + cf) * g->info.src_frame_bytes;
+            uint8_t *qhp = hp + (int64_t)(B + cf) * g->lay_src.fstride;
             if (s.quality) {
-                const dts_output_spec &o = s.out[s.quality_out];
-                for (int f = 0; f < n; ++f)
-                    pack_frame(qhp + (int64_t)f * g->info.out_frame_bytes[s.quality_out], qref[f0 + f], o.w, o.h, o.fmt);
+                parallel_for(n, [&](int f) {
+                    pack_frame(qhp + (int64_t)f * g->lay_q.fstride, qref[f0 + f], g->lay_q);
+                });
                 HIPCHK(ctx, copy_frames(g->dev_q[sl], g->lay_q, qhp, n, true, st));
             }
             dts_dev_frames dsrc = dev_frames(g->dev_src[sl], g->lay_src);
@@ -2005,7 +2026,7 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             uint8_t *op = g->pin_out[sl];
             for (int k = 0; k < s.nout; ++k) {
                 HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
-                op += (int64_t)B * g->info.out_frame_bytes[k];
+                op += (int64_t)B * g->lay_out[k].fstride;
             }
             if (s.quality || g->ref)
                 HIPCHK(ctx, hipMemcpyAsync(g->pin_qraw[sl], g->dev_qraw[sl],

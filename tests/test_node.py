@@ -158,9 +158,9 @@ def test_worker_gpu_y4m_quality_assembled(tmp_path):
     frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 11, i) for i in range(n)]
     src = tmp_path / "src.y4m"
     _write_y4m(src, frames, sw, sh)
-    jobs = [{"id": 31, "sourceID": 2, "width": 192, "height": 108, "framerate": 60,
+    jobs = [{"id": 31, "sourceID": 2, "width": 192, "height": 108, "framerate": 60, "chunks": 3,
              "codecSettings": json.dumps({"quality": "both"})},
-            {"id": 32, "sourceID": 2, "width": 128, "height": 72, "framerate": 60,
+            {"id": 32, "sourceID": 2, "width": 128, "height": 72, "framerate": 60, "chunks": 3,
              "codecSettings": json.dumps({"scale": "lanczos", "format": "yuv420p"})}]
     chunks = [{"id": k * 3 + off + 1, "mainJob": j["id"], "chunkOffset": off, "status": None}
               for k, j in enumerate(jobs) for off in range(3)]
@@ -173,6 +173,7 @@ def test_worker_gpu_y4m_quality_assembled(tmp_path):
     assert r.returncode == 0, r.stderr
     res = json.loads(r.stdout)
     spec = {31: (192, 108, D.FMT_NV12, D.SCALE_BICUBIC), 32: (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS)}
+    job_recs = []
     for c in res["chunks"]:
         assert c["status"] == "done"
         rec = json.loads(c["result"])
@@ -188,6 +189,7 @@ def test_worker_gpu_y4m_quality_assembled(tmp_path):
             if c["mainJob"] == 31:
                 ref = orc.scale_frame(frames[i], sw, sh, D.FMT_YUV420P, w, h, fmt, D.SCALE_LANCZOS)
                 recs.append(orc.quality_frame(w, h, _planar(want, fmt), _planar(ref, fmt)))
+        job_recs += recs
         if c["mainJob"] == 31:
             q = rec["quality"]
             mse_y = sum(x["mse"][0] for x in recs) / len(recs)
@@ -200,10 +202,24 @@ def test_worker_gpu_y4m_quality_assembled(tmp_path):
         a = json.loads(j["assembledData"])
         files = [json.loads(c["result"])["file"] for c in sorted(res["chunks"], key=lambda c: c["chunkOffset"])
                  if c["mainJob"] == j["id"]]
-        whole = b"".join(open(f, "rb").read() for f in files)
+        # one Y4M stream: the first segment whole, the later ones without their header line
+        parts = [open(f, "rb").read() for f in files]
+        whole = parts[0] + b"".join(p[p.index(b"\n") + 1:] for p in parts[1:])
         assert a["size"] == len(whole) and len(a["chunk"]) == -(-len(whole) // 1048576)
         blocks = b"".join((out / "blocks" / cid).read_bytes() for cid in a["chunk"])
         assert blocks == whole
+        (out / f"whole{j['id']}.y4m").write_bytes(blocks)
+        w, h, got = _read_y4m(out / f"whole{j['id']}.y4m")
+        assert len(got) == n
+    # the job's stream averages (Jobs row `quality`): vf_psnr's mean-MSE PSNR, vf_ssim's mean SSIM
+    q = json.loads(next(j for j in res["jobs"] if j["id"] == 31)["quality"])
+    assert q["frames"] == n and q["segments"] == 3
+    mse = [sum(x["mse"][c] for x in job_recs) / n for c in range(3)]
+    area = [192 * 108, 96 * 54, 96 * 54]
+    mse_avg = sum(m * a for m, a in zip(mse, area)) / sum(area)
+    assert q["psnr"]["avg"] == pytest.approx(10 * np.log10(255 * 255 / mse_avg), rel=1e-9)
+    assert q["ssim"]["all"] == pytest.approx(sum(x["ssim_all"] for x in job_recs) / n, abs=1e-4)
+    assert "quality" not in next(j for j in res["jobs"] if j["id"] == 32)
 
 
 @pytest.mark.gpu

@@ -7,3 +7,9 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_ladder.py tests/test_gpu_co
 echo "tests rc=$rc"; tail -5 gpurun_out/t_v7.log
 [ $rc -ne 0 ] && exit $rc
 ./tools/ab7.sh new:: hs256::DTS_L7_HSPLIT=256 nobal::DTS_L7_BAL=0 old::DTS_L7_HSPLIT=256,DTS_L7_BAL=0 new2::
+for t in 1 16; do
+  DTS_HOST_THREADS=$t timeout -k 10 300 python -u bench.py --e2e --steps 6 --warmup 2 > gpurun_out/e2e_t$t.log 2>&1; rc=$?
+  echo "== e2e threads $t rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/e2e_t$t.log) $(grep -o '"host_io_GBps": [0-9.]*' gpurun_out/e2e_t$t.log) $(grep -o '"verified_vs_oracle": [a-z]*' gpurun_out/e2e_t$t.log)"
+  [ $rc -ge 124 ] && exit $rc
+done
+exit 0
