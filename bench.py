@@ -75,6 +75,11 @@ WORKLOADS = {
              "desc": "cfg5: 2-hour 4K60 ABR ladder as 600-frame segments sharded over GPUs (weak scaling): "
                      "1080p/720p/854x480 nv12 bicubic + per-rung vf_psnr/vf_ssim vs lanczos reference "
                      "renditions; per-segment quality records all-gathered over RCCL"},
+    # not a BASELINE config: cfg2's ladder from an nv12 source (hardware decoders' output
+    # format; k_ladder7 de-interleaves the chroma in its A operand reads)
+    "cfg2nv12": {"src": (SRC_W, SRC_H, D.FMT_NV12), "outs": LADDER, "tonemap": None, "quality": False,
+                 "batch": 512,
+                 "desc": "cfg2 from nv12: 4K60 8-bit nv12 -> 1080p/720p/854x480 nv12 ABR ladder, bicubic"},
     # not a BASELINE config: the vf_yadif kernel on a 4K sequence
     "yadif": {"src": (SRC_W, SRC_H, D.FMT_YUV420P), "outs": [(SRC_W, SRC_H, D.FMT_YUV420P, 0)], "tonemap": None,
               "quality": False, "yadif": 0, "batch": 64,

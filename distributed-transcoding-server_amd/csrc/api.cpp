@@ -471,7 +471,7 @@ int validate_spec(const dts_graph_spec &s)
     }
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
     if ((s.range & ~0x11) != 0) return DTS_E_INVAL;              // DTS_RANGE_* in bits 0 and 4
-    if ((s.range & 1) != ((s.range >> 4) & 1) && (s.hdr_to_sdr || s.src_fmt != DTS_FMT_YUV420P))
+    if ((s.range & 1) != ((s.range >> 4) & 1) && (s.hdr_to_sdr || s.src_fmt == DTS_FMT_P010LE))
         return DTS_E_UNSUPPORTED;                                // range conversion: k_ladder7 sources only
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
     for (int k = 0; k < s.nout; ++k) {                  // rendition quality (ABI 6)
@@ -608,8 +608,10 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
     gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    gp.v7 = gp.v6 && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), l7_stager(),
-                                                  gp.p7);
+    // k_ladder7 takes planar and nv12 sources (k_ladder6 planar only: the fallback for planar
+    // frames that are not 16-byte aligned; v5 for the rest)
+    gp.v7 = v6_enabled() && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
+                                                        l7_stager(), gp.p7);
     return true;
 }
 
@@ -1412,7 +1414,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
             HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
-                                       g->hsplit7, st));
+                                       g->hsplit7, s.src_fmt == DTS_FMT_NV12, st));
             continue;
         }
         bool aligned6 = g->v6 && planes_aligned6(pp.src);

@@ -337,6 +337,8 @@ struct Group7 {                     // one workgroup's strip of one frame
     int32_t ngran, srcH;
     int32_t scr;                    // LDS offset of the per-wave store exchange (1 KB per wave)
     int32_t xown;                   // the next strip's X0 (plane width for the last): diagnostics only
+    int32_t il;                     // 1: chroma staged from one interleaved plane (nv12 source: U V
+                                    //    byte pairs, 2 npc pieces per granule), else U and V planes
 };
 
 struct Ladder7Params {
@@ -350,7 +352,7 @@ struct Ladder7Params {
 };
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          hipStream_t s);
+                          bool interleaved, hipStream_t s);
 void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
 
 // ---------------------------------------------------------------------------

@@ -57,6 +57,9 @@
 #ifndef DTS_L7_PAIR
 #define DTS_L7_PAIR (kL7Batch == 2)  // 1: stage 2 granules per batch (one barrier per 2 granules); plan with DTS_L7_PB=2
 #endif
+#ifndef DTS_L7_DMAPOS
+#define DTS_L7_DMAPOS 0     // where a wave issues the next batch's pieces (walk7 issue())
+#endif
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
 #endif
@@ -126,21 +129,25 @@ __device__ __forceinline__ void group_barrier7()
 struct Stage7 {
     uint64_t sb[2];                 // plane bases of this frame (chroma: U, V)
     uint32_t sp[2];                 // plane pitches
-    int np, npc, npieces, w, nw, srcH1, ngran, stage_bytes, nown;
+    int np, npc, ppp, npieces, w, nw, srcH1, ngran, stage_bytes, nown;
     uint32_t lcol;                  // this lane's byte in a piece row: X0 + 16 chunk
     int dr;                         // this lane's row in a piece
     int ops, e[NS7 - 1];
 
-    __device__ __forceinline__ void init(const Group7 &G, const DevPlanes &S, int f, int wave, int waves, int lane)
+    // il: nv12 chroma (the group stages one interleaved plane, 2 bytes per sample column,
+    // 2 npc pieces per granule); a compile-time false for planar sources
+    __device__ __forceinline__ void init(const Group7 &G, const DevPlanes &S, int f, int wave, int waves, int lane,
+                                         bool il)
     {
-        np = G.kind ? 2 : 1;
+        np = G.kind && !il ? 2 : 1;
         for (int p = 0; p < 2; ++p) {
-            sb[p] = (G.kind ? S.data[1 + p] : S.data[0]) + (uint64_t)f * (uint64_t)S.fstride;
-            sp[p] = (uint32_t)(G.kind ? S.pitch[1 + p] : S.pitch[0]);
+            sb[p] = (G.kind ? S.data[1 + (il ? 0 : p)] : S.data[0]) + (uint64_t)f * (uint64_t)S.fstride;
+            sp[p] = (uint32_t)(G.kind ? S.pitch[1 + (il ? 0 : p)] : S.pitch[0]);
         }
         npc = G.npc;
-        npieces = np * npc;
-        nown = min(npc, (G.xown - G.X0 + 63) >> 6);
+        ppp = il ? 2 * npc : npc;
+        npieces = np * ppp;
+        nown = min(ppp, ((G.xown - G.X0) * (il ? 2 : 1) + 63) >> 6);
         // the waves beyond the group's units (if any) stage every piece; else all deal them
         const int stagers = waves - G.nwaves;
         w = stagers > 0 ? (wave >= G.nwaves ? wave - G.nwaves : npieces) : wave;
@@ -149,7 +156,7 @@ struct Stage7 {
         ngran = G.ngran;
         stage_bytes = PB7 * npieces * 1024;
         dr = lane >> 2;
-        lcol = (uint32_t)G.X0 + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
+        lcol = (uint32_t)(il ? 2 * G.X0 : G.X0) + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
         ops = 0;
     }
     // this wave's pieces of batch b (granules PB7 b ..) into stage st (nothing past the plane)
@@ -164,7 +171,7 @@ struct Stage7 {
         const uint32_t row = (uint32_t)min(kL6Gran * q + dr, srcH1);
         uint8_t *dst = lds + at;
         for (int k = w; k < npieces; k += nw) {
-            const int p = k >= npc ? 1 : 0, i = k - p * npc;
+            const int p = k >= ppp ? 1 : 0, i = k - p * ppp;
             if ((DTS_L7_ABLATE & 4) && i >= nown) continue;
             const uint64_t src = (p ? sb[1] : sb[0]) + (uint64_t)(row * (p ? sp[1] : sp[0])) + lcol + 64u * (uint32_t)i;
             __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)src,
@@ -308,6 +315,7 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
 }
 
 // a wave with no unit: stage its pieces, keep the group's barrier count
+template <bool IL>
 __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
@@ -315,7 +323,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
     __builtin_amdgcn_s_setprio(DTS_L7_STAGER_PRIO);     // diagnostic: the staging wave issues first
 #endif
     Stage7 Z;
-    Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63);
+    Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63, IL && G.kind);
 #pragma unroll
     for (int i = 0; i < NS7 - 1; ++i) {
         Z.pieces(lds7, i, i);
@@ -346,7 +354,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
 // exactly (128 (...) is a multiple of 128): the lo MFMAs run first from the bias, one
 // shift, and the hi MFMAs accumulate onto it -- y comes out of the matrix core and the
 // epilogue is the saturating pack (FFMIN(y, 32767), y >= -32768 for 8-bit sources).
-template <int VAR, bool RC, int HS>
+template <int VAR, bool RC, int HS, bool IL>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -355,7 +363,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
     const int lane = (int)threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     Stage7 Z;
-    Z.init(G, S, f, wave, waves, lane);
+    Z.init(G, S, f, wave, waves, lane, W::NP == 2 && IL);
     // output planes: luma plane 0; nv12 chroma plane 1; yuv420p chroma planes 1 and 2
     uint64_t ob[2];
     uint32_t op[2];
@@ -384,6 +392,22 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     constexpr bool B64 = l7_b64(VAR);
     constexpr int NH = B64 ? 2 : 1;
     uint32_t aoff[T][HKB][NH];
+    // nv12 chroma: the U and V operands of column tile c come from the same 32 interleaved
+    // bytes per lane (two 16-B chunks: byte 2 (x0 + 64 kb + 16 g) of the strip)
+    constexpr bool il = W::NP == 2 && IL;        // (IL: the graph's source is nv12)
+    uint32_t ioff[CT][HKB][2];
+    if (il) {
+        const uint32_t sw = 2u * (uint32_t)((m >> 3) & 1);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int kb = 0; kb < HKB; ++kb)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t cc = (2u * ((uint32_t)U.xo[c] + 64u * (uint32_t)kb + 16u * (uint32_t)g)) / 16u + h;
+                    ioff[c][kb][h] = (cc >> 2) * 1024u + 16u * (4u * (uint32_t)m + ((cc & 3u) ^ sw));
+                }
+    }
     {
         const uint32_t sw = 2u * (uint32_t)((m >> 3) & 1);
 #pragma unroll
@@ -394,7 +418,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 for (int h = 0; h < NH; ++h) {
                     const uint32_t b = (uint32_t)U.xo[t % CT] + 64u * (uint32_t)kb + 16u * (uint32_t)g + 8u * (uint32_t)h;
                     const uint32_t c = b / 16u;
-                    aoff[t][kb][h] = (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u +
+                    aoff[t][kb][h] = il ? 0u : (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u +
                                      16u * (4u * (uint32_t)m + ((c & 3u) ^ sw)) + (B64 ? (b & 8u) : 0u);
                 }
     }
@@ -510,7 +534,24 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 L7_STAMP(1);
             }
             v4i a[T][HKB];
-            {
+            if (il) {
+                // nv12 chroma: even bytes are U, odd bytes V (yuv2nv12 order, input.c nv12ToUV_c)
+                const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
+#pragma unroll
+                for (int c = 0; c < CT; ++c)
+#pragma unroll
+                    for (int kb = 0; kb < HKB; ++kb) {
+                        const v4i x = *reinterpret_cast<const v4i *>(st + ioff[c][kb][0]);
+                        const v4i y = *reinterpret_cast<const v4i *>(st + ioff[c][kb][1]);
+                        const uint32_t w8[8] = {(uint32_t)x.x, (uint32_t)x.y, (uint32_t)x.z, (uint32_t)x.w,
+                                                (uint32_t)y.x, (uint32_t)y.y, (uint32_t)y.z, (uint32_t)y.w};
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4) {
+                            a[c][kb][q4] = (int)__builtin_amdgcn_perm(w8[2 * q4 + 1], w8[2 * q4], 0x06040200u);
+                            a[CT + c][kb][q4] = (int)__builtin_amdgcn_perm(w8[2 * q4 + 1], w8[2 * q4], 0x07050301u);
+                        }
+                    }
+            } else {
                 const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
 #pragma unroll
                 for (int t = 0; t < T; ++t)
@@ -526,14 +567,27 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                     }
             }
+            // the next batch's pieces: right after the A reads (DTS_L7_DMAPOS 0), or after the
+            // deferred row blocks (1: the 16 waves of a CU then do not all queue their DMAs
+            // on the memory pipe at the moment they leave the barrier)
+#if DTS_L7_DMAPOS == 0
             if (s % PB7 == 0) {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
                 frags(PB7 * bn + PB7 - 1);
                 Z.pieces(lds7, bn, sn);
                 Z.shift();
             }
+#endif
             L7_STAMP(2);
             if (DTS_L7_DEFER) vfire(q - 1);
+#if DTS_L7_DMAPOS == 1
+            if (s % PB7 == 0) {
+                const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
+                frags(PB7 * bn + PB7 - 1);
+                Z.pieces(lds7, bn, sn);
+                Z.shift();
+            }
+#endif
             L7_STAMP(4);
             {
                 v4i ah[T], al[T];
@@ -624,7 +678,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 
 // RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
 // the common kernel keeps its register allocation)
-template <bool RC, int HS>
+template <bool RC, int HS, bool IL>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -641,25 +695,25 @@ void k_ladder7(Ladder7Params P)
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
     if (wave >= G.nwaves) {
-        idle7(G, S, f, wave, waves);
+        idle7<IL>(G, S, f, wave, waves);
         return;
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
-    walk7<DTS_L7_ONLYVAR, RC, HS>(P, G, U, S, f, wave, waves);
+    walk7<DTS_L7_ONLYVAR, RC, HS, IL>(P, G, U, S, f, wave, waves);
     return;
 #endif
     switch (U.variant) {
-    case 0: walk7<0, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7, RC, HS>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8, RC, HS>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12, RC, HS>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
     }
 }
 
@@ -686,18 +740,26 @@ void ladder7_compiled(int *stages, int *batch)
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          hipStream_t s)
+                          bool interleaved, hipStream_t s)
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
+    if (interleaved) {                   // nv12 sources: 128-split taps only (plan7_graph)
+        if (hsplit != 128) return hipErrorInvalidValue;
+        if (range_conv)
+            hipLaunchKernelGGL((k_ladder7<true, 128, true>), g, b, lds_bytes, s, p);
+        else
+            hipLaunchKernelGGL((k_ladder7<false, 128, true>), g, b, lds_bytes, s, p);
+        return hipGetLastError();
+    }
     if (range_conv && hsplit == 128)
-        hipLaunchKernelGGL((k_ladder7<true, 128>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<true, 128, false>), g, b, lds_bytes, s, p);
     else if (range_conv)
-        hipLaunchKernelGGL((k_ladder7<true, 256>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<true, 256, false>), g, b, lds_bytes, s, p);
     else if (hsplit == 128)
-        hipLaunchKernelGGL((k_ladder7<false, 128>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<false, 128, false>), g, b, lds_bytes, s, p);
     else
-        hipLaunchKernelGGL((k_ladder7<false, 256>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<false, 256, false>), g, b, lds_bytes, s, p);
     return hipGetLastError();
 }
 

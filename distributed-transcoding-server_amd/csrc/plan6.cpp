@@ -157,7 +157,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
     std::vector<Pending> todo;
     for (int kind = 0; kind < 2; ++kind) {
         const Plan5In &in = kinds[kind];
-        if (in.nv12_chroma) return false;                  // planar sources only (nv12: k_ladder5)
+        if (in.nv12_chroma && align) return false;         // k_ladder6: planar sources only (nv12: k_ladder5 / 7)
         if ((int)in.rungs.size() < 1 || (int)in.rungs.size() > DTS_MAX_OUTPUTS) return false;
         for (int k = 0; k < (int)in.rungs.size(); ++k) {
             const Plan5Rung &R = in.rungs[k];
@@ -305,6 +305,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             out.hsplit = 256;
             if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
         }
+    if (out.hsplit != 128 && kinds[1].nv12_chroma) return false;   // nv12: k_ladder7<.., 128, true> only
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
     for (int kind = 0; kind < 2; ++kind) {
@@ -471,6 +472,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                 out.units.push_back(v);
             }
             g.scr = lds;
+            g.il = kinds[kind].nv12_chroma ? 1 : 0;
             out.groups.push_back(g);
             u += cnt;
         }

@@ -122,8 +122,10 @@ class GpuSegmentScheduler extends EventEmitter {
         this.onUpdate = opts.onUpdate || function () {};
         this.onJobUpdate = opts.onJobUpdate || function () {};
         this.readers = {};
-        this.slots = this.gpus.map(function (dev) {
-            return { dev: dev, ctx: null, graphs: new Map(), busy: false, done: 0, failed: 0, ms: 0 };
+        // a slot = one libdts context on one device; several slots may share a device
+        // (gpus: [0, 0] drives GPU 0 from two libuv threads)
+        this.slots = this.gpus.map(function (dev, i) {
+            return { id: i, dev: dev, ctx: null, graphs: new Map(), busy: false, done: 0, failed: 0, ms: 0 };
         });
     }
 
@@ -237,7 +239,7 @@ class GpuSegmentScheduler extends EventEmitter {
             o.per[k].forEach(function (f) {
                 f.data.forEach(function (b) { if (b) { h.update(b); bytes += b.length; } });
             });
-            const r = { frames: o.per[k].length, bytes: bytes, sha1: h.digest("hex"), gpu: slot.dev, ms: t4 - t0,
+            const r = { frames: o.per[k].length, bytes: bytes, sha1: h.digest("hex"), gpu: slot.dev, slot: slot.id, ms: t4 - t0,
                         readMs: t1 - t0, gpuMs: t2 - t1, qualityMs: t3 - t2, writeMs: t4 - t3,
                         width: outs[k].w, height: outs[k].h, fmt: outs[k].fmt };
             if (quality[k]) r.quality = quality[k];
@@ -365,7 +367,7 @@ class GpuSegmentScheduler extends EventEmitter {
                 const rows = byOff.get(off);
                 // a rendition without a row at this offset still runs (it shares the launch); only
                 // rows that exist are updated
-                queue.push({ plan: plan, chunkOffset: off, rows: rows, tries: 0, lastGpu: -1 });
+                queue.push({ plan: plan, chunkOffset: off, rows: rows, tries: 0, lastGpu: -1, lastSlot: -1 });
             });
         });
         // segments in stream order across ladders (a pipe source is read once, front to back)
@@ -389,8 +391,11 @@ class GpuSegmentScheduler extends EventEmitter {
             if (!total) return finish();
             function pull(slot) {
                 if (slot.busy) return;
-                // prefer a task that did not just fail on this GPU
+                // prefer a task that did not just fail on this GPU, then one that did not fail
+                // on this slot; a task that failed here waits for another slot unless this is
+                // the only one
                 let i = queue.findIndex(function (t) { return t.lastGpu !== slot.dev; });
+                if (i < 0) i = queue.findIndex(function (t) { return t.lastSlot !== slot.id; });
                 if (i < 0 && queue.length && self.slots.length === 1) i = 0;
                 if (i < 0) return;
                 const task = queue.splice(i, 1)[0];
@@ -415,6 +420,7 @@ class GpuSegmentScheduler extends EventEmitter {
                 }, function (err) {
                     task.tries++;
                     task.lastGpu = slot.dev;
+                    task.lastSlot = slot.id;
                     slot.failed++;
                     if (task.tries > self.maxRetries) {
                         counted = true;
@@ -453,7 +459,7 @@ class GpuSegmentScheduler extends EventEmitter {
 
     _summary(total) {
         return { segments: total, gpus: this.slots.map(function (s) {
-            return { device: s.dev, segments: s.done, failures: s.failed, ms: s.ms };
+            return { device: s.dev, slot: s.id, segments: s.done, failures: s.failed, ms: s.ms };
         }) };
     }
 }

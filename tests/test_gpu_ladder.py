@@ -251,13 +251,15 @@ def test_v7_geometries(ctx, ladder_kernel, sw, sh, outs, method):
 
 @pytest.mark.parametrize("src_range,dst_range", [(0, 1), (1, 0)])
 @pytest.mark.parametrize("method", [BIC, LAN, BIL])
-def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method):
+@pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12])
+def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method, sfmt):
     """`scale=in_range:out_range`: swscale.c's lum/chrRange{To,From}Jpeg_c on the
     15-bit H output, in k_ladder7's H epilogue, bit-exact vs the oracle (random and
-    full-swing frames, nv12 and yuv420p renditions).  Other kernels refuse it."""
+    full-swing frames, nv12 and yuv420p renditions; planar and nv12 sources -- nv12
+    chroma de-interleaved in the A reads).  Other kernels refuse it."""
     sw, sh = 384, 216
     outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_YUV420P, method), (384, 216, D.FMT_NV12, method)]
-    spec = D.make_spec(sw, sh, D.FMT_YUV420P, outs, src_range=src_range, dst_range=dst_range)
+    spec = D.make_spec(sw, sh, sfmt, outs, src_range=src_range, dst_range=dst_range)
     if ladder_kernel != "v7":
         with pytest.raises(D.DtsError):
             D.Graph(ctx, spec)
@@ -266,11 +268,14 @@ def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method):
     swing = [np.where((np.arange(sw)[None, :] // 3) % 2 == 0, 255, 0).astype(np.uint8).repeat(sh, 0),
              np.full((sh // 2, sw // 2), 255, np.uint8), np.zeros((sh // 2, sw // 2), np.uint8)]
     frames = [random_frame(sw, sh, D.FMT_YUV420P, rng), D.synth_host(sw, sh, D.FMT_YUV420P, 0, 3, 1), swing]
+    if sfmt == D.FMT_NV12:                    # the same pictures, chroma interleaved
+        frames = [[f[0], np.ascontiguousarray(np.stack([f[1], f[2]], -1).reshape(f[1].shape[0], -1)), None]
+                  for f in frames]
     g = D.Graph(ctx, spec)
     got, _ = g.run_host(frames)
     for f, src in enumerate(frames):
         for k, (w, h, fmt, m) in enumerate(outs):
-            want = orc.scale_frame(src, sw, sh, D.FMT_YUV420P, w, h, fmt, m, src_range=src_range, dst_range=dst_range)
+            want = orc.scale_frame(src, sw, sh, sfmt, w, h, fmt, m, src_range=src_range, dst_range=dst_range)
             assert planes_equal(got[f][k], want), f"frame {f} out {k}: {first_diff(got[f][k], want)}"
     g.close()
 

@@ -127,7 +127,8 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
     """8-bit sources with 8-bit outputs (cfg1, cfg2, cfg4 and upscales) plan the whole
     graph onto the v5 (matrix-core) ladder: every strip's H entries fit the waves and
     its LDS fits one workgroup per CU.  p010 sources and HDR graphs stay on v4 / v3.
-    Planar sources go on to v7 (ladder_v5 == 3), nv12 sources stay on v5."""
+    Without DTS_LADDER both go on to v7 (ladder_v5 == 3): nv12 chroma is de-interleaved
+    in k_ladder7's A operand reads."""
     monkeypatch.setenv("DTS_LADDER", "5")
     for sw, sh, outs in [(3840, 2160, LADDER4K), (7680, 4320, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)]),
                          (1920, 1080, [(1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]),
@@ -137,7 +138,7 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
         assert info.lds_bytes <= 160 * 1024 and min(info.v5_strips) >= 1
     assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, LADDER4K)).ladder_v5 == 0
     monkeypatch.delenv("DTS_LADDER", raising=False)
-    want = 3 if fmt == D.FMT_YUV420P else 1
+    want = 3
     assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == want
     assert D.graph_plan(D.make_spec(7680, 4320, fmt, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)])).ladder_v5 == want
     monkeypatch.setenv("DTS_LADDER", "4")
@@ -186,13 +187,14 @@ def test_plan_v7_groups(monkeypatch):
 
 def test_plan_range_conversion(monkeypatch):
     """Range conversion (dts_graph_spec.range) plans onto k_ladder7 only: 8-bit planar
-    sources with plane widths multiples of 16; nv12 / p010 sources, HDR graphs, other
+    and nv12 sources with plane widths multiples of 16; p010 sources, HDR graphs, other
     widths and DTS_LADDER=6 are refused with DTS_E_UNSUPPORTED, bad bits with INVAL."""
     monkeypatch.delenv("DTS_LADDER", raising=False)
     outs = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]
     for sr, dr in [(0, 1), (1, 0), (1, 1)]:
-        assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=sr, dst_range=dr)).ladder_v5 == 3
-    for fmt in (D.FMT_NV12, D.FMT_P010LE):
+        for fmt in (D.FMT_YUV420P, D.FMT_NV12):
+            assert D.graph_plan(D.make_spec(3840, 2160, fmt, outs, src_range=sr, dst_range=dr)).ladder_v5 == 3
+    for fmt in (D.FMT_P010LE,):
         with pytest.raises(D.DtsError):
             D.graph_plan(D.make_spec(3840, 2160, fmt, outs, src_range=1))
     with pytest.raises(D.DtsError):

@@ -258,3 +258,40 @@ def test_worker_gpu_yadif_fps(tmp_path):
             de = orc.yadif_frame(frames[max(i - 1, 0)], frames[i], frames[min(i + 1, n - 1)], sw, sh, 0, 1, 0)
             want = orc.scale_frame(de, sw, sh, D.FMT_YUV420P, 128, 72, D.FMT_YUV420P, D.SCALE_BICUBIC)
             assert planes_equal(g, want), (c["chunkOffset"], j)
+
+
+@pytest.mark.gpu
+def test_worker_gpu_two_slots_one_device_with_a_failure(tmp_path):
+    """gpus [0, 0]: two libdts contexts on one MI355X driven from two libuv threads
+    (dts.h: distinct contexts may run concurrently), one segment's source failing once
+    and retried on the other slot.  Every row comes back done, every frame bit-exact,
+    both slots did work, and the job-level quality matches the oracle's mean MSE."""
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "gpu_multislot.js"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().split("\n")[-1])
+    assert res["failed"] == 1 and res["retries"] == 1
+    slots = {g["slot"]: g for g in res["summary"]["gpus"]}
+    assert set(slots) == {0, 1} and all(g["device"] == 0 for g in slots.values())
+    assert sum(g["failures"] for g in slots.values()) == 1
+    assert all(g["segments"] > 0 for g in slots.values())
+    outs = {81: (192, 108, D.FMT_NV12, D.SCALE_BICUBIC), 82: (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS)}
+    recs = []
+    for c in res["chunks"]:
+        assert c["status"] == "done" and c["assignedTo"] == 9, c
+        rec = json.loads(c["result"])
+        w, h, fmt, m = outs[c["mainJob"]]
+        for i in range(4):
+            src = D.synth_host(384, 216, D.FMT_YUV420P, 0, 0x5EED, c["chunkOffset"] * 4 + i)
+            want = orc.scale_frame(src, 384, 216, D.FMT_YUV420P, w, h, fmt, m)
+            got = (tmp_path / f"{c['mainJob']}_{c['chunkOffset']}_{i}.raw").read_bytes()
+            assert got == b"".join(np.ascontiguousarray(p).tobytes() for p in want if p is not None)
+            if c["mainJob"] == 81:
+                ref = orc.scale_frame(src, 384, 216, D.FMT_YUV420P, w, h, fmt, D.SCALE_LANCZOS)
+                recs.append(orc.quality_frame(w, h, _planar(want, fmt), _planar(ref, fmt)))
+    q = json.loads(next(j for j in res["jobs"] if j["id"] == 81)["quality"])
+    area = [192 * 108, 96 * 54, 96 * 54]
+    mse = [sum(x["mse"][c] for x in recs) / len(recs) for c in range(3)]
+    mse_avg = sum(m_ * a for m_, a in zip(mse, area)) / sum(area)
+    assert q["frames"] == 24 and q["psnr"]["avg"] == pytest.approx(10 * np.log10(255 * 255 / mse_avg), rel=1e-9)
+    assert q["ssim"]["all"] == pytest.approx(sum(x["ssim_all"] for x in recs) / len(recs), abs=1e-4)
