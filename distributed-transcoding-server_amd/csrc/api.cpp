@@ -231,7 +231,12 @@ struct dts_graph {
     bool hdr = false;
     DevLayout lay_mid[DTS_MAX_OUTPUTS];
     uint8_t *hdr_mid[2][DTS_MAX_OUTPUTS] = {};
-    hipEvent_t hdr_ev[2] = {nullptr, nullptr};
+    hipEvent_t hdr_ev[2] = {nullptr, nullptr};   // k_tonemap done reading intermediate sl
+    hipEvent_t hdr_mid_ev[2] = {nullptr, nullptr};   // the ladder wrote intermediate sl
+    hipEvent_t hdr_go = nullptr, hdr_end = nullptr;
+    hipStream_t hdr_tm = nullptr;         // k_tonemap's own stream: the ladder of chunk i + 1 runs
+                                          // beside the tonemap of chunk i (nullptr: one stream)
+    int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk
     unsigned hdr_next = 0;
     TonemapParams tm{};
     float *dev_tm_lut = nullptr;          // the transfer-curve tables of tm (TonemapParams::lut)
@@ -1102,14 +1107,32 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         if (s.hdr_to_sdr) {
             g->hdr = true;
             g->tm = tonemap_params(s.tonemap);
-            for (int sl = 0; sl < 2 && !e; ++sl) {
-                for (int k = 0; k < s.nout && !e; ++k) {
-                    g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
-                    if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->batch * g->lay_mid[k].fstride) != hipSuccess)
-                        e = DTS_E_NOMEM;
-                }
-                if (!e && hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
+            // Chunks whose two p010 intermediates fit the Infinity Cache (~96 MB of the 256):
+            // the tonemap reads what the ladder wrote from the cache, not from HBM
+            // (DTS_HDR_CHUNK: frames per chunk, A/B; DTS_HDR_STREAMS=1: no second stream)
+            int64_t mid_bytes = 0;
+            for (int k = 0; k < s.nout; ++k) {
+                g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
+                mid_bytes += g->lay_mid[k].fstride;
             }
+            const char *hc = std::getenv("DTS_HDR_CHUNK");
+            g->hdr_chunk = hc ? std::atoi(hc) : (int)((int64_t)48 << 20) / (int)std::max<int64_t>(mid_bytes, 1);
+            g->hdr_chunk = std::min(std::max(g->hdr_chunk, 4), g->batch);
+            const char *hs = std::getenv("DTS_HDR_STREAMS");
+            const bool two = !(hs && hs[0] == '1');
+            for (int sl = 0; sl < 2 && !e; ++sl) {
+                for (int k = 0; k < s.nout && !e; ++k)
+                    if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->hdr_chunk * g->lay_mid[k].fstride) != hipSuccess)
+                        e = DTS_E_NOMEM;
+                if (!e && (hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess ||
+                           hipEventCreateWithFlags(&g->hdr_mid_ev[sl], hipEventDisableTiming) != hipSuccess))
+                    e = DTS_E_HIP;
+            }
+            if (!e && two &&
+                (hipStreamCreateWithFlags(&g->hdr_tm, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&g->hdr_go, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&g->hdr_end, hipEventDisableTiming) != hipSuccess))
+                e = DTS_E_HIP;
             if (!e) {
                 const std::vector<float> luts = tonemap_luts(s.tonemap);
                 const size_t nb = luts.size() * sizeof(float);
@@ -1184,7 +1207,14 @@ void dts_graph_destroy(dts_graph *g)
     if (!g) return;
     hipSetDevice(g->ctx->device);
     free_host_path(g);
+    if (g->hdr_tm) {
+        hipStreamSynchronize(g->hdr_tm);
+        hipStreamDestroy(g->hdr_tm);
+    }
+    if (g->hdr_go) hipEventDestroy(g->hdr_go);
+    if (g->hdr_end) hipEventDestroy(g->hdr_end);
     for (int sl = 0; sl < 2; ++sl) {
+        if (g->hdr_mid_ev[sl]) hipEventDestroy(g->hdr_mid_ev[sl]);
         if (g->hdr_ev[sl]) {
             hipEventSynchronize(g->hdr_ev[sl]);
             hipEventDestroy(g->hdr_ev[sl]);
@@ -1482,16 +1512,24 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     return DTS_OK;
 }
 
-// HDR10 -> SDR: per chunk of `batch` frames, the bit-exact ladder into the p010
-// intermediates, then k_tonemap from each intermediate into the caller's output.
+// HDR10 -> SDR: per chunk of hdr_chunk frames, the bit-exact ladder into a p010
+// intermediate (two, alternating), then k_tonemap from it into the caller's output.  The
+// tonemaps run on the graph's second stream: the ladder of chunk i + 1 overlaps the
+// tonemap of chunk i, and a chunk's intermediate is still in the Infinity Cache when the
+// tonemap reads it.  The caller's stream waits for the last tonemap before returning.
 static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, int nframes, hipStream_t st)
 {
     const dts_graph_spec &s = g->spec;
     dts_ctx *ctx = g->ctx;
-    for (int f0 = 0; f0 < nframes; f0 += g->batch) {
-        const int n = std::min(g->batch, nframes - f0);
+    hipStream_t tm = g->hdr_tm ? g->hdr_tm : st;
+    if (g->hdr_tm) {                                  // the outputs' earlier users on st come first
+        HIPCHK(ctx, hipEventRecord(g->hdr_go, st));
+        HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_go, 0));
+    }
+    for (int f0 = 0; f0 < nframes; f0 += g->hdr_chunk) {
+        const int n = std::min(g->hdr_chunk, nframes - f0);
         const int sl = (int)(g->hdr_next++ & 1u);
-        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_ev[sl], 0));   // the buffer's previous user is done
+        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_ev[sl], 0));   // the buffer's previous tonemap is done
         DevPlanes sc = src, mid[DTS_MAX_OUTPUTS];
         int mid_fmt[DTS_MAX_OUTPUTS];
         for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)(f0 * src.fstride);
@@ -1501,6 +1539,10 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
         }
         int e = enqueue_ladder(g, sc, mid, mid_fmt, n, st);
         if (e) return e;
+        if (g->hdr_tm) {
+            HIPCHK(ctx, hipEventRecord(g->hdr_mid_ev[sl], st));
+            HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_mid_ev[sl], 0));
+        }
         for (int k = 0; k < s.nout; ++k) {
             TonemapParams tp = g->tm;
             tp.src = mid[k];
@@ -1510,9 +1552,13 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
             tp.w = s.out[k].w;
             tp.h = s.out[k].h;
             tp.nframes = n;
-            HIPCHK(ctx, launch_tonemap(tp, st));
+            HIPCHK(ctx, launch_tonemap(tp, tm));
         }
-        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], st));
+        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], tm));
+    }
+    if (g->hdr_tm) {
+        HIPCHK(ctx, hipEventRecord(g->hdr_end, tm));
+        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_end, 0));
     }
     return DTS_OK;
 }

@@ -744,12 +744,15 @@ hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_b
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
-    if (interleaved) {                   // nv12 sources: 128-split taps only (plan7_graph)
-        if (hsplit != 128) return hipErrorInvalidValue;
-        if (range_conv)
+    if (interleaved) {                   // nv12 sources
+        if (range_conv && hsplit == 128)
             hipLaunchKernelGGL((k_ladder7<true, 128, true>), g, b, lds_bytes, s, p);
-        else
+        else if (range_conv)
+            hipLaunchKernelGGL((k_ladder7<true, 256, true>), g, b, lds_bytes, s, p);
+        else if (hsplit == 128)
             hipLaunchKernelGGL((k_ladder7<false, 128, true>), g, b, lds_bytes, s, p);
+        else
+            hipLaunchKernelGGL((k_ladder7<false, 256, true>), g, b, lds_bytes, s, p);
         return hipGetLastError();
     }
     if (range_conv && hsplit == 128)

@@ -305,7 +305,6 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             out.hsplit = 256;
             if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
         }
-    if (out.hsplit != 128 && kinds[1].nv12_chroma) return false;   // nv12: k_ladder7<.., 128, true> only
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
     for (int kind = 0; kind < 2; ++kind) {
