@@ -1107,19 +1107,22 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         if (s.hdr_to_sdr) {
             g->hdr = true;
             g->tm = tonemap_params(s.tonemap);
-            // Chunks whose two p010 intermediates fit the Infinity Cache (~96 MB of the 256):
-            // the tonemap reads what the ladder wrote from the cache, not from HBM
-            // (DTS_HDR_CHUNK: frames per chunk, A/B; DTS_HDR_STREAMS=1: no second stream)
+            // Chunks of `batch` frames on one stream.  Diagnostic A/B knobs (r03, cfg3: no
+            // gain): DTS_HDR_CHUNK = frames per chunk (7 frames keep both intermediates in the
+            // Infinity Cache: 25.2k fps, 16: 32.5k, 256: 44.8k -- k_ladder4's persistent grid
+            // pays a tail per launch), DTS_HDR_STREAMS=2 tonemaps on a second stream beside
+            // the next chunk's ladder (44.4k vs 44.8k)
             int64_t mid_bytes = 0;
             for (int k = 0; k < s.nout; ++k) {
                 g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
                 mid_bytes += g->lay_mid[k].fstride;
             }
             const char *hc = std::getenv("DTS_HDR_CHUNK");
-            g->hdr_chunk = hc ? std::atoi(hc) : (int)((int64_t)48 << 20) / (int)std::max<int64_t>(mid_bytes, 1);
-            g->hdr_chunk = std::min(std::max(g->hdr_chunk, 4), g->batch);
+            g->hdr_chunk = hc ? std::atoi(hc) : g->batch;
+            g->hdr_chunk = std::min(std::max(g->hdr_chunk, 1), g->batch);
+            (void)mid_bytes;
             const char *hs = std::getenv("DTS_HDR_STREAMS");
-            const bool two = !(hs && hs[0] == '1');
+            const bool two = hs && hs[0] == '2';
             for (int sl = 0; sl < 2 && !e; ++sl) {
                 for (int k = 0; k < s.nout && !e; ++k)
                     if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->hdr_chunk * g->lay_mid[k].fstride) != hipSuccess)

@@ -101,16 +101,34 @@ static_assert(NS7 >= 2 && NS7 <= 4, "stages (plan7_graph: V fragment slots for P
 
 // s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0: waiting for fewer outstanding
 // operations than were issued after the batch is never too short
+#ifndef DTS_L7_WAITTREE
+#define DTS_L7_WAITTREE 0   // 1: the run-time vmcnt wait as a 4-level binary tree of branches
+#endif
 __device__ __forceinline__ void vm_wait_rt7(int n)
 {
+#define DTS_W7I(k) __builtin_amdgcn_s_waitcnt((k) | (7 << 4) | (15 << 8))
+#if DTS_L7_WAITTREE
+    const int v = min(max(n, 0), 15);
+#define DTS_W7P(k) if (v == (k)) DTS_W7I(k); else DTS_W7I((k) + 1)
+    if (v < 8) {
+        if (v < 4) { if (v < 2) { DTS_W7P(0); } else { DTS_W7P(2); } }
+        else { if (v < 6) { DTS_W7P(4); } else { DTS_W7P(6); } }
+    } else {
+        if (v < 12) { if (v < 10) { DTS_W7P(8); } else { DTS_W7P(10); } }
+        else { if (v < 14) { DTS_W7P(12); } else { DTS_W7P(14); } }
+    }
+#undef DTS_W7P
+#else
 #define DTS_W7(k) \
-    case k: __builtin_amdgcn_s_waitcnt((k) | (7 << 4) | (15 << 8)); break;
+    case k: DTS_W7I(k); break;
     switch (min(max(n, 0), 15)) {
         DTS_W7(0) DTS_W7(1) DTS_W7(2) DTS_W7(3) DTS_W7(4) DTS_W7(5) DTS_W7(6) DTS_W7(7)
         DTS_W7(8) DTS_W7(9) DTS_W7(10) DTS_W7(11) DTS_W7(12) DTS_W7(13) DTS_W7(14)
     default: DTS_W7(15)
     }
 #undef DTS_W7
+#endif
+#undef DTS_W7I
 }
 
 // every wave's pieces of the granule have landed (each wave waited for its own) and
@@ -521,6 +539,11 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     static_assert(8 % R == 0, "ring periods divide the unroll");
     const int ngran = G.ngran;
     int sq = 0;
+#ifdef DTS_L7_HEAVY_PRIO
+    // diagnostic: the heaviest walks (4-tile one-K-block: the 1080p luma / chroma units) set
+    // the group's pace at every barrier; give them the issue port first
+    if (CT * HKB * W::NP >= 4) __builtin_amdgcn_s_setprio(DTS_L7_HEAVY_PRIO);
+#endif
     L7_STAMP_INIT;
     for (int q0 = 0; q0 < ngran; q0 += 8) {
 #pragma unroll
