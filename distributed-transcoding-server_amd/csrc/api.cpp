@@ -620,6 +620,29 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     return true;
 }
 
+// p010 sources on k_ladder7 (its 16-bit walks: the H sums from the samples' raw bytes,
+// p010 / 8-bit dithered renditions); k_ladder4 stays planned for frames whose planes are
+// not 16-byte aligned
+bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
+{
+    if (!v6_enabled() || !v7_enabled() || s.src_fmt != DTS_FMT_P010LE) return false;
+    if ((s.range & 1) != ((s.range >> 4) & 1)) return false;
+    Plan5In ins[2];
+    for (int kind = 0; kind < 2; ++kind) {
+        Plan5In &in = ins[kind];
+        in.chroma = kind == 1;
+        in.nv12_chroma = kind == 1;
+        in.p10 = true;
+        in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
+        in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
+        for (int k = 0; k < s.nout; ++k) {
+            const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
+            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
+        }
+    }
+    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, l7_stager(), gp.p7);
+}
+
 bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
 {
     const bool p010 = s.src_fmt == DTS_FMT_P010LE, nv12 = s.src_fmt == DTS_FMT_NV12;
@@ -648,6 +671,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
         if (e) return e;
     }
     const bool v5 = plan5_graph(s, gp);
+    if (!v5) gp.v7 = plan7_p010(s, gp);
     // range conversion runs in k_ladder7's H epilogue only
     if ((s.range & 1) != ((s.range >> 4) & 1) && !gp.v7) return DTS_E_UNSUPPORTED;
     int ndmax_need = 1;
@@ -1447,7 +1471,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
             HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
-                                       g->hsplit7, s.src_fmt == DTS_FMT_NV12, st));
+                                       g->hsplit7, g->src_kind, st));
             continue;
         }
         bool aligned6 = g->v6 && planes_aligned6(pp.src);

@@ -253,8 +253,10 @@ constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, 
 // variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns
 // per H tile, VKB K blocks of 64 source rows (4 VKB granules held) per V row block, and
 // CT 16-column tiles per plane: 4 MFMA tiles when HKB = VKB = 1, else 2
-// (k_ladder7 only: + 8 = "narrow", the one-K-block variants with half the tiles)
-constexpr int kL7Variants = 16;
+// (k_ladder7 only: + 8 = "narrow", the one-K-block variants with half the tiles;
+// + 16 = 16-bit (p010) source samples: one column tile per plane, the H K blocks of 64
+// samples read as two MFMA K blocks of raw little-endian bytes)
+constexpr int kL7Variants = 32;
 constexpr int l6_variant(int np, int hkb, int vkb, bool narrow = false)
 {
     return (np == 2 ? 4 : 0) + 2 * (hkb - 1) + (vkb - 1) + (narrow && hkb == 1 && vkb == 1 ? 8 : 0);
@@ -262,7 +264,7 @@ constexpr int l6_variant(int np, int hkb, int vkb, bool narrow = false)
 constexpr int l6_np(int v) { return (v & 4) ? 2 : 1; }
 constexpr int l6_hkb(int v) { return ((v >> 1) & 1) + 1; }
 constexpr int l6_vkb(int v) { return (v & 1) + 1; }
-constexpr int l6_ct(int v) { return ((v & 3) == 0 && !(v & 8) ? 4 : 2) / l6_np(v); }
+constexpr int l6_ct(int v) { return (v & 16) ? 1 : ((v & 3) == 0 && !(v & 8) ? 4 : 2) / l6_np(v); }
 // k_ladder7 variants whose A operands are two ds_read_b64 (K windows on 8-column
 // boundaries allowed): one H K block, two V K blocks (luma 2 tiles, chroma 1 tile per plane)
 constexpr bool l7_b64(int v) { return v == 1 || v == 5; }
@@ -337,8 +339,9 @@ struct Group7 {                     // one workgroup's strip of one frame
     int32_t ngran, srcH;
     int32_t scr;                    // LDS offset of the per-wave store exchange (1 KB per wave)
     int32_t xown;                   // the next strip's X0 (plane width for the last): diagnostics only
-    int32_t il;                     // 1: chroma staged from one interleaved plane (nv12 source: U V
-                                    //    byte pairs, 2 npc pieces per granule), else U and V planes
+    int32_t bpc;                    // staged bytes per source column: 1 (8-bit planes; chroma: U and V
+                                    // planes), 2 (nv12 chroma: U V byte pairs; p010 luma), 4 (p010
+                                    // chroma: U V 16-bit pairs); bpc npc pieces per plane and granule
 };
 
 struct Ladder7Params {
@@ -352,7 +355,7 @@ struct Ladder7Params {
 };
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          bool interleaved, hipStream_t s);
+                          int src_kind, hipStream_t s);   // src_kind: SrcKind
 void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
 
 // ---------------------------------------------------------------------------

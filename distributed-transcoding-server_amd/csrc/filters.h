@@ -86,6 +86,7 @@ struct Plan5Rung {
 struct Plan5In {
     bool chroma = false;             // U + V planes (else luma)
     bool nv12_chroma = false;        // chroma staged from an interleaved nv12 plane
+    bool p10 = false;                // 16-bit (p010) source samples (k_ladder7 only)
     int srcW = 0, srcH = 0;          // plane size
     int lds_cap = 160 * 1024;        // bytes per workgroup (one per CU)
     int range_conv = 0;              // 0 none, 1 *RangeToJpeg, 2 *RangeFromJpeg (k_ladder7 only)

@@ -152,20 +152,22 @@ struct Stage7 {
     int dr;                         // this lane's row in a piece
     int ops, e[NS7 - 1];
 
-    // il: nv12 chroma (the group stages one interleaved plane, 2 bytes per sample column,
-    // 2 npc pieces per granule); a compile-time false for planar sources
+    // bpc: staged bytes per source column (Group7::bpc; a compile-time 1 for planar 8-bit
+    // sources): the chroma of planar sources is two planes, every other staging one plane of
+    // bpc npc pieces per granule
     __device__ __forceinline__ void init(const Group7 &G, const DevPlanes &S, int f, int wave, int waves, int lane,
-                                         bool il)
+                                         int bpc)
     {
+        const bool il = bpc > 1;
         np = G.kind && !il ? 2 : 1;
         for (int p = 0; p < 2; ++p) {
             sb[p] = (G.kind ? S.data[1 + (il ? 0 : p)] : S.data[0]) + (uint64_t)f * (uint64_t)S.fstride;
             sp[p] = (uint32_t)(G.kind ? S.pitch[1 + (il ? 0 : p)] : S.pitch[0]);
         }
         npc = G.npc;
-        ppp = il ? 2 * npc : npc;
+        ppp = bpc * npc;
         npieces = np * ppp;
-        nown = min(ppp, ((G.xown - G.X0) * (il ? 2 : 1) + 63) >> 6);
+        nown = min(ppp, ((G.xown - G.X0) * bpc + 63) >> 6);
         // the waves beyond the group's units (if any) stage every piece; else all deal them
         const int stagers = waves - G.nwaves;
         w = stagers > 0 ? (wave >= G.nwaves ? wave - G.nwaves : npieces) : wave;
@@ -174,7 +176,7 @@ struct Stage7 {
         ngran = G.ngran;
         stage_bytes = PB7 * npieces * 1024;
         dr = lane >> 2;
-        lcol = (uint32_t)(il ? 2 * G.X0 : G.X0) + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
+        lcol = (uint32_t)(bpc * G.X0) + 16u * (uint32_t)((lane & 3) ^ (2 * ((dr >> 3) & 1)));
         ops = 0;
     }
     // this wave's pieces of batch b (granules PB7 b ..) into stage st (nothing past the plane)
@@ -232,6 +234,10 @@ __device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR
             *reinterpret_cast<u32x4 *>(scr + 16 * d) = (u32x4){o[0], o[1], o[2], o[3]};
             const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * dr);
             x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w;
+        } else if (W::CT == 1) {                           // (p010 sources) 16-byte tile rows
+            *reinterpret_cast<uint32_t *>(scr + 4 * d) = w[0];
+            x[0] = *reinterpret_cast<const uint32_t *>(scr + 4 * dr);
+            x[1] = x[2] = x[3] = 0;
         } else {
             uint32_t o[2];
             transpose2(w[0], w[1 % W::T], o);
@@ -288,6 +294,35 @@ __device__ __forceinline__ void xchg7(const UT &U, const uint32_t (&w)[Walk6<VAR
     __builtin_amdgcn_wave_barrier();
 }
 
+// p010 renditions (yuv2p010lX / yuv2p010cX, LE 16-bit): lane (m, g) holds the 16-bit values
+// of columns 4 g .. 4 g + 3 of one column tile (v[p][0..1]: plane p, two per dword); luma
+// rows are 32 bytes per tile (8 per lane), chroma rows U V interleaved, 64 bytes (16 per
+// lane); the same exchange as xchg7 gives four consecutive lanes one row's segment
+template <int VAR, class UT>
+__device__ __forceinline__ void xchg7p(const UT &U, const uint32_t (&v)[Walk6<VAR>::T][2], uint8_t *scr, int m,
+                                       int g, int lane, uint32_t (&x)[4])
+{
+    using W = Walk6<VAR>;
+    static_assert(W::CT == 1, "p010 renditions: one column tile per plane");
+    __builtin_amdgcn_wave_barrier();
+    const int d = 4 * m + (g ^ ((m >> 2) & 3));
+    const int r4 = lane >> 2, dr = 4 * r4 + ((lane & 3) ^ ((r4 >> 2) & 3));
+    if (W::NP == 1) {
+        *reinterpret_cast<u32x2 *>(scr + 8 * d) = (u32x2){v[0][0], v[0][1]};
+        const u32x2 r = *reinterpret_cast<const u32x2 *>(scr + 8 * dr);
+        x[0] = r.x; x[1] = r.y; x[2] = x[3] = 0;
+    } else {
+        const uint32_t u0 = v[0][0], u1 = v[0][1], v0 = v[W::T - 1][0], v1 = v[W::T - 1][1];
+        *reinterpret_cast<u32x4 *>(scr + 16 * d) =
+            (u32x4){__builtin_amdgcn_perm(v0, u0, 0x05040100u), __builtin_amdgcn_perm(v0, u0, 0x07060302u),
+                    __builtin_amdgcn_perm(v1, u1, 0x05040100u), __builtin_amdgcn_perm(v1, u1, 0x07060302u)};
+        const u32x4 r = *reinterpret_cast<const u32x4 *>(scr + 16 * dr);
+        x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w;
+    }
+    (void)U;
+    __builtin_amdgcn_wave_barrier();
+}
+
 // the stores of row block j from x (xchg7); returns the store instructions issued (edge
 // units' byte stores are not counted, which only makes the next source wait longer)
 template <int VAR, class UT>
@@ -297,10 +332,23 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
     using W = Walk6<VAR>;
     const int y = 16 * j + (lane >> 2), q4 = lane & 3;
     if (y < U.dstH) {
-        if (W::NP == 1) {
+        if (W::CT == 1 && U.fmt == DTS_FMT_P010LE) {        // p010 renditions (xchg7p)
+            if (W::NP == 1) {
+                const uint32_t o[2] = {x[0], x[1]};
+                const int at = 2 * U.col0 + 8 * q4;
+                put_row6<8>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
+            } else {
+                const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
+                const int at = 4 * U.col0 + 16 * q4;
+                put_row6<16>(ob[0] + (uint64_t)y * op[0], at, 4 * U.dstW - at, o);
+            }
+        } else if (W::NP == 1) {
             if (W::CT == 4) {
                 const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
                 put_row6<16>(ob[0] + (uint64_t)y * op[0], U.col0 + 16 * q4, U.dstW - U.col0 - 16 * q4, o);
+            } else if (W::CT == 1) {
+                const uint32_t o[1] = {x[0]};
+                put_row6<4>(ob[0] + (uint64_t)y * op[0], U.col0 + 4 * q4, U.dstW - U.col0 - 4 * q4, o);
             } else {
                 const uint32_t o[2] = {x[0], x[1]};
                 put_row6<8>(ob[0] + (uint64_t)y * op[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
@@ -332,8 +380,92 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
     return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
 }
 
+// V of one row block over the whole ring, as vcalc (ladder_mfma.h): 65536 hh + 256 (hl +
+// lh) + ll as three chained accumulations; the bias enters as b1 << 16 (the chain's start)
+// and b2 << 8 (added with the first shift), so a per-lane bias (the ordered dither of
+// p010 sources: DIT) costs nothing.  8-bit: av_clip_uint8(v >> 19) of 4 columns, packed.
+template <int VAR, bool DIT>
+__device__ __forceinline__ void vcalc7(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                       const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                       const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
+                                       const v4i (&vdit)[2], uint32_t (&w)[Walk6<VAR>::T])
+{
+    using W = Walk6<VAR>;
+    static_assert(kL5VBias == 12 << 16, "flat-dither V bias folded into the hh chain");
+    const int b1 = DIT ? 0 : 12;                  // (128 + 64) << 12, or the dither's 128 << 12 in b2
+    v4i acc[W::T];
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] = (v4i){b1, b1, b1, b1};
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vh[kb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] = DIT ? (acc[t] << 8) + vdit[t / W::CT] : acc[t] << 8;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vl[kb], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vh[kb], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] <<= 8;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vl[kb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) {
+        const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][0], acc[t][1], 19);
+        const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][2], acc[t][3], 19);
+        w[t] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+    }
+}
+
+// the same chain for a p010 rendition: bias (1 << 16) + the ring's 128 << 12 = 9 << 16,
+// av_clip_uintp2(v >> 17, 10) << 6, two 16-bit values per dword
+template <int VAR>
+__device__ __forceinline__ void vcalc7p(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                        const v4i (&rl)[Walk6<VAR>::VKB][Walk6<VAR>::T],
+                                        const v4i (&vh)[Walk6<VAR>::VKB], const v4i (&vl)[Walk6<VAR>::VKB],
+                                        uint32_t (&w)[Walk6<VAR>::T][2])
+{
+    using W = Walk6<VAR>;
+    v4i acc[W::T];
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] = (v4i){9, 9, 9, 9};
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vh[kb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] <<= 8;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rh[kb][t], vl[kb], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vh[kb], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) acc[t] <<= 8;
+#pragma unroll
+    for (int kb = 0; kb < W::VKB; ++kb)
+#pragma unroll
+        for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vl[kb], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < W::T; ++t) {
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (uint32_t)min(max(acc[t][i] >> 17, 0), 1023) << 6;
+        w[t][0] = __builtin_amdgcn_perm(o[1], o[0], 0x05040100u);
+        w[t][1] = __builtin_amdgcn_perm(o[3], o[2], 0x05040100u);
+    }
+}
+
 // a wave with no unit: stage its pieces, keep the group's barrier count
-template <bool IL>
+template <int SK>
 __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
@@ -341,7 +473,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
     __builtin_amdgcn_s_setprio(DTS_L7_STAGER_PRIO);     // diagnostic: the staging wave issues first
 #endif
     Stage7 Z;
-    Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63, IL && G.kind);
+    Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63, SK == 0 ? 1 : G.bpc);
 #pragma unroll
     for (int i = 0; i < NS7 - 1; ++i) {
         Z.pieces(lds7, i, i);
@@ -372,16 +504,30 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
 // exactly (128 (...) is a multiple of 128): the lo MFMAs run first from the bias, one
 // shift, and the hi MFMAs accumulate onto it -- y comes out of the matrix core and the
 // epilogue is the saturating pack (FFMIN(y, 32767), y >= -32768 for 8-bit sources).
-template <int VAR, bool RC, int HS, bool IL>
+//
+// SK: the source kind -- 0 planar 8-bit, 1 nv12 (chroma U V byte pairs, de-interleaved
+// in the A reads), 2 p010 (16-bit samples, VAR | 16: one column tile per plane).  p010
+// (input.c p010LEToY_c / p010LEToUV_c, swscale.c hScale16To15_c with sh = 9): the A
+// operands are the samples' raw little-endian bytes masked to (s >> 2, (s & 3) << 6) and
+// offset by 128, B the fragment triple of put6p (plan6.cpp); the three MFMA chains give
+//   y = FFMIN(sum(s c) >> 9, 32767) = 2 A + ((M + ((L + K) >> 8)) >> 7)
+// exactly (the floors nest), so the same saturating pack ends the H step.  8-bit outputs of
+// p010 sources add the ordered dither ff_dither_8x8_128[y & 7][(x + off) & 7] << 12 (off 3
+// for V) instead of the flat 64; p010 outputs (any source) are yuv2p010lX / cX:
+// av_clip_uintp2((sum + (1 << 16)) >> 17, 10) << 6.
+template <int VAR, bool RC, int HS, int SK>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
     using W = Walk6<VAR>;
     constexpr int CT = W::CT, HKB = W::HKB, VKB = W::VKB, T = W::T, R = W::R;
+    constexpr bool IL = SK == 1, P10 = SK == 2;
+    static_assert(!P10 || (VAR & 16), "p010 walks are the 16-bit variants");
+    constexpr int RKB = P10 ? 2 * HKB : HKB;        // MFMA K blocks per tile (p010: 32 samples each)
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
     const int lane = (int)threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     Stage7 Z;
-    Z.init(G, S, f, wave, waves, lane, W::NP == 2 && IL);
+    Z.init(G, S, f, wave, waves, lane, P10 ? (W::NP == 2 ? 4 : 2) : (W::NP == 2 && IL ? 2 : 1));
     // output planes: luma plane 0; nv12 chroma plane 1; yuv420p chroma planes 1 and 2
     uint64_t ob[2];
     uint32_t op[2];
@@ -395,34 +541,59 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         }
     }
     const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
-    // H B operands of the walk
-    v4i bh[CT][HKB], bl[CT][HKB];
+    // H B operands of the walk (p010: bh = the M fragments, bl = L, ba = A of put6p)
+    constexpr int BC = P10 ? RKB : HKB;
+    v4i bh[CT][BC], bl[CT][BC], ba[P10 ? CT : 1][P10 ? RKB : 1];
 #pragma unroll
     for (int c = 0; c < CT; ++c)
 #pragma unroll
-        for (int kb = 0; kb < HKB; ++kb) {
-            const uint64_t o = fr + (uint64_t)(U.hfrag + (uint32_t)(c * HKB + kb)) * 2048u;
-            bh[c][kb] = *GP6(g_cv4i, o);
-            bl[c][kb] = *GP6(g_cv4i, o + 1024);
+        for (int kb = 0; kb < BC; ++kb) {
+            if (P10) {
+                const uint64_t o = fr + (uint64_t)(U.hfrag + (uint32_t)(c * RKB + kb) * 2u) * 2048u;
+                bl[c][kb] = *GP6(g_cv4i, o);
+                bh[c][kb] = *GP6(g_cv4i, o + 1024);
+                ba[P10 ? c : 0][P10 ? kb : 0] = *GP6(g_cv4i, o + 2048);
+            } else {
+                const uint64_t o = fr + (uint64_t)(U.hfrag + (uint32_t)(c * HKB + kb)) * 2048u;
+                bh[c][kb] = *GP6(g_cv4i, o);
+                bl[c][kb] = *GP6(g_cv4i, o + 1024);
+            }
         }
+    // p010 sources, 8-bit outputs: the ordered dither of the lane's 4 values (row y & 7 = m & 7,
+    // column (4 g + i) & 7: the units start on 16-column boundaries), luma / U and V (offset 3),
+    // as the middle term of the V chain ((d + 128) << 12 = 256 (16 (d + 128)))
+    v4i vdit[2];
+    if (P10) {
+        static constexpr uint8_t kDit[8][8] = DTS_DITHER_8X8_128;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) vdit[p][i] = 16 * ((int)kDit[m & 7][(4 * g + i + 3 * p) & 7] + 128);
+    }
     // A read offsets in a stage: tile t = (plane t / CT, column tile t % CT), K block kb;
     // B64 variants: the two 8-byte halves of the lane's 16 (windows 8-column aligned)
     constexpr bool B64 = l7_b64(VAR);
     constexpr int NH = B64 ? 2 : 1;
     uint32_t aoff[T][HKB][NH];
-    // nv12 chroma: the U and V operands of column tile c come from the same 32 interleaved
-    // bytes per lane (two 16-B chunks: byte 2 (x0 + 64 kb + 16 g) of the strip)
-    constexpr bool il = W::NP == 2 && IL;        // (IL: the graph's source is nv12)
-    uint32_t ioff[CT][HKB][2];
-    if (il) {
+    // interleaved chroma (nv12; p010): the U and V operands of column tile c come from the
+    // same 32 staged bytes per lane (two 16-B chunks); p010 luma: one 16-B chunk of raw
+    // sample bytes per lane and K block
+    constexpr bool il = W::NP == 2 && (IL || P10);
+    constexpr int ICT = il || P10 ? CT : 1, IKB = il || P10 ? RKB : 1;
+    uint32_t ioff[ICT][IKB][2];
+    if (il || P10) {
         const uint32_t sw = 2u * (uint32_t)((m >> 3) & 1);
 #pragma unroll
-        for (int c = 0; c < CT; ++c)
+        for (int c = 0; c < ICT; ++c)
 #pragma unroll
-            for (int kb = 0; kb < HKB; ++kb)
+            for (int kb = 0; kb < IKB; ++kb)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const uint32_t cc = (2u * ((uint32_t)U.xo[c] + 64u * (uint32_t)kb + 16u * (uint32_t)g)) / 16u + h;
+                    // first staged byte of the lane's A chunk(s): nv12 2 (x0 + 64 kb + 16 g),
+                    // p010 chroma 4 (x0 + 32 kb + 8 g), p010 luma 2 (x0 + 32 kb + 8 g)
+                    const uint32_t b = IL ? 2u * ((uint32_t)U.xo[c] + 64u * (uint32_t)kb + 16u * (uint32_t)g)
+                                          : (W::NP == 2 ? 4u : 2u) * ((uint32_t)U.xo[c] + 32u * (uint32_t)kb + 8u * (uint32_t)g);
+                    const uint32_t cc = b / 16u + (uint32_t)h;
                     ioff[c][kb][h] = (cc >> 2) * 1024u + 16u * (4u * (uint32_t)m + ((cc & 3u) ^ sw));
                 }
     }
@@ -436,7 +607,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 for (int h = 0; h < NH; ++h) {
                     const uint32_t b = (uint32_t)U.xo[t % CT] + 64u * (uint32_t)kb + 16u * (uint32_t)g + 8u * (uint32_t)h;
                     const uint32_t c = b / 16u;
-                    aoff[t][kb][h] = il ? 0u : (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u +
+                    aoff[t][kb][h] = (il || P10) ? 0u : (uint32_t)((t / CT) * G.npc) * 1024u + (c >> 2) * 1024u +
                                      16u * (4u * (uint32_t)m + ((c & 3u) ^ sw)) + (B64 ? (b & 8u) : 0u);
                 }
     }
@@ -514,10 +685,22 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
             }
             fsu = fsu + 1 == FS ? 0 : fsu + 1;
-            uint32_t w[T];
-            vcalc<VAR>(rh, rl, vh, vl, w);
-            flush();
-            xchg7<VAR>(U, w, scr, m, g, lane, px);
+            bool p010out = false;
+            if constexpr (CT == 1 && P10) {
+                if (U.fmt == DTS_FMT_P010LE) {              // p010 rendition
+                    uint32_t w2[T][2];
+                    vcalc7p<VAR>(rh, rl, vh, vl, w2);
+                    flush();
+                    xchg7p<VAR>(U, w2, scr, m, g, lane, px);
+                    p010out = true;
+                }
+            }
+            if (!p010out) {
+                uint32_t w[T];
+                vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
+                flush();
+                xchg7<VAR>(U, w, scr, m, g, lane, px);
+            }
             pj = j;
             if (!DEFER_ST) flush();
             ++j;
@@ -556,8 +739,33 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 group_barrier7();
                 L7_STAMP(1);
             }
-            v4i a[T][HKB];
-            if (il) {
+            v4i a[T][RKB];
+            if (P10) {
+                // raw sample bytes masked to (s >> 2, (s & 3) << 6) ^ 0x80 (one v_bitop3 per dword)
+                const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
+#pragma unroll
+                for (int c = 0; c < CT; ++c)
+#pragma unroll
+                    for (int kb = 0; kb < RKB; ++kb) {
+                        if (W::NP == 1) {
+                            const v4i x = *reinterpret_cast<const v4i *>(st + ioff[c][kb][0]);
+                            a[c][kb] = (x & (int)0xFFC0FFC0u) ^ (int)0x80808080u;
+                        } else {
+                            // U V 16-bit pairs: dword 2 q + h = [U lo, U hi, V lo, V hi] of sample 2 q + h
+                            const v4i x = *reinterpret_cast<const v4i *>(st + ioff[c][kb][0]);
+                            const v4i y = *reinterpret_cast<const v4i *>(st + ioff[c][kb][1]);
+                            const uint32_t w8[8] = {(uint32_t)x.x, (uint32_t)x.y, (uint32_t)x.z, (uint32_t)x.w,
+                                                    (uint32_t)y.x, (uint32_t)y.y, (uint32_t)y.z, (uint32_t)y.w};
+#pragma unroll
+                            for (int q4 = 0; q4 < 4; ++q4) {
+                                const uint32_t u = __builtin_amdgcn_perm(w8[2 * q4 + 1], w8[2 * q4], 0x05040100u);
+                                const uint32_t v = __builtin_amdgcn_perm(w8[2 * q4 + 1], w8[2 * q4], 0x07060302u);
+                                a[c][kb][q4] = (int)((u & 0xFFC0FFC0u) ^ 0x80808080u);
+                                a[CT + c][kb][q4] = (int)((v & 0xFFC0FFC0u) ^ 0x80808080u);
+                            }
+                        }
+                    }
+            } else if (il) {
                 // nv12 chroma: even bytes are U, odd bytes V (yuv2nv12 order, input.c nv12ToUV_c)
                 const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
 #pragma unroll
@@ -619,7 +827,32 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     ah[t] = zero;
                     al[t] = hbias;
                 }
-                if (HS == 128) {
+                if (P10) {
+                    // L from K, >> 8, + M, >> 7, + A: y = FFMIN(sum(s c) >> 9, ...) before the pack
+                    const v4i kp = {538968064, 538968064, 538968064, 538968064};   // 32896 << 14
+#pragma unroll
+                    for (int t = 0; t < T; ++t) al[t] = kp;
+#pragma unroll
+                    for (int kb = 0; kb < RKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t)
+                            al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bl[t % CT][kb], al[t], 0, 0, 0);
+#pragma unroll
+                    for (int t = 0; t < T; ++t) al[t] >>= 8;
+#pragma unroll
+                    for (int kb = 0; kb < RKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t)
+                            al[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], bh[t % CT][kb], al[t], 0, 0, 0);
+#pragma unroll
+                    for (int t = 0; t < T; ++t) ah[t] = al[t] >> 7;
+#pragma unroll
+                    for (int kb = 0; kb < RKB; ++kb)
+#pragma unroll
+                        for (int t = 0; t < T; ++t)
+                            ah[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t][kb], ba[P10 ? t % CT : 0][P10 ? kb : 0],
+                                                                          ah[t], 0, 0, 0);
+                } else if (HS == 128) {
                     v4i x[T][HKB];
 #pragma unroll
                     for (int kb = 0; kb < HKB; ++kb)
@@ -646,7 +879,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                 }
                 const int rs = s % R;
-                if (HS == 128 && !RC) {
+                if ((HS == 128 || P10) && !RC) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
                         const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(ah[t].x, ah[t].y));
@@ -670,7 +903,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         int y[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const int v = min(HS == 128 ? ah[t][i] : ((ah[t][i] << 8) + al[t][i]) >> 7, 32767);
+                            const int v = min((HS == 128 || P10) ? ah[t][i] : ((ah[t][i] << 8) + al[t][i]) >> 7, 32767);
                             y[i] = (min(v, U.rc_cap) * U.rc_mul + U.rc_add) >> U.rc_sh;
                         }
                         const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)y[1], (uint32_t)y[0], 0x05040100u);
@@ -701,7 +934,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 
 // RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
 // the common kernel keeps its register allocation)
-template <bool RC, int HS, bool IL>
+template <bool RC, int HS, int SK>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -718,25 +951,33 @@ void k_ladder7(Ladder7Params P)
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
     if (wave >= G.nwaves) {
-        idle7<IL>(G, S, f, wave, waves);
+        idle7<SK>(G, S, f, wave, waves);
         return;
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
-    walk7<DTS_L7_ONLYVAR, RC, HS, IL>(P, G, U, S, f, wave, waves);
+    walk7<DTS_L7_ONLYVAR, RC, HS, SK>(P, G, U, S, f, wave, waves);
     return;
 #endif
+    if constexpr (SK == 2) {                // p010 sources: the 16-bit one-K-block variants
+        switch (U.variant) {
+        case 16: walk7<16, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        case 17: walk7<17, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        default: walk7<20, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        }
+    } else {
     switch (U.variant) {
-    case 0: walk7<0, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12, RC, HS, IL>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    }
     }
 }
 
@@ -763,29 +1004,34 @@ void ladder7_compiled(int *stages, int *batch)
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          bool interleaved, hipStream_t s)
+                          int src_kind, hipStream_t s)
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
-    if (interleaved) {                   // nv12 sources
+    if (src_kind == kSrcP010) {          // p010 sources (no range conversion: dts_graph_create refuses it)
+        if (range_conv) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_ladder7<false, 256, 2>), g, b, lds_bytes, s, p);
+        return hipGetLastError();
+    }
+    if (src_kind == kSrcNV12) {          // nv12 sources
         if (range_conv && hsplit == 128)
-            hipLaunchKernelGGL((k_ladder7<true, 128, true>), g, b, lds_bytes, s, p);
+            hipLaunchKernelGGL((k_ladder7<true, 128, 1>), g, b, lds_bytes, s, p);
         else if (range_conv)
-            hipLaunchKernelGGL((k_ladder7<true, 256, true>), g, b, lds_bytes, s, p);
+            hipLaunchKernelGGL((k_ladder7<true, 256, 1>), g, b, lds_bytes, s, p);
         else if (hsplit == 128)
-            hipLaunchKernelGGL((k_ladder7<false, 128, true>), g, b, lds_bytes, s, p);
+            hipLaunchKernelGGL((k_ladder7<false, 128, 1>), g, b, lds_bytes, s, p);
         else
-            hipLaunchKernelGGL((k_ladder7<false, 256, true>), g, b, lds_bytes, s, p);
+            hipLaunchKernelGGL((k_ladder7<false, 256, 1>), g, b, lds_bytes, s, p);
         return hipGetLastError();
     }
     if (range_conv && hsplit == 128)
-        hipLaunchKernelGGL((k_ladder7<true, 128, false>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<true, 128, 0>), g, b, lds_bytes, s, p);
     else if (range_conv)
-        hipLaunchKernelGGL((k_ladder7<true, 256, false>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<true, 256, 0>), g, b, lds_bytes, s, p);
     else if (hsplit == 128)
-        hipLaunchKernelGGL((k_ladder7<false, 128, false>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<false, 128, 0>), g, b, lds_bytes, s, p);
     else
-        hipLaunchKernelGGL((k_ladder7<false, 256, false>), g, b, lds_bytes, s, p);
+        hipLaunchKernelGGL((k_ladder7<false, 256, 0>), g, b, lds_bytes, s, p);
     return hipGetLastError();
 }
 

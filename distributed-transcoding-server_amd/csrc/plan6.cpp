@@ -53,6 +53,31 @@ int vtap6(const VTable &v, int y, int row)
     return (int16_t)(d & 1 ? w >> 16 : w & 0xffff);
 }
 
+// The H fragment triple of a 16-bit source (k_ladder7, ladder7.hip walk7 P10): the A
+// operand is 16 raw little-endian bytes of 8 samples per lane, hi byte hb = s >> 2 and lo
+// byte lbm = (s & 3) << 6 once masked, both offset by 128.  With c = 256 chi + clo (signed
+// bytes) the sum over the window is
+//   sum(64 s c) = 65536 sum(hb' chi) + 256 (sum(hb' clo) + sum(lbm' chi)) + sum(lbm' clo) + K
+// so three B operands, L = [clo, 0], M = [chi, clo], A = [0, 2 chi] over the (lo, hi) byte
+// positions, give the three terms; false if a tap does not split (2 chi beyond a byte).
+template <class F>
+bool put6p(std::vector<uint32_t> &bf, uint32_t pair, F tapf)
+{
+    uint8_t *L = reinterpret_cast<uint8_t *>(bf.data() + (size_t)pair * 512);
+    uint8_t *M = L + 1024, *A = L + 2048;
+    for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 16; ++j) {
+            const int c = tapf(lane, j / 2);          // sample j / 2 of the lane's 8
+            const int lo = (int8_t)(c & 0xff), hi = (c - lo) >> 8;
+            if (hi < -64 || hi > 63) return false;
+            const bool odd = j & 1;                   // the hi byte of the sample
+            L[lane * 16 + j] = (uint8_t)(odd ? 0 : lo);
+            M[lane * 16 + j] = (uint8_t)(odd ? lo : hi);
+            A[lane * 16 + j] = (uint8_t)(odd ? 2 * hi : 0);
+        }
+    return true;
+}
+
 // one fragment pair from tapf(lane, j) (j = byte of the lane's 16): c = 256 hi + lo,
 // hi and lo signed bytes (split 256), or c = 128 hi + lo with lo in [0, 127] (split 128);
 // false if a tap does not split
@@ -157,11 +182,13 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
     std::vector<Pending> todo;
     for (int kind = 0; kind < 2; ++kind) {
         const Plan5In &in = kinds[kind];
-        if (in.nv12_chroma && align) return false;         // k_ladder6: planar sources only (nv12: k_ladder5 / 7)
+        if ((in.nv12_chroma || in.p10) && align) return false;   // k_ladder6: planar 8-bit sources only
         if ((int)in.rungs.size() < 1 || (int)in.rungs.size() > DTS_MAX_OUTPUTS) return false;
         for (int k = 0; k < (int)in.rungs.size(); ++k) {
             const Plan5Rung &R = in.rungs[k];
-            if (R.fmt != DTS_FMT_YUV420P && R.fmt != DTS_FMT_NV12) return false;
+            // p010 renditions: k_ladder7 from p010 sources (one column tile per plane)
+            if (R.fmt != DTS_FMT_YUV420P && R.fmt != DTS_FMT_NV12 && (align || !in.p10 || R.fmt != DTS_FMT_P010LE))
+                return false;
             const SwsFilter &f = *R.fh;
             for (int i = 0; i < R.dstW; ++i) {             // H bias = 128 * 16384
                 int sum = 0;
@@ -179,6 +206,12 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
             const int np = in.chroma ? 2 : 1;
             if (align) {
                 if (!plan_h6(f, in.srcW, R.dstW, p.r, align) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
+            } else if (in.p10) {
+                // 16-bit samples: windows on 8-sample (16-byte) boundaries, one 64-sample K block
+                // (two raw-byte MFMA K blocks; wider windows keep the graph on k_ladder4: their
+                // B operands and A reads would not fit the walk's 128 registers)
+                if (!plan_h6(f, in.srcW, R.dstW, p.r, 8) || !plan_v6(*R.v, in.srcH, R.dstH, p.r)) return false;
+                if (p.r.hkb != 1 || (in.chroma && p.r.vkb != 1)) return false;   // (chroma: one V K block too)
             } else {
                 // k_ladder7: K windows on 16-column boundaries (one ds_read_b128 per A operand),
                 // or on 8-column boundaries where that saves a K block and the variant reads
@@ -191,12 +224,13 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
                 else if (!ok16)
                     return false;
             }
-            p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb, narrow));
+            p.ct = l6_ct(l6_variant(np, p.r.hkb, p.r.vkb, narrow) | (in.p10 ? 16 : 0));
             const int ntiles = (R.dstW + 15) / 16;
             const int ntp = (ntiles + p.ct - 1) / p.ct * p.ct;  // tiles padded to whole units
             p.r.x0.resize(ntp, 0);
             p.hfrag = nfrag;
-            nfrag += (uint32_t)(ntp * p.r.hkb);
+            // 16-bit sources: per tile 2 hkb raw K blocks, a fragment triple (2 pair slots) each
+            nfrag += (uint32_t)(ntp * p.r.hkb * (in.p10 ? 4 : 1));
             p.vfrag = nfrag;
             nfrag += (uint32_t)(p.r.fire.size() * p.r.vkb);
             p.fire = (int)out.fire.size();
@@ -211,9 +245,18 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
         const SwsFilter &f = *R.fh;
         const VTable &v = *R.v;
         const int np = in.chroma ? 2 : 1;
-        const int var = l6_variant(np, p.r.hkb, p.r.vkb, narrow);
+        const int var = l6_variant(np, p.r.hkb, p.r.vkb, narrow) | (in.p10 ? 16 : 0);
         const int ntp = (int)p.r.x0.size();
-        for (int t = 0; t < ntp; ++t)
+        for (int t = 0; t < ntp && in.p10; ++t)
+            for (int rkb = 0; rkb < 2 * p.r.hkb; ++rkb) {
+                const int base = p.r.x0[t] + 32 * rkb;        // raw K block rkb: 32 samples
+                if (!put6p(out.frag, p.hfrag + (uint32_t)(t * 2 * p.r.hkb + rkb) * 2u, [&](int lane, int js) {
+                        const int o = 16 * t + (lane & 15);
+                        return o < R.dstW ? htap6(f, o, base + 8 * (lane >> 4) + js) : 0;
+                    }))
+                    return false;
+            }
+        for (int t = 0; t < ntp && !in.p10; ++t)
             for (int kb = 0; kb < p.r.hkb; ++kb) {
                 const int base = p.r.x0[t] + 64 * kb;
                 if (!put6(out.frag, p.hfrag + (uint32_t)(t * p.r.hkb + kb), [&](int lane, int j) {
@@ -263,7 +306,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
             w.dstW = R.dstW;
             w.nrb = nrb;
             w.fmt = R.fmt;
-            w.hfrag = p.hfrag + (uint32_t)(u * p.ct * p.r.hkb);
+            w.hfrag = p.hfrag + (uint32_t)(u * p.ct * p.r.hkb * (in.p10 ? 4 : 1));
             w.vfrag = p.vfrag;
             w.fire = p.fire;
             for (int c = 0; c < 4; ++c) w.x0[c] = c < p.ct ? p.r.x0[(size_t)u * p.ct + c] : 0;
@@ -307,9 +350,13 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         }
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
+    const int wmax0 = wmax;
     for (int kind = 0; kind < 2; ++kind) {
         const int srcW = kinds[kind].srcW, np = kinds[kind].chroma ? 2 : 1;
         if (srcW % 16) return false;
+        // p010 chroma stages 4 bytes per column: groups of half the waves keep two
+        // workgroups' stages within one CU's LDS
+        wmax = kinds[kind].p10 && kind ? std::max(1, wmax0 / 2) : wmax0;
         std::vector<Unit6> us;
         for (const Unit6 &u : p6.units)
             if (u.kind == kind) us.push_back(u);
@@ -425,7 +472,8 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             g.X0 = std::min(a, srcW - 64 * g.npc);
             if (g.X0 < 0 || g.X0 % 16) return false;
             // per rendition: the first wave of the group DMAs its V fragments; slots in LDS
-            int lds = stages * pb * np * g.npc * 1024;
+            const int bpc = kinds[kind].p10 ? (np == 2 ? 4 : 2) : (kinds[kind].nv12_chroma ? 2 : 1);
+            int lds = stages * pb * (bpc == 1 ? np : 1) * bpc * g.npc * 1024;
             int flds[DTS_MAX_OUTPUTS], lead[DTS_MAX_OUTPUTS];
             for (int r = 0; r < DTS_MAX_OUTPUTS; ++r) flds[r] = lead[r] = -1;
             for (int i = u; i < u + cnt; ++i) {
@@ -471,7 +519,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                 out.units.push_back(v);
             }
             g.scr = lds;
-            g.il = kinds[kind].nv12_chroma ? 1 : 0;
+            g.bpc = bpc;
             out.groups.push_back(g);
             u += cnt;
         }

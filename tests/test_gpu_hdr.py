@@ -22,13 +22,38 @@ BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
 MAX_OFF_BY_ONE = 0.01
 
 
-@pytest.fixture(params=["v4", "v3"])
+@pytest.fixture(params=["v7", "v4", "v3"])
 def ladder_kernel(request, monkeypatch):
-    if request.param == "v3":
-        monkeypatch.setenv("DTS_LADDER", "3")
-    else:
+    """The default choice (k_ladder7's 16-bit walks for p010 sources where they fit),
+    DTS_LADDER=4 (k_ladder4) and DTS_LADDER=3."""
+    if request.param == "v7":
         monkeypatch.delenv("DTS_LADDER", raising=False)
+    else:
+        monkeypatch.setenv("DTS_LADDER", request.param[1])
     return request.param
+
+
+@pytest.mark.parametrize("outs", [
+    [(1920, 1080, D.FMT_P010LE, BIC)],
+    [(1920, 1080, D.FMT_YUV420P, BIC), (1600, 900, D.FMT_NV12, BIL), (2560, 1440, D.FMT_P010LE, LAN)],
+    [(2880, 1620, D.FMT_P010LE, BIC), (1920, 1080, D.FMT_NV12, LAN)],
+])
+def test_p010_sources_on_ladder7(ctx, outs):
+    """p010 sources on k_ladder7's 16-bit walks (three raw-byte MFMA chains per K block,
+    the p010 V epilogue, the ordered dither for 8-bit renditions): bit-exact vs the
+    oracle on synthetic and fully random 16-bit words (the low 6 bits discarded, as
+    p010LEToY_c's >> 6), including the 1080p intermediate of config 3."""
+    sw, sh = 3840, 2160
+    rng = np.random.default_rng(31)
+    frames = [D.synth_host(sw, sh, D.FMT_P010LE, 0, 0x5EED, 2), random_frame(sw, sh, D.FMT_P010LE, rng)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_P010LE, outs))
+    assert g.info.ladder_v5 == 3, "the graph should run on k_ladder7"
+    got, _ = g.run_host(frames)
+    for f, src in enumerate(frames):
+        for k, o in enumerate(outs):
+            want = oracle_frame(src, sw, sh, D.FMT_P010LE, o[0], o[1], o[2], o[3])
+            assert planes_equal(got[f][k], want), f"frame {f} out {k} {o}: {first_diff(got[f][k], want)}"
+    g.close()
 
 
 @pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
