@@ -25,9 +25,6 @@ using namespace dts;
 #ifdef DTS_L5_STAMP
 namespace dts { int ladder5_stamps(unsigned long long *out, bool reset); }
 #endif
-#ifdef DTS_L6_STAMP
-namespace dts { int ladder6_stamps(unsigned long long *out, bool reset); }
-#endif
 #ifdef DTS_L7_STAMP
 namespace dts { int ladder7_stamps(unsigned long long *out, bool reset); }
 #endif
@@ -191,16 +188,8 @@ struct dts_graph {
     Job5 *dev_jobs5 = nullptr;
     Kind5 *dev_kinds5 = nullptr;
     int njobs5 = 0, lds5 = 0, grid5 = 0;
-    // v6 ladder (ladder6.hip): planar 8-bit sources; v5 stays planned for frames whose
-    // planes are not 4-byte aligned
-    bool v6 = false;
-    void *dev_tables6 = nullptr;
-    const Unit6 *dev_units6 = nullptr;
-    const uint32_t *dev_frag6 = nullptr;
-    const int32_t *dev_fire6 = nullptr;
-    int nunits6 = 0, lds6 = 0;
-    // v7 ladder (ladder7.hip): the v6 waves in strip groups; k_ladder6 / k_ladder5 run
-    // frames whose planes are not 16-byte aligned
+    // v7 ladder (ladder7.hip): wave walks in strip groups; k_ladder5 (8-bit) / k_ladder4
+    // (p010) run frames whose planes are not 16-byte aligned
     bool v7 = false;
     void *dev_tables7 = nullptr;
     const Group7 *dev_groups7 = nullptr;
@@ -457,8 +446,6 @@ struct GraphPlan {
     Plan5Kind p5[2];                      // luma, chroma
     std::vector<Job5> jobs5;
     int lds5 = 0;
-    bool v6 = false;                      // ... and on k_ladder6 where frames are 4-byte aligned
-    Plan6 p6;
     bool v7 = false;                      // ... and on k_ladder7 where frames are 16-byte aligned
     Plan7 p7;
     dts_graph_info info{};
@@ -514,14 +501,7 @@ bool v5_enabled()
     return !(f && (f[0] == '3' || f[0] == '4'));
 }
 
-// DTS_LADDER=5 / 4 / 3 keep the graph off the v6 kernel
-bool v6_enabled()
-{
-    const char *f = std::getenv("DTS_LADDER");
-    return !(f && (f[0] == '3' || f[0] == '4' || f[0] == '5'));
-}
-
-// DTS_LADDER=6 / 5 / 4 / 3 keep the graph off the v7 kernel
+// DTS_LADDER=5 / 4 / 3 keep the graph off the v7 kernel (6: the retired k_ladder6, read as 5)
 bool v7_enabled()
 {
     const char *f = std::getenv("DTS_LADDER");
@@ -585,7 +565,7 @@ bool l7_narrow()
 }
 
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
-// and k_ladder6 too where it fits
+// and k_ladder7 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
 {
     if (!v5_enabled() || s.hdr_to_sdr) return false;
@@ -612,10 +592,9 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     std::stable_sort(gp.jobs5.begin(), gp.jobs5.end(), [&](const Job5 &a, const Job5 &b) { return srcx(a) < srcx(b); });
     gp.lds5 = std::max(gp.p5[0].lds_bytes, gp.p5[1].lds_bytes);
     gp.v5 = true;
-    gp.v6 = v6_enabled() && plan6_graph(ins, gp.p6);
-    // k_ladder7 takes planar and nv12 sources (k_ladder6 planar only: the fallback for planar
-    // frames that are not 16-byte aligned; v5 for the rest)
-    gp.v7 = v6_enabled() && v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
+    // k_ladder7 takes planar and nv12 sources (k_ladder5: the fallback for frames that are
+    // not 16-byte aligned)
+    gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
                                                         l7_stager(), gp.p7);
     return true;
 }
@@ -625,7 +604,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
 // not 16-byte aligned
 bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
 {
-    if (!v6_enabled() || !v7_enabled() || s.src_fmt != DTS_FMT_P010LE) return false;
+    if (!v7_enabled() || s.src_fmt != DTS_FMT_P010LE) return false;
     if ((s.range & 1) != ((s.range >> 4) & 1)) return false;
     Plan5In ins[2];
     for (int kind = 0; kind < 2; ++kind) {
@@ -637,7 +616,9 @@ bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
         in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
         for (int k = 0; k < s.nout; ++k) {
             const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
-            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
+            // an HDR graph's ladder writes the p010 intermediates k_tonemap reads
+            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH,
+                                         s.hdr_to_sdr ? (int)DTS_FMT_P010LE : s.out[k].fmt});
         }
     }
     return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, l7_stager(), gp.p7);
@@ -769,10 +750,10 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     if (s.quality) algo += in.out_frame_bytes[s.quality_out];
     in.algo_bytes_per_frame = algo;
     in.njobs = gp.v7 ? (int)gp.p7.groups.size()
-                     : gp.v6 ? (int)gp.p6.units.size() : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
-    in.lds_bytes = gp.v7 ? gp.p7.lds_bytes : gp.v6 ? gp.p6.lds_bytes : std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
+                     : (int)(gp.jobs.size() + gp.jobs4.size() + gp.jobs5.size());
+    in.lds_bytes = gp.v7 ? gp.p7.lds_bytes : std::max(std::max(gp.lds_bytes, gp.lds4), gp.lds5);
     in.ladder_v4_mask = (int32_t)gp.v4_mask;
-    in.ladder_v5 = gp.v7 ? 3 : gp.v6 ? 2 : (gp.v5 ? 1 : 0);
+    in.ladder_v5 = gp.v7 ? 3 : (gp.v5 ? 1 : 0);
     for (int kind = 0; kind < 2; ++kind) {
         in.v5_strip_width[kind] = gp.v5 ? gp.p5[kind].strip_width : 0;
         in.v5_strips[kind] = gp.v5 ? (int32_t)gp.p5[kind].strips.size() : 0;
@@ -1045,26 +1026,6 @@ static int upload_v5(dts_graph *g, const GraphPlan &gp)
     return DTS_OK;
 }
 
-// v6 tables -> one device blob (units, fragment pairs, fire tables)
-static int upload_v6(dts_graph *g, const GraphPlan &gp)
-{
-    dts_ctx *ctx = g->ctx;
-    std::vector<uint8_t> blob;
-    const size_t u_off = push_blob(blob, gp.p6.units);
-    const size_t f_off = push_blob(blob, gp.p6.frag);
-    const size_t r_off = push_blob(blob, gp.p6.fire);
-    HIPCHK(ctx, hipMalloc(&g->dev_tables6, blob.size()));
-    HIPCHK(ctx, hipMemcpy(g->dev_tables6, blob.data(), blob.size(), hipMemcpyHostToDevice));
-    const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables6);
-    g->dev_units6 = reinterpret_cast<const Unit6 *>(base + u_off);
-    g->dev_frag6 = reinterpret_cast<const uint32_t *>(base + f_off);
-    g->dev_fire6 = reinterpret_cast<const int32_t *>(base + r_off);
-    g->nunits6 = (int)gp.p6.units.size();
-    g->lds6 = gp.p6.lds_bytes;
-    g->v6 = true;
-    return DTS_OK;
-}
-
 // v7 tables -> one device blob (groups, units, fragment pairs, fire tables)
 static int upload_v7(dts_graph *g, const GraphPlan &gp)
 {
@@ -1116,7 +1077,6 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         e = gp.v5 ? DTS_OK : upload_v3(g, gp.kts);
         if (!e && gp.v4_mask) e = upload_v4(g, gp);
         if (!e && gp.v5) e = upload_v5(g, gp);
-        if (!e && gp.v6) e = upload_v6(g, gp);
         if (!e && gp.v7) e = upload_v7(g, gp);
         if (!e && hipMalloc(&g->dev_queue, kQueueSlots * kQueueWidth * sizeof(unsigned int)) != hipSuccess) {
             ctx->last_hip = (int)hipGetLastError();
@@ -1254,7 +1214,6 @@ void dts_graph_destroy(dts_graph *g)
     if (g->dev_tables) hipFree(g->dev_tables);
     if (g->dev_tables4) hipFree(g->dev_tables4);
     if (g->dev_tables5) hipFree(g->dev_tables5);
-    if (g->dev_tables6) hipFree(g->dev_tables6);
     if (g->dev_tables7) hipFree(g->dev_tables7);
     if (g->dev_queue) hipFree(g->dev_queue);
     qscratch_free(g->qs);
@@ -1401,9 +1360,9 @@ static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, co
     return DTS_OK;
 }
 
-// k_ladder6 reads and writes planes with 4-byte accesses: every plane base and pitch
-// 4-byte aligned (else the graph runs on k_ladder5)
-static bool planes_aligned6(const DevPlanes &p)
+// k_ladder7 writes its outputs with 4-byte (and wider) row segments: every output plane
+// base and pitch 4-byte aligned
+static bool planes_aligned4(const DevPlanes &p)
 {
     for (int pl = 0; pl < 3; ++pl)
         if ((p.data[pl] | (uint64_t)p.pitch[pl]) & 3u) return false;
@@ -1411,7 +1370,7 @@ static bool planes_aligned6(const DevPlanes &p)
 }
 
 // k_ladder7 stages source rows with 16-byte LDS-DMA lanes: every plane base and pitch
-// 16-byte aligned (else k_ladder6 / k_ladder5)
+// 16-byte aligned (else k_ladder5 / k_ladder4)
 static bool planes_aligned7(const DevPlanes &p)
 {
     for (int pl = 0; pl < 3; ++pl)
@@ -1444,7 +1403,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     p.stage_bytes = g->stage_bytes;
     p.jobs = g->dev_jobs;
     p.rk = g->dev_rk;
-    const int njobs_max = std::max(1, std::max(std::max(p.njobs, g->njobs4), std::max(g->njobs5, g->nunits6)));
+    const int njobs_max = std::max(1, std::max(std::max(p.njobs, g->njobs4), g->njobs5));
     const int max_frames = std::max(1, (1 << 30) / njobs_max);
     for (int f0 = 0; f0 < nframes; f0 += max_frames) {
         const int n = std::min(max_frames, nframes - f0);
@@ -1454,9 +1413,8 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
         for (int pl = 0; pl < 3; ++pl) pp.src.data[pl] += (uint64_t)(f0 * src.fstride);
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k)
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
-        // (k_ladder7 stores whole 4-, 8- or 16-byte row segments: outputs as k_ladder6 needs them)
         bool aligned7 = g->v7 && planes_aligned7(pp.src);
-        for (int k = 0; k < s.nout && aligned7; ++k) aligned7 = planes_aligned6(pp.dst[k]);
+        for (int k = 0; k < s.nout && aligned7; ++k) aligned7 = planes_aligned4(pp.dst[k]);
         if (!aligned7 && (s.range & 1) != ((s.range >> 4) & 1)) return DTS_E_UNSUPPORTED;   // range conversion: v7 only
         if (aligned7) {
             Ladder7Params q{};
@@ -1472,22 +1430,6 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             if (grid > INT32_MAX) return DTS_E_RANGE;
             HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
                                        g->hsplit7, g->src_kind, st));
-            continue;
-        }
-        bool aligned6 = g->v6 && planes_aligned6(pp.src);
-        for (int k = 0; k < s.nout && aligned6; ++k) aligned6 = planes_aligned6(pp.dst[k]);
-        if (aligned6) {
-            Ladder6Params q{};
-            q.src = pp.src;
-            for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
-            q.nunits = g->nunits6;
-            q.nframes = n;
-            q.units = g->dev_units6;
-            q.frag = g->dev_frag6;
-            q.fire = g->dev_fire6;
-            const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->nunits6;
-            if (grid > INT32_MAX) return DTS_E_RANGE;
-            HIPCHK(ctx, launch_ladder6(q, (int)grid, g->lds6, st));
             continue;
         }
         if (g->v5) {
@@ -2209,10 +2151,6 @@ int dts_synth_device(dts_ctx *ctx, int w, int h, int fmt, int pattern, uint32_t 
 int dts_debug_ladder5_stamps(unsigned long long *out, int reset) { return dts::ladder5_stamps(out, reset != 0); }
 #endif
 
-#ifdef DTS_L6_STAMP
-// diagnostic builds only (tools/build_stamp6.sh): per-variant, per-phase cycle sums of k_ladder6
-int dts_debug_ladder6_stamps(unsigned long long *out, int reset) { return dts::ladder6_stamps(out, reset != 0); }
-#endif
 #ifdef DTS_L7_STAMP
 // diagnostic builds only (tools/build_stamp7.sh): per-variant, per-phase cycle sums of k_ladder7
 extern "C" int dts_debug_ladder7_stamps(unsigned long long *out, int reset) { return dts::ladder7_stamps(out, reset != 0); }

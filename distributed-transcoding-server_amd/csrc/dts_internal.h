@@ -241,14 +241,13 @@ hipError_t launch_ladder5(const Ladder5Params &p, int src_kind, int lds_bytes, i
 int ladder5_blocks_per_cu(int src_kind, int lds_bytes);
 
 // ---------------------------------------------------------------------------
-// v6 ladder (ladder6.hip, plan6.cpp): one wave per (frame, plane kind,
+// ladder work units (plan6.cpp, ladder7.hip): one wave per (frame, plane kind,
 // rendition, column group), walking the plane top to bottom; the H outputs stay
-// in VGPRs (the H MFMA's C layout is the V MFMA's A layout), so there is no LDS,
-// no barrier and no ring traffic.
+// in VGPRs (the H MFMA's C layout is the V MFMA's A layout).
 // ---------------------------------------------------------------------------
 constexpr int kL6Gran = 16;         // source rows per granule (the H MFMA's M)
-constexpr int kL6Stages = 4;        // source granules in flight per wave (LDS stages; ladder6.hip DTS_L6_NS <= this)
-constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, V K blocks), ladder6.hip
+constexpr int kL6Stages = 4;        // V fragment slots: row blocks firing within this many granules
+constexpr int kL6Variants = 8;      // (column tiles CT, planes NP, H K blocks, V K blocks)
 
 // variant v: NP planes (luma 1; chroma 2: U and V), HKB K blocks of 64 source columns
 // per H tile, VKB K blocks of 64 source rows (4 VKB granules held) per V row block, and
@@ -270,7 +269,7 @@ constexpr int l6_ct(int v) { return (v & 16) ? 1 : ((v & 3) == 0 && !(v & 8) ? 4
 constexpr bool l7_b64(int v) { return v == 1 || v == 5; }
 
 struct Unit6 {                      // one wave's share of a frame
-    int32_t variant;                // ladder6.hip kVar6[variant]
+    int32_t variant;                // l6_variant(): the walk shape
     int32_t kind;                   // 0 luma, 1 chroma (U and V planes in one unit)
     int32_t rung;
     int32_t col0;                   // first output column (multiple of 16)
@@ -289,21 +288,9 @@ struct Unit6 {                      // one wave's share of a frame
     int32_t pad_;
 };
 
-struct Ladder6Params {
-    DevPlanes src;
-    DevPlanes dst[kMaxRungs];
-    int32_t nunits, nframes, pad_[2];
-    const Unit6 *units;
-    const uint32_t *frag;           // fragment pairs (taps >> 8, taps & 255 as signed bytes), 512 dwords each
-    const int32_t *fire;
-};
-
-hipError_t launch_ladder6(const Ladder6Params &p, int grid, int lds_bytes, hipStream_t s);
-// LDS per wave of a unit: its source stages and its V fragment slots
-int ladder6_lds_bytes(const Unit6 &u);
 
 // ---------------------------------------------------------------------------
-// v7 ladder (ladder7.hip, plan6.cpp plan7_graph): the v6 waves (same variants,
+// v7 ladder (ladder7.hip, plan6.cpp plan7_graph): the work-unit waves (Unit6 variants,
 // same H -> V register pipeline), grouped into workgroups that cover one source
 // column strip of one plane kind for every rendition.  Per granule the group
 // stages the strip's 16 source rows into LDS once (LDS-DMA pieces dealt over its

@@ -107,30 +107,29 @@ struct Plan5Kind {
 // false: the geometry / format does not fit k_ladder5 (the kind then runs on v4 / v3)
 bool plan5_kind(const Plan5In &in, Plan5Kind &out);
 
-// v6 ladder plan (plan6.cpp, ladder6.hip): the work units of one frame (both
-// plane kinds, every rendition), their B fragments and the V fire tables.
+// ladder work-unit plan (plan6.cpp): the work units of one frame (both plane kinds,
+// every rendition), their B fragments and the V fire tables; plan7_graph groups them.
 struct Plan6 {
     std::vector<Unit6> units;
     std::vector<uint32_t> frag;      // fragment pairs, 512 dwords each
     std::vector<int32_t> fire;
-    int lds_bytes = 0;               // dynamic LDS of the launch (the largest unit's)
 };
 
 // kinds[0] luma, kinds[1] chroma (Plan5In: same inputs as v5).  false: the graph
-// does not fit k_ladder6 (nv12 source, planes narrower than 64 or 128 columns,
-// windows wider than two K blocks ...): it then runs on k_ladder5.
-// align: the H K windows start on multiples of align source columns (4 for k_ladder6;
-// 16 for k_ladder7, whose A operands are 16-B LDS reads); sort: heaviest units first.
+// does not fit the walks (planes narrower than 64 or 128 columns, windows wider
+// than two K blocks ...): it then runs on k_ladder5.
+// align: the H K windows start on multiples of align source columns (16 for k_ladder7,
+// whose A operands are 16-B LDS reads; 0: 8 or 16); sort: heaviest units first.
 // narrow (k_ladder7): the one-K-block walks get 2 tiles per plane (luma) / 1 (chroma), not 4 / 2
 // fs_window: granules whose firing row blocks share the V fragment slots
-// hsplit: the H taps as hsplit * hi + lo (256: lo a signed byte, k_ladder6; 128: lo in
+// hsplit: the H taps as hsplit * hi + lo (256: lo a signed byte; 128: lo in
 // [0, 127], k_ladder7's one-shift epilogue; false if a tap does not split)
 bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align = 4, bool sort = true, bool narrow = false,
                  int fs_window = kL6Stages, int hsplit = 256);
 
-// v7 ladder plan: the v6 units (align 16) in groups of at most wmax waves over one
+// v7 ladder plan: the work units (align 16) in groups of at most wmax waves over one
 // source strip (Group7, Unit7).  false: the graph does not fit k_ladder7 (plane widths
-// not multiples of 16, strips wider than the plane ...): k_ladder6 / k_ladder5 run it.
+// not multiples of 16, strips wider than the plane ...): k_ladder5 / k_ladder4 run it.
 struct Plan7 {
     std::vector<Group7> groups;
     std::vector<Unit7> units;

@@ -1,23 +1,38 @@
-// ladder7.hip -- k_ladder7, the v7 ladder kernel: 8-bit 4:2:0 planar sources to
-// 8-bit renditions on v_mfma_i32_16x16x64_i8, the source staged once per strip.
+// ladder7.hip -- k_ladder7, the ladder kernel: 4:2:0 sources (8-bit planar, nv12,
+// p010) to every rendition of a graph, both FIR passes on v_mfma_i32_16x16x64_i8,
+// the source staged once per strip and the H outputs never leaving the VGPRs.
 //
-// Same arithmetic and the same per-wave pipeline as k_ladder6 (ladder6.hip header;
-// libswscale hScale8To15_c -> yuv2planeX_8_c / yuv2nv12cX_c under
-// SWS_BITEXACT|SWS_ACCURATE_RND, FFmpeg 4.4): a wave owns CT 16-column tiles of
-// one rendition of one plane kind and walks them top to bottom in granules of 16
-// source rows; H per granule and tile on the matrix cores, the H results kept in a
-// register ring that is the V MFMA's A operand, V per 16-row block right after the
-// granule that completes its window, coalesced row stores.
+// Arithmetic: libswscale hScale8To15_c / hScale16To15 -> yuv2planeX_8_c /
+// yuv2nv12cX_c / yuv2p010lX_c under SWS_BITEXACT|SWS_ACCURATE_RND (FFmpeg 4.4;
+// bit-exact, DESIGN.md "Oracle"), the integer identities of k_ladder5 (ladder5.hip
+// header) on signed-byte MFMA operands:
 //
-// What changes is where the A operands come from.  k_ladder6 stages, per wave,
-// the 16 rows x 64 columns of every (tile, K block) it needs: every rendition and
-// every column tile fetches its own copy of the source, ~5x the plane per frame
-// through L2, and the LDS-DMA issue of those copies was ~45 % of a wave's cycles
-// (profiles/r02b_*; tools/stamp6.py).  Here a workgroup is a group of waves of
-// every rendition whose K windows lie in one source strip [X0, X0 + 64 npc) of the
-// plane(s) (plan6.cpp plan7_graph); per granule the group DMAs the strip's 16 rows
-// into LDS once -- npc 1-KB pieces per plane, dealt round robin over all its waves
-// -- and every wave reads its A operands there:
+//  * one wave = one work unit: CT 16-column tiles of one rendition of one plane
+//    kind (chroma: the same columns of U and V) of one frame, walked top to bottom
+//    in granules of 16 source rows;
+//  * H of a granule: per tile one MFMA per K block and tap part.  A = 16 source rows
+//    x 64 columns (bytes xor 0x80), B = the tile's taps split into signed bytes
+//    (c = HS hi + lo, plan6.cpp put6), held in VGPRs for the whole walk; p010: A =
+//    the raw little-endian bytes, three chains (walk7 header below);
+//  * the H result of a tile is, per lane, 4 consecutive source rows of one output
+//    column -- a V A-operand dword once split into y >> 8 and (y & 255) ^ 0x80
+//    bytes.  The last 4 VKB granules of every tile stay in a register ring (slot =
+//    granule mod 4 VKB; the walk is unrolled by the ring length, so every slot is a
+//    fixed register);
+//  * V of a row block (16 output rows) runs after the granule that completes its
+//    window: out^T = H^T C^T over the whole ring, the fragment laid out for where
+//    each granule sits in the ring;
+//  * stores: each lane holds 4 consecutive columns of one output row per tile;
+//    permlane swaps transpose the tiles so a lane holds 4-16 consecutive bytes of its
+//    row (nv12: U and V interleaved by v_perm), stored as whole row segments.
+//
+// Staging: a workgroup is a group of waves of every rendition whose K windows lie in
+// one source strip [X0, X0 + 64 npc) of the plane(s) (plan6.cpp plan7_graph); per
+// granule the group DMAs the strip's 16 rows into LDS once -- npc 1-KB pieces per
+// plane, dealt round robin over all its waves -- and every wave reads its A operands
+// there.  (Per-wave staging of every (tile, K block), the retired k_ladder6, moved
+// ~5x the plane per frame through L2 and spent ~45 % of a wave's cycles issuing it:
+// profiles/r02b_*.)
 //
 //  * LDS image of a piece: 16 rows x 64 bytes, lane-linear as the DMA writes it.
 //    DMA lane l loads row l >> 2, 16-B chunk (l & 3) ^ sw(row), sw(r) = 2 ((r >> 3) & 1):

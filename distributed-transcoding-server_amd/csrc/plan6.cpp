@@ -1,5 +1,5 @@
-// plan6.cpp -- host planning of the v6 ladder (ladder6.hip, dts_internal.h
-// "v6 ladder"): per frame, one work unit per (plane kind, rendition, group of
+// plan6.cpp -- host planning of the ladder work units (ladder7.hip, dts_internal.h
+// "ladder work units"): per frame, one work unit per (plane kind, rendition, group of
 // 16-column tiles); per tile the H K blocks (64 source columns each) and their
 // B fragments; per rendition the V row blocks (16 output rows), the granule
 // after which each runs and its B fragments.  The taps are the libswscale
@@ -182,7 +182,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
     std::vector<Pending> todo;
     for (int kind = 0; kind < 2; ++kind) {
         const Plan5In &in = kinds[kind];
-        if ((in.nv12_chroma || in.p10) && align) return false;   // k_ladder6: planar 8-bit sources only
+        if ((in.nv12_chroma || in.p10) && align) return false;   // 4-column windows: planar 8-bit sources only
         if ((int)in.rungs.size() < 1 || (int)in.rungs.size() > DTS_MAX_OUTPUTS) return false;
         for (int k = 0; k < (int)in.rungs.size(); ++k) {
             const Plan5Rung &R = in.rungs[k];
@@ -311,7 +311,6 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
             w.fire = p.fire;
             for (int c = 0; c < 4; ++c) w.x0[c] = c < p.ct ? p.r.x0[(size_t)u * p.ct + c] : 0;
             w.fs = fs;
-            out.lds_bytes = std::max(out.lds_bytes, ladder6_lds_bytes(w));
             // MFMAs per unit: H ngran x tiles x HKB x 2, V row blocks x tiles x VKB x 4
             const int tiles = p.ct * np;
             const int64_t cost = (int64_t)ngran * tiles * p.r.hkb * 2 + (int64_t)nrb * tiles * p.r.vkb * 4;

@@ -196,12 +196,12 @@ typedef struct dts_graph_info {
                                            ladder kernel (the rest on v3; DTS_LADDER=3 forces v3) */
     int32_t h_pairs4[DTS_MAX_OUTPUTS][2]; /* v4 H tap pairs per output (luma, chroma), 0 = v3 */
     int32_t ladder_v5;                  /* 1: the whole graph runs on the v5 ladder kernel (H on the
-                                           matrix cores); 2: on the v6 kernel (H and V on the matrix
-                                           cores, H outputs in registers; v5 for frames whose planes
-                                           are not 4-byte aligned); 3: on the v7 kernel (v6's waves
-                                           in workgroups that stage each source strip once; plane
-                                           widths multiples of 16).  DTS_LADDER=6 / 5 / 4 / 3 force
-                                           v6 / v5 / v4 / v3 */
+                                           matrix cores); 3: on the v7 kernel (H and V on the matrix
+                                           cores, H outputs in registers, waves in workgroups that
+                                           stage each source strip once; plane widths multiples of
+                                           16; v5 / v4 for frames whose planes are not 16-byte
+                                           aligned).  2 (the retired v6 kernel) is no longer
+                                           produced.  DTS_LADDER=5 (or 6) / 4 / 3 force v5 / v4 / v3 */
     int32_t v5_strip_width[2];          /* v5 source columns per strip (luma, chroma) */
     int32_t v5_strips[2];               /* v5 strips per plane kind */
 } dts_graph_info;

@@ -17,12 +17,11 @@ pytestmark = pytest.mark.gpu
 BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
 
 
-@pytest.fixture(autouse=True, params=["v7", "v6", "v5", "v4", "v3"])
+@pytest.fixture(autouse=True, params=["v7", "v5", "v4", "v3"])
 def ladder_kernel(request, monkeypatch):
-    """Every parity case runs five times: the default kernel choice (v7, the
+    """Every parity case runs four times: the default kernel choice (v7, the
     strip-staged matrix-core ladder, wherever the graph fits it and the planes are
-    16-byte aligned, else v6, else v5), DTS_LADDER=6 (v6 where it fits), DTS_LADDER=5
-    (v5 where it fits), DTS_LADDER=4 (v4 where the geometry fits it, else v3) and
+    16-byte aligned, else v5), DTS_LADDER=5 (v5 where it fits), DTS_LADDER=4 (v4 where the geometry fits it, else v3) and
     DTS_LADDER=3 (v3 for every plane)."""
     if request.param == "v7":
         monkeypatch.delenv("DTS_LADDER", raising=False)
@@ -92,7 +91,7 @@ def test_ladder_4k_one_frame(ctx, ladder_kernel):
     frames = [D.synth_host(3840, 2160, D.FMT_YUV420P, 0, 0x5EED, 0)]
     outs = [(1920, 1080, D.FMT_NV12, BIC), (1280, 720, D.FMT_NV12, BIC), (854, 480, D.FMT_NV12, BIC)]
     g = D.Graph(ctx, D.make_spec(3840, 2160, D.FMT_YUV420P, outs))
-    assert g.info.ladder_v5 == {"v7": 3, "v6": 2, "v5": 1}.get(ladder_kernel, 0)
+    assert g.info.ladder_v5 == {"v7": 3, "v5": 1}.get(ladder_kernel, 0)
     assert g.info.ladder_v4_mask == (0x3f if ladder_kernel == "v4" else 0)
     g.close()
     run_and_check(ctx, 3840, 2160, D.FMT_YUV420P, outs, frames)
@@ -240,7 +239,7 @@ def test_v7_geometries(ctx, ladder_kernel, sw, sh, outs, method):
     """Plane widths that are multiples of 16 (k_ladder7's domain): single-granule
     planes, upscales, tall / wide planes, 1:1 renditions; nv12 and yuv420p outputs,
     bit-exact vs the oracle on every kernel."""
-    if ladder_kernel not in ("v7", "v6"):
+    if ladder_kernel != "v7":
         pytest.skip("the v5 / v4 / v3 kernels are covered by the other geometry tests")
     rng = np.random.default_rng(sw + 7 * sh + method)
     frames = [random_frame(sw, sh, D.FMT_YUV420P, rng), D.synth_host(sw, sh, D.FMT_YUV420P, 0, 5, 3)]

@@ -145,17 +145,14 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
     assert D.graph_plan(D.make_spec(3840, 2160, fmt, LADDER4K)).ladder_v5 == 0
 
 
-def test_plan_v6_units(monkeypatch):
-    """cfg2 on v6: one work unit per (plane kind, rendition, column group) of a frame;
-    a tile whose taps span more than two 64-column K blocks keeps the graph on v5."""
+def test_plan_retired_v6_and_wide_windows(monkeypatch):
+    """DTS_LADDER=6 (the retired k_ladder6) now plans like DTS_LADDER=5; a tile whose
+    taps span more than two 64-column K blocks keeps the graph off k_ladder7."""
     monkeypatch.setenv("DTS_LADDER", "6")
-    info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
-    assert info.ladder_v5 == 2
-    # luma: 1080p 30 x 64 columns, 720p 40 x 32 (two V K blocks), 480p 27 x 32 (two H and V K blocks);
-    # chroma (U and V per unit): 1080p 30 x 32, 720p 40 x 16, 480p 27 x 16
-    assert info.njobs == 30 + 40 + 27 + 30 + 40 + 27
-    # 8K -> 480p bicubic: 36 taps, 16 outputs span 180 source columns: v5 cannot either
-    assert D.graph_plan(D.make_spec(7680, 4320, D.FMT_YUV420P, [(854, 480, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 < 2
+    assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 1
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    # 8K -> 480p bicubic: 36 taps, 16 outputs span 180 source columns
+    assert D.graph_plan(D.make_spec(7680, 4320, D.FMT_YUV420P, [(854, 480, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 < 3
 
 
 def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
@@ -171,8 +168,8 @@ def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
 
 
 def test_plan_v7_groups(monkeypatch):
-    """cfg2 on v7: the v6 units (K windows on 16-column boundaries) in strip groups of
-    at most DTS_L7_W waves; planes whose widths are not multiples of 16 stay on v6."""
+    """cfg2 on v7: the work units (K windows on 16-column boundaries) in strip groups of
+    at most DTS_L7_W waves; planes whose widths are not multiples of 16 run on v5."""
     monkeypatch.delenv("DTS_LADDER", raising=False)
     for w, ngroups in [(8, 13 + 13), (16, 7 + 7), (4, 25 + 25)]:
         monkeypatch.setenv("DTS_L7_W", str(w))
@@ -181,7 +178,7 @@ def test_plan_v7_groups(monkeypatch):
         assert info.njobs == ngroups                      # 97 luma and 97 chroma units
         assert info.lds_bytes <= 160 * 1024
     monkeypatch.delenv("DTS_L7_W", raising=False)
-    assert D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 2
+    assert D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 1
     assert D.graph_plan(D.make_spec(384, 216, D.FMT_YUV420P, [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 == 3
 
 
@@ -206,7 +203,7 @@ def test_plan_range_conversion(monkeypatch):
     monkeypatch.setenv("DTS_LADDER", "6")
     with pytest.raises(D.DtsError):
         D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1))
-    assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1, dst_range=1)).ladder_v5 == 2
+    assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1, dst_range=1)).ladder_v5 == 1
 
 
 @pytest.mark.parametrize("knob", [("DTS_L7_PB", "1"), ("DTS_L7_NS", "3"), ("DTS_L7_NS", "4")])
