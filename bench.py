@@ -250,10 +250,11 @@ def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_firs
     return True
 
 
-def load_traffic():
-    """(HBM bytes per frame, profile tag) from the newest committed rocprofv3 PMC
-    summary (tools/prof_summary.py writes profiles/pmc_latest.json), or (None, None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def load_traffic(workload):
+    """(HBM bytes per frame, profile tag) of this workload's step from its newest committed
+    rocprofv3 PMC summary (tools/prof_wl.py writes profiles/pmc_<workload>.json: FETCH_SIZE x2 +
+    WRITE_SIZE summed over the step's kernels, per frame), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None, None
     try:
@@ -566,7 +567,7 @@ def main():
         fps = frames_total / wall_max
         algo = algo_bytes
         achieved = algo * B / (kern_ms * 1e-3)
-        traffic_pf, traffic_tag = load_traffic() if args.workload == "cfg2" else (None, None)
+        traffic_pf, traffic_tag = load_traffic(args.workload)
         # PMC bytes (FETCH_SIZE + WRITE_SIZE, Infinity-Cache hits included) per launch over this run's
         # kernel time, in the unit of `achieved`
         traffic = round(traffic_pf * B / (kern_ms * 1e-3) / 1e9, 1) if traffic_pf else None

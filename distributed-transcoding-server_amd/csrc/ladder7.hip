@@ -55,7 +55,8 @@
 
 #ifndef DTS_L7_ABLATE
 #define DTS_L7_ABLATE 0     // diagnostic builds only (wrong results): 1 no group barrier, 2 no A xor,
-                            // 4 stage only the pieces left of the next strip's X0 (no halo re-reads)
+                            // 4 stage only the pieces left of the next strip's X0 (no halo re-reads),
+                            // 8 no V (no row blocks, no stores), 16 no H (no A reads, MFMAs, epilogue)
 #endif
 #ifndef DTS_L7_DEFER
 #define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
@@ -691,6 +692,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     };
     // the row blocks firing at granule qq (their window's last granule is in the ring)
     auto vfire = [&](int qq) {
+        if (DTS_L7_ABLATE & 8) return;
         while (fg == qq) {
             v4i vh[VKB], vl[VKB];
             const uint8_t *fu = fb + (uint32_t)fsu * (uint32_t)(VKB * 2048) + 16u * (uint32_t)lane;
@@ -755,7 +757,12 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 L7_STAMP(1);
             }
             v4i a[T][RKB];
-            if (P10) {
+            if (DTS_L7_ABLATE & 16) {
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int kb = 0; kb < RKB; ++kb) a[t][kb] = (v4i){0, 0, 0, 0};
+            } else if (P10) {
                 // raw sample bytes masked to (s >> 2, (s & 3) << 6) ^ 0x80 (one v_bitop3 per dword)
                 const uint8_t *st = lds7 + sq * Z.stage_bytes + (s % PB7) * Z.npieces * 1024;
 #pragma unroll
@@ -835,7 +842,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             }
 #endif
             L7_STAMP(4);
-            {
+            if (!(DTS_L7_ABLATE & 16)) {
                 v4i ah[T], al[T];
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
@@ -971,8 +978,10 @@ void k_ladder7(Ladder7Params P)
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
-    walk7<DTS_L7_ONLYVAR, RC, HS, SK>(P, G, U, S, f, wave, waves);
-    return;
+    if constexpr ((SK == 2) == ((DTS_L7_ONLYVAR & 16) != 0)) {
+        walk7<DTS_L7_ONLYVAR, RC, HS, SK>(P, G, U, S, f, wave, waves);
+        return;
+    }
 #endif
     if constexpr (SK == 2) {                // p010 sources: the 16-bit one-K-block variants
         switch (U.variant) {
