@@ -196,6 +196,7 @@ struct dts_graph {
     const Unit7 *dev_units7 = nullptr;
     const uint32_t *dev_frag7 = nullptr;
     const int32_t *dev_fire7 = nullptr;
+    const FragOp7 *dev_fsched7 = nullptr;
     int ngroups7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
@@ -523,16 +524,16 @@ int l7_waves()
 // refused (l7_knobs_ok), never planned for a kernel that would overrun its slots.
 int l7_stages()
 {
-    int ns, pb;
-    ladder7_compiled(&ns, &pb);
+    int ns, pb, dc;
+    ladder7_compiled(&ns, &pb, &dc);
     return ns;
 }
 
 // granules per k_ladder7 staging batch (see l7_stages)
 int l7_pb()
 {
-    int ns, pb;
-    ladder7_compiled(&ns, &pb);
+    int ns, pb, dc;
+    ladder7_compiled(&ns, &pb, &dc);
     return pb;
 }
 
@@ -550,11 +551,13 @@ bool l7_by_rung()
     return f ? f[0] == 'r' : false;
 }
 
-// a staging-only wave in every k_ladder7 group (DTS_L7_STAGER=1; plan groups of W - 1 units)
-bool l7_stager()
+// decoupled staging (what the linked kernel was compiled with, ladder7.hip DTS_L7_DECOUPLE): one wave
+// of every group stages every source piece and V fragment, the others never wait on vmcnt
+int l7_decouple()
 {
-    const char *f = std::getenv("DTS_L7_STAGER");
-    return f ? f[0] == '1' : false;
+    int ns, pb, dc;
+    ladder7_compiled(&ns, &pb, &dc);
+    return dc;
 }
 
 // k_ladder7 one-K-block walks with half the tiles (DTS_L7_NARROW=1)
@@ -595,7 +598,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     // k_ladder7 takes planar and nv12 sources (k_ladder5: the fallback for frames that are
     // not 16-byte aligned)
     gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
-                                                        l7_stager(), gp.p7);
+                                                        l7_decouple(), gp.p7);
     return true;
 }
 
@@ -621,7 +624,7 @@ bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
                                          s.hdr_to_sdr ? (int)DTS_FMT_P010LE : s.out[k].fmt});
         }
     }
-    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, l7_stager(), gp.p7);
+    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, l7_decouple(), gp.p7);
 }
 
 bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
@@ -1035,6 +1038,7 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     const size_t u_off = push_blob(blob, gp.p7.units);
     const size_t f_off = push_blob(blob, gp.p7.frag);
     const size_t r_off = push_blob(blob, gp.p7.fire);
+    const size_t s_off = push_blob(blob, gp.p7.fsched);
     HIPCHK(ctx, hipMalloc(&g->dev_tables7, blob.size()));
     HIPCHK(ctx, hipMemcpy(g->dev_tables7, blob.data(), blob.size(), hipMemcpyHostToDevice));
     const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables7);
@@ -1042,6 +1046,7 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_units7 = reinterpret_cast<const Unit7 *>(base + u_off);
     g->dev_frag7 = reinterpret_cast<const uint32_t *>(base + f_off);
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
+    g->dev_fsched7 = gp.p7.fsched.empty() ? nullptr : reinterpret_cast<const FragOp7 *>(base + s_off);
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
     g->waves7 = gp.p7.waves;
@@ -1426,6 +1431,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.units = g->dev_units7;
             q.frag = g->dev_frag7;
             q.fire = g->dev_fire7;
+            q.fsched = g->dev_fsched7;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
             HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),

@@ -329,6 +329,19 @@ struct Group7 {                     // one workgroup's strip of one frame
     int32_t bpc;                    // staged bytes per source column: 1 (8-bit planes; chroma: U and V
                                     // planes), 2 (nv12 chroma: U V byte pairs; p010 luma), 4 (p010
                                     // chroma: U V 16-bit pairs); bpc npc pieces per plane and granule
+    int32_t fs0, nfs;               // decoupled groups: the staging wave's V fragment DMAs (FragOp7)
+    int32_t st0;                    // first staging wave: waves st0.. deal the source pieces (and, decoupled,
+                                    // wave st0 issues the FragOp7 schedule); the waves before issue no loads
+    int32_t pad_;
+};
+
+// Decoupled staging (ladder7.hip DTS_L7_DECOUPLE): one V fragment DMA of a group, issued by
+// its staging wave with the source pieces of staging batch `batch`, in batch order
+struct FragOp7 {
+    int32_t batch;
+    uint32_t pair;                  // fragment pair (2 KB: hi 1 KB, lo 1 KB; VKB pairs per row block)
+    int32_t lds;                    // LDS destination (the rendition's slot of this row block)
+    int32_t n1k;                    // 1-KB DMAs (2 VKB)
 };
 
 struct Ladder7Params {
@@ -339,11 +352,12 @@ struct Ladder7Params {
     const Unit7 *units;
     const uint32_t *frag;           // as Ladder6Params
     const int32_t *fire;
+    const FragOp7 *fsched;          // decoupled groups' fragment DMA schedules (Group7::fs0 / nfs)
 };
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
                           int src_kind, hipStream_t s);   // src_kind: SrcKind
-void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
+void ladder7_compiled(int *stages, int *batch, int *decouple);   // NS7 / PB7 / DTS_L7_DECOUPLE of the linked k_ladder7
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

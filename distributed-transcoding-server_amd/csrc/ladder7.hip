@@ -56,7 +56,10 @@
 #ifndef DTS_L7_ABLATE
 #define DTS_L7_ABLATE 0     // diagnostic builds only (wrong results): 1 no group barrier, 2 no A xor,
                             // 4 stage only the pieces left of the next strip's X0 (no halo re-reads),
-                            // 8 no V (no row blocks, no stores), 16 no H (no A reads, MFMAs, epilogue)
+                            // 8 no V (no row blocks, no stores), 16 no H (no A reads, MFMAs, epilogue),
+                            // 32 V without its global stores, 64 V without exchange and stores,
+                            // 128 V without its MFMAs (the ring's dwords exchanged and stored),
+                            // 256 no V fragment DMAs, 512 every row block stored to its plane's row 0
 #endif
 #ifndef DTS_L7_DEFER
 #define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
@@ -78,6 +81,14 @@
 #endif
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
+#endif
+#ifndef DTS_L7_DECOUPLE
+#define DTS_L7_DECOUPLE 0   // who issues the group's loads (Group7::st0; plan7_graph): 0 every wave deals the
+                            // source pieces (a group's spare waves, if any, stage them all) and the first
+                            // wave of each rendition DMAs its V fragments; 1 a staging-only wave per group
+                            // issues every piece and fragment (FragOp7 schedule); 2 the lighter half of the
+                            // unit waves (or the spare waves) issue them, so the heavy waves, which set the
+                            // group's pace at every barrier, issue no loads and never wait on vmcnt
 #endif
 
 namespace dts {
@@ -184,10 +195,9 @@ struct Stage7 {
         ppp = bpc * npc;
         npieces = np * ppp;
         nown = min(ppp, ((G.xown - G.X0) * bpc + 63) >> 6);
-        // the waves beyond the group's units (if any) stage every piece; else all deal them
-        const int stagers = waves - G.nwaves;
-        w = stagers > 0 ? (wave >= G.nwaves ? wave - G.nwaves : npieces) : wave;
-        nw = stagers > 0 ? stagers : waves;
+        // the staging waves st0.. deal the pieces (Group7::st0)
+        w = wave >= G.st0 ? wave - G.st0 : npieces;
+        nw = waves - G.st0;
         srcH1 = G.srcH - 1;
         ngran = G.ngran;
         stage_bytes = PB7 * npieces * 1024;
@@ -346,7 +356,7 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
                                        const uint32_t (&op)[2], int lane)
 {
     using W = Walk6<VAR>;
-    const int y = 16 * j + (lane >> 2), q4 = lane & 3;
+    const int y = (DTS_L7_ABLATE & 512) ? 0 : 16 * j + (lane >> 2), q4 = lane & 3;
     if (y < U.dstH) {
         if (W::CT == 1 && U.fmt == DTS_FMT_P010LE) {        // p010 renditions (xchg7p)
             if (W::NP == 1) {
@@ -480,9 +490,11 @@ __device__ __forceinline__ void vcalc7p(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<V
     }
 }
 
-// a wave with no unit: stage its pieces, keep the group's barrier count
+// a wave with no unit: stage its pieces (decoupled groups: the first such wave also DMAs every
+// V fragment of the group, FragOp7 schedule in batch order), keep the group's barrier count
 template <int SK>
-__device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
+__device__ __forceinline__ void idle7(const Ladder7Params &P, const Group7 &G, const DevPlanes &S, int f, int wave,
+                                      int waves)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
 #ifdef DTS_L7_STAGER_PRIO
@@ -490,8 +502,27 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
 #endif
     Stage7 Z;
     Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63, SK == 0 ? 1 : G.bpc);
+    const int lane = (int)threadIdx.x & 63;
+    // the fragment DMAs of batch bn (the first staging wave of a decoupled group)
+    const bool fw = DTS_L7_DECOUPLE && wave == G.st0;
+    const FragOp7 *fs = P.fsched + G.fs0, *fe = fs + (fw ? G.nfs : 0);
+    const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
+    auto frags = [&](int bn) {
+        for (; fs < fe; ++fs) {
+            const FragOp7 op = kld6(fs);
+            if (op.batch > bn) break;
+            if (DTS_L7_ABLATE & 256) continue;
+            const uint64_t src = fr + (uint64_t)op.pair * 2048u;
+            for (int h = 0; h < op.n1k; ++h)
+                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
+                                                 (__attribute__((address_space(3))) void *)(lds7 + op.lds + 1024 * h),
+                                                 16, 0, 0);
+            Z.ops += op.n1k;
+        }
+    };
 #pragma unroll
     for (int i = 0; i < NS7 - 1; ++i) {
+        frags(i);
         Z.pieces(lds7, i, i);
         Z.e[i] = Z.ops;
     }
@@ -504,6 +535,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
         group_barrier7();
         L7_STAMP(1);
         const int sn = sq == 0 ? NS7 - 1 : sq - 1;
+        frags(b + NS7 - 1);
         Z.pieces(lds7, b + NS7 - 1, sn);
         Z.shift();
         sq = sq + 1 == NS7 ? 0 : sq + 1;
@@ -663,15 +695,38 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     const int FS = U.fs;
     int fsi = 0, fsu = 0;
     // the V fragments of the row blocks firing at granule <= upto (lead wave only)
+    // decoupled groups: staging waves (wave >= G.st0) issue the pieces, wave st0 the fragment
+    // schedule of the batch (FragOp7, as idle7); the other waves issue no loads and never wait
+    const bool stg = DTS_L7_DECOUPLE == 0 || (DTS_L7_DECOUPLE == 2 && wave >= G.st0);
+    const FragOp7 *fsp = P.fsched + G.fs0, *fse = fsp + (DTS_L7_DECOUPLE && wave == G.st0 ? G.nfs : 0);
+    auto fsched = [&](int bn) {
+        for (; fsp < fse; ++fsp) {
+            const FragOp7 op = kld6(fsp);
+            if (op.batch > bn) break;
+            if (DTS_L7_ABLATE & 256) continue;
+            const uint64_t src = fr + (uint64_t)op.pair * 2048u;
+            for (int h = 0; h < op.n1k; ++h)
+                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
+                                                 (__attribute__((address_space(3))) void *)(lds7 + op.lds + 1024 * h),
+                                                 16, 0, 0);
+            Z.ops += op.n1k;
+        }
+    };
     auto frags = [&](int upto) {
+        if (DTS_L7_DECOUPLE) {                          // the staging wave st0's schedule (batch upto / PB7)
+            fsched(upto / PB7);
+            return;
+        }
         while (fgf <= upto) {
-            Z.ops += 2 * VKB;
             uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
             const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
+            if (!(DTS_L7_ABLATE & 256)) {
+                Z.ops += 2 * VKB;
 #pragma unroll
-            for (int h = 0; h < 2 * VKB; ++h)
-                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
-                                                 (__attribute__((address_space(3))) void *)(dst + 1024 * h), 16, 0, 0);
+                for (int h = 0; h < 2 * VKB; ++h)
+                    __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
+                                                     (__attribute__((address_space(3))) void *)(dst + 1024 * h), 16, 0, 0);
+            }
             fsi = fsi + 1 == FS ? 0 : fsi + 1;
             ++jf;
             fgf = fgf1;
@@ -714,11 +769,21 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             }
             if (!p010out) {
                 uint32_t w[T];
-                vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
+                if (DTS_L7_ABLATE & 128) {
+#pragma unroll
+                    for (int t = 0; t < T; ++t) w[t] = (uint32_t)(rh[0][t][0] ^ vh[0][t & 3]);
+                } else {
+                    vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
+                }
                 flush();
-                xchg7<VAR>(U, w, scr, m, g, lane, px);
+                if (DTS_L7_ABLATE & 64) {
+#pragma unroll
+                    for (int t = 0; t < T; ++t) asm volatile("" ::"v"(w[t]));
+                } else {
+                    xchg7<VAR>(U, w, scr, m, g, lane, px);
+                }
             }
-            pj = j;
+            pj = (DTS_L7_ABLATE & 96) ? -1 : j;
             if (!DEFER_ST) flush();
             ++j;
             fg = fg1;
@@ -726,7 +791,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         }
     };
 #pragma unroll
-    for (int i = 0; i < NS7 - 1; ++i) {
+    for (int i = 0; i < NS7 - 1 && stg; ++i) {
         frags(PB7 * i + PB7 - 1);
         Z.pieces(lds7, i, i);
         Z.e[i] = Z.ops;
@@ -751,7 +816,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             const int q = q0 + s;
             if (q >= ngran) break;
             if (s % PB7 == 0) {
-                Z.wait_batch();
+                if (stg) Z.wait_batch();
                 L7_STAMP(0);
                 group_barrier7();
                 L7_STAMP(1);
@@ -824,7 +889,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             // deferred row blocks (1: the 16 waves of a CU then do not all queue their DMAs
             // on the memory pipe at the moment they leave the barrier)
 #if DTS_L7_DMAPOS == 0
-            if (s % PB7 == 0) {
+            if (s % PB7 == 0 && stg) {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
                 frags(PB7 * bn + PB7 - 1);
                 Z.pieces(lds7, bn, sn);
@@ -834,7 +899,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             L7_STAMP(2);
             if (DTS_L7_DEFER) vfire(q - 1);
 #if DTS_L7_DMAPOS == 1
-            if (s % PB7 == 0) {
+            if (s % PB7 == 0 && stg) {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
                 frags(PB7 * bn + PB7 - 1);
                 Z.pieces(lds7, bn, sn);
@@ -973,7 +1038,7 @@ void k_ladder7(Ladder7Params P)
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
     if (wave >= G.nwaves) {
-        idle7<SK>(G, S, f, wave, waves);
+        idle7<SK>(P, G, S, f, wave, waves);
         return;
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
@@ -1021,10 +1086,11 @@ int ladder7_stamps(unsigned long long *out, bool reset)
 
 // the staging geometry this build of k_ladder7 was compiled with: the planner sizes the
 // stage buffers and the V fragment slots for exactly these, and refuses any other
-void ladder7_compiled(int *stages, int *batch)
+void ladder7_compiled(int *stages, int *batch, int *decouple)
 {
     *stages = NS7;
     *batch = PB7;
+    *decouple = DTS_L7_DECOUPLE;
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,

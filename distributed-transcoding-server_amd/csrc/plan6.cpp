@@ -327,10 +327,12 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, bool stager,
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, int decouple,
                  Plan7 &out)
 {
     out = Plan7{};
+    const int wtotal = wmax;
+    if (decouple == 1) --wmax;                             // one wave of every group only stages
     // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
     // granules (the batches in flight + the one-granule V deferral; ladder7.hip)
     if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages > 4 || pb < 1 || pb > 2) return false;
@@ -531,9 +533,36 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     if (std::getenv("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
         for (const Group7 &g : out.groups)
             std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d\n", g.kind, g.X0, g.npc, g.nwaves);
+    // decoupled groups: the staging wave's V fragment DMAs, row block by row block of every
+    // rendition, each with the source pieces of the batch holding its fire granule (the batch
+    // a rendition's lead wave would issue it with: ladder7.hip walk7 frags())
+    if (decouple)
+        for (Group7 &g : out.groups) {
+            g.fs0 = (int)out.fsched.size();
+            for (int i = g.u0; i < g.u0 + g.nwaves; ++i) {
+                const Unit7 &v = out.units[(size_t)i];
+                if (!v.lead) continue;
+                const int vkb = l6_vkb(v.variant);
+                for (int j = 0; j < v.nrb; ++j) {
+                    FragOp7 op{};
+                    op.batch = out.fire[(size_t)v.fire + j] / pb;
+                    op.pair = v.vfrag + (uint32_t)(j * vkb);
+                    op.lds = v.flds + (j % v.fs) * vkb * 2048;
+                    op.n1k = 2 * vkb;
+                    out.fsched.push_back(op);
+                }
+            }
+            std::stable_sort(out.fsched.begin() + g.fs0, out.fsched.end(),
+                             [](const FragOp7 &a, const FragOp7 &b) { return a.batch < b.batch; });
+            g.nfs = (int)out.fsched.size() - g.fs0;
+        }
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
-    if (stager) ++out.waves;                               // one staging-only wave in every group
+    if (decouple == 1) out.waves = std::max(out.waves + 1, std::min(wtotal, kL7MaxWaves));
+    // the staging waves: a group's spare waves; else all its waves (0) or its lighter half (2: the
+    // planner put the heaviest units first)
+    for (Group7 &g : out.groups)
+        g.st0 = g.nwaves < out.waves ? g.nwaves : (decouple == 2 ? g.nwaves / 2 : 0);
     for (const Group7 &g : out.groups) out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
     return out.lds_bytes <= 160 * 1024;
 }

@@ -29,8 +29,8 @@ dst = os.path.join(root, "profiles")
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "").replace("dts::", "").replace("(anonymous namespace)::", "")
-    return n
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "").replace("dts::", "")
+    return n.split("(")[0]
 
 
 def step_rows(rows):

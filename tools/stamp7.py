@@ -16,11 +16,12 @@ import dtsffi as D  # noqa: E402
 
 lib = D.lib()
 lib.dts_debug_ladder7_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 136)()
+NV = 33                                 # kL7Variants + 1 rows (the last: staging-only waves)
+buf = (ctypes.c_ulonglong * (8 * NV))()
 bench.main()
 lib.dts_debug_ladder7_stamps(buf, 0)
 names = ["vm wait", "barrier", "dma issue", "H", "V", "tail"]
-for v in range(17):
+for v in range(NV):
     row = buf[8 * v: 8 * v + 8]
     gran, waves = row[6], row[7]
     if not waves:
