@@ -430,7 +430,11 @@ def main():
     rungq = bool(wl.get("rung_quality"))
     yadif = wl.get("yadif")
     if yadif is None:
-        g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, wl["outs"], quality=D.Q_BOTH if wl["quality"] else D.Q_NONE,
+        # cfg5: every rendition scored against its reference batch (DTS_QREF_EXTERNAL), in the graph:
+        # vf_psnr / vf_ssim fused into the ladder kernel's V epilogue
+        gouts = [(w, h, fmt, m, None, (D.Q_BOTH, D.QREF_EXTERNAL)) if rungq else (w, h, fmt, m)
+                 for (w, h, fmt, m) in wl["outs"]]
+        g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, gouts, quality=D.Q_BOTH if wl["quality"] else D.Q_NONE,
                                      max_batch=B, tonemap=wl["tonemap"]))
         algo_bytes = g.info.algo_bytes_per_frame
         if rungq:                          # + each rendition's reference read once
@@ -466,11 +470,13 @@ def main():
     if rungq:
         ref_outs = [(w, h, fmt, D.SCALE_LANCZOS) for (w, h, fmt, _m) in wl["outs"]]
         qg = D.Graph(ctx, D.make_spec(sw, sh, sfmt, ref_outs, max_batch=B))
-        for (w, h, fmt, _m) in wl["outs"]:
+        # the graph's records: rendition k's frame f at row k * B + f
+        qall = torch.zeros((len(wl["outs"]) * B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev)
+        for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
             t = torch.empty((R, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
             d, _ = dev_batch(t, w, h, fmt)
             qrefs.append((t, d))
-            qraws.append(torch.zeros((B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev))
+            qraws.append(qall[k * B:(k + 1) * B])
         for i0 in range(0, R, B):
             sdi = D.DevFrames()
             for p in range(3):
@@ -512,11 +518,13 @@ def main():
         if g is None:                      # prev/next of the batch's frames come from the same ring
             ctx.yadif_device(sw, sh, yadif, 1, sd, R, (i * B) % R, B, ods[0], sptr)
             return
-        g.run_device(batch_src(i), B, ods, qref=qrd, qraw_ptr=qraw.data_ptr() if qraw is not None else 0,
-                     stream=sptr)
-        if rungq:                          # every rendition vs its reference, then the segment's record
-            for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
-                ctx.quality_device(w, h, fmt, ods[k], qref_batch(k, i), B, qraws[k].data_ptr(), sptr)
+        if rungq:                          # the ladder with every rendition scored against its reference
+            g.run_device(batch_src(i), B, ods, qref=[qref_batch(k, i) for k in range(len(ods))],
+                         qraw_ptr=qall.data_ptr(), stream=sptr)
+        else:
+            g.run_device(batch_src(i), B, ods, qref=qrd, qraw_ptr=qraw.data_ptr() if qraw is not None else 0,
+                         stream=sptr)
+        if rungq:
             # the segment's record (computed in warmup too, so torch's reduction kernels are
             # loaded before the timed region)
             sse = torch.stack([q.view(torch.int64)[:, :3].sum(0) for q in qraws])

@@ -198,6 +198,11 @@ struct dts_graph {
     const int32_t *dev_fire7 = nullptr;
     const FragOp7 *dev_fsched7 = nullptr;
     int ngroups7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
+    // fused quality (GraphPlan::qf): the per (rendition, plane) unit lists and boundaries
+    bool qf7 = false;
+    const QRend7 *dev_qrend7 = nullptr;
+    const int32_t *dev_qunit7 = nullptr, *dev_qbound7 = nullptr;
+    int nqrend7 = 0, nunits7 = 0, nqbound7 = 0, qmax_h4 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -448,6 +453,7 @@ struct GraphPlan {
     std::vector<Job5> jobs5;
     int lds5 = 0;
     bool v7 = false;                      // ... and on k_ladder7 where frames are 16-byte aligned
+    bool qf = false;                      // ... with vf_psnr / vf_ssim fused into it (Unit7::qual)
     Plan7 p7;
     dts_graph_info info{};
 };
@@ -471,7 +477,7 @@ int validate_spec(const dts_graph_spec &s)
         const dts_output_spec &o = s.out[k];
         if (o.quality < 0 || o.quality > DTS_Q_BOTH) return DTS_E_INVAL;
         if (!o.quality) continue;
-        if (!method_ok(o.qref_method)) return DTS_E_UNSUPPORTED;
+        if (o.qref_method != DTS_QREF_EXTERNAL && !method_ok(o.qref_method)) return DTS_E_UNSUPPORTED;
         if (s.quality || s.hdr_to_sdr || !fmt_8bit(o.fmt)) return DTS_E_UNSUPPORTED;
     }
     if (s.quality && !fmt_8bit(s.out[s.quality_out].fmt)) return DTS_E_UNSUPPORTED;   // vf_psnr/vf_ssim: 8-bit
@@ -567,6 +573,19 @@ bool l7_narrow()
     return f ? f[0] == '1' : false;
 }
 
+// vf_psnr / vf_ssim of output k: the graph's quality output or a rendition with quality
+bool wants_quality(const dts_graph_spec &s, int k)
+{
+    return (s.quality && k == s.quality_out) || s.out[k].quality;
+}
+
+// quality fused into k_ladder7's V epilogue (DTS_QFUSE=1; else the separate k_quality pass)
+bool qfuse_enabled()
+{
+    const char *f = std::getenv("DTS_QFUSE");
+    return f && f[0] == '1';
+}
+
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
 // and k_ladder7 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
@@ -583,7 +602,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
         if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         for (int k = 0; k < s.nout; ++k) {
             const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
-            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
+            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt, false});
         }
         if (!plan5_kind(in, gp.p5[kind])) return false;
     }
@@ -597,8 +616,21 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.v5 = true;
     // k_ladder7 takes planar and nv12 sources (k_ladder5: the fallback for frames that are
     // not 16-byte aligned)
-    gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
-                                                        l7_decouple(), gp.p7);
+    gp.v7 = false;
+    if (v7_enabled() && qfuse_enabled()) {        // quality fused into the V epilogue where asked for
+        Plan5In iq[2] = {ins[0], ins[1]};
+        bool any = false;
+        for (int kind = 0; kind < 2; ++kind)
+            for (int k = 0; k < s.nout; ++k) {
+                iq[kind].rungs[(size_t)k].qual = wants_quality(s, k);
+                any = any || iq[kind].rungs[(size_t)k].qual;
+            }
+        gp.qf = gp.v7 = any && plan7_graph(iq, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
+                                           l7_decouple(), gp.p7);
+    }
+    if (!gp.v7)
+        gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
+                                            l7_decouple(), gp.p7);
     return true;
 }
 
@@ -1039,6 +1071,9 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     const size_t f_off = push_blob(blob, gp.p7.frag);
     const size_t r_off = push_blob(blob, gp.p7.fire);
     const size_t s_off = push_blob(blob, gp.p7.fsched);
+    const size_t qr_off = push_blob(blob, gp.p7.qrend);
+    const size_t qu_off = push_blob(blob, gp.p7.qunit);
+    const size_t qb_off = push_blob(blob, gp.p7.qbound);
     HIPCHK(ctx, hipMalloc(&g->dev_tables7, blob.size()));
     HIPCHK(ctx, hipMemcpy(g->dev_tables7, blob.data(), blob.size(), hipMemcpyHostToDevice));
     const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables7);
@@ -1047,6 +1082,14 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_frag7 = reinterpret_cast<const uint32_t *>(base + f_off);
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
     g->dev_fsched7 = gp.p7.fsched.empty() ? nullptr : reinterpret_cast<const FragOp7 *>(base + s_off);
+    g->qf7 = gp.qf;
+    g->dev_qrend7 = reinterpret_cast<const QRend7 *>(base + qr_off);
+    g->dev_qunit7 = reinterpret_cast<const int32_t *>(base + qu_off);
+    g->dev_qbound7 = reinterpret_cast<const int32_t *>(base + qb_off);
+    g->nqrend7 = (int)gp.p7.qrend.size();
+    g->nunits7 = (int)gp.p7.units.size();
+    g->nqbound7 = (int)gp.p7.qbound.size() / 2;
+    for (const QRend7 &q : gp.p7.qrend) g->qmax_h4 = std::max(g->qmax_h4, q.h >> 2);
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
     g->waves7 = gp.p7.waves;
@@ -1148,7 +1191,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         rs.deint = 0;
         rs.max_batch = g->batch;
         for (int k = 0; k < s.nout; ++k)
-            if (s.out[k].quality) {
+            if (s.out[k].quality && s.out[k].qref_method != DTS_QREF_EXTERNAL) {
                 dts_output_spec &o = rs.out[rs.nout];
                 o = s.out[k];
                 o.method = s.out[k].qref_method;
@@ -1487,6 +1530,73 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     return DTS_OK;
 }
 
+// The ladder with vf_psnr / vf_ssim fused into k_ladder7 (GraphPlan::qf): per chunk of at most
+// g->batch frames one k_ladder7<QF> launch (each quality unit scores its row blocks against
+// qref[k] in its V epilogue), k_qfix7 (the windows straddling two units) and k_qfin7 (per
+// frame and rendition, out_q[k * qstride + f]).  DTS_E_UNSUPPORTED when a batch cannot run on
+// k_ladder7 (planes not 16 / 4-byte aligned): the caller then takes the separate pass.
+static int enqueue_ladder_q(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, int nframes,
+                            const DevPlanes *qref, dts_qraw *out_q, int64_t qstride, hipStream_t st)
+{
+    const dts_graph_spec &s = g->spec;
+    dts_ctx *ctx = g->ctx;
+    if (!g->qf7 || !planes_aligned7(src)) return DTS_E_UNSUPPORTED;
+    for (int k = 0; k < s.nout; ++k)
+        if (!planes_aligned4(dst[k]) || (qref[k].data[0] && !planes_aligned4(qref[k]))) return DTS_E_UNSUPPORTED;
+    const int B = g->batch, nsp = qfuse7_spans(g->qmax_h4);
+    const size_t part = (size_t)B * g->nunits7 * sizeof(QPart7);
+    const size_t need = part + (size_t)B * std::max(g->nqbound7, 1) * nsp * sizeof(double);
+    int e = ensure_qscratch(ctx, qs, need);
+    if (e) return e;
+    for (int f0 = 0; f0 < nframes; f0 += B) {
+        const int n = std::min(B, nframes - f0);
+        HIPCHK(ctx, hipStreamWaitEvent(st, qs.ev, 0));         // the previous user of the partials
+        Ladder7Params q{};
+        q.src = src;
+        for (int pl = 0; pl < 3; ++pl) q.src.data[pl] += (uint64_t)((int64_t)f0 * src.fstride);
+        QFinParams fp{};
+        for (int k = 0; k < kMaxRungs; ++k) {
+            const int kk = k < s.nout ? k : 0;
+            q.dst[k] = dst[kk];
+            for (int pl = 0; pl < 3; ++pl) q.dst[k].data[pl] += (uint64_t)((int64_t)f0 * dst[kk].fstride);
+            if (k < s.nout && qref[k].data[0]) {
+                q.qref[k] = qref[k];
+                for (int pl = 0; pl < 3; ++pl)
+                    if (q.qref[k].data[pl]) q.qref[k].data[pl] += (uint64_t)((int64_t)f0 * qref[k].fstride);
+            }
+            fp.out[k] = q.dst[k];
+            fp.ref[k] = q.qref[k];
+            fp.fmt[k] = k < s.nout ? s.out[k].fmt : 0;
+        }
+        q.ngroups = g->ngroups7;
+        q.nframes = n;
+        q.groups = g->dev_groups7;
+        q.units = g->dev_units7;
+        q.frag = g->dev_frag7;
+        q.fire = g->dev_fire7;
+        q.fsched = g->dev_fsched7;
+        q.qpart = static_cast<QPart7 *>(qs.p);
+        q.nunits = g->nunits7;
+        const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
+        if (grid > INT32_MAX) return DTS_E_RANGE;
+        HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, false, g->hsplit7, g->src_kind, st, true));
+        fp.rend = g->dev_qrend7;
+        fp.qunit = g->dev_qunit7;
+        fp.qbound = g->dev_qbound7;
+        fp.qpart = q.qpart;
+        fp.fixp = reinterpret_cast<double *>(static_cast<uint8_t *>(qs.p) + part);
+        fp.out_q = out_q + f0;
+        fp.nrend = g->nqrend7;
+        fp.nunits = g->nunits7;
+        fp.nbound = g->nqbound7;
+        fp.nframes = n;
+        fp.qstride = qstride;
+        HIPCHK(ctx, launch_qfuse7(fp, s.nout, g->qmax_h4, st));
+        HIPCHK(ctx, hipEventRecord(qs.ev, st));
+    }
+    return DTS_OK;
+}
+
 // HDR10 -> SDR: per chunk of hdr_chunk frames, the bit-exact ladder into a p010
 // intermediate (two, alternating), then k_tonemap from it into the caller's output.  The
 // tonemaps run on the graph's second stream: the ladder of chunk i + 1 overlaps the
@@ -1554,54 +1664,78 @@ static int ensure_rscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
     return DTS_OK;
 }
 
-// Rendition quality of frames f0 .. f0 + n - 1 of a call over `ntot` frames: per batch
-// the reference graph scales the same source frames (src, already deinterlaced) into a
-// scratch batch, then k_quality scores each rendition that asked for it against its
-// reference; records go to qraw[k * ntot + f] (vf_psnr / vf_ssim per frame, exactly as
-// the dts_quality_run_device path).
-static int rung_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, int f0, int n,
-                        int ntot, dts_qraw *qraw, hipStream_t st)
+// The ladder of frames c0 .. c0 + m - 1 of a call over ntot frames (src / dst already at
+// frame c0) and its quality: graph quality (qref = the quality_out reference batch, records
+// qraw[c0 + f]), rendition quality against references the graph makes (g->ref, into scratch)
+// or that come with the call (DTS_QREF_EXTERNAL: qref = nout batches), records
+// qraw[k * ntot + c0 + f].  Fused into k_ladder7 where the graph planned it, else the separate
+// k_quality pass.  m <= g->batch when the graph makes references.
+static int ladder_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, const int *dfmt,
+                          int c0, int m, int ntot, const dts_dev_frames *qref, dts_qraw *qraw, hipStream_t st)
 {
-    dts_ctx *ctx = g->ctx;
     const dts_graph_spec &s = g->spec;
-    dts_graph *r = g->ref;
-    const int B = g->batch;
-    size_t off[DTS_MAX_OUTPUTS], total = 0;
-    for (int j = 0; j < g->nrq; ++j) {
-        off[j] = total;
-        total += (size_t)B * (size_t)r->lay_out[j].fstride;
+    dts_ctx *ctx = g->ctx;
+    const bool gq = s.quality && qref && qraw;
+    bool ext = false, rq = g->ref && qraw;
+    for (int k = 0; k < s.nout; ++k) ext = ext || (s.out[k].quality && s.out[k].qref_method == DTS_QREF_EXTERNAL);
+    ext = ext && qref && qraw;
+    if (!gq && !ext && !rq) return g->hdr ? enqueue_hdr(g, src, dst, m, st) : enqueue_ladder(g, src, dst, dfmt, m, st);
+    DevPlanes qr[kMaxRungs] = {};
+    dts_qraw *out_q = qraw + c0;
+    int64_t qstride = ntot;
+    auto at_c0 = [&](const dts_dev_frames &d, int fmt) {
+        DevPlanes r = to_dev(d, fmt);
+        for (int pl = 0; pl < 3; ++pl)
+            if (r.data[pl]) r.data[pl] += (uint64_t)((int64_t)c0 * d.frame_stride);
+        return r;
+    };
+    if (gq) {
+        qr[s.quality_out] = at_c0(*qref, s.out[s.quality_out].fmt);
+        qstride = 0;
     }
-    int e = ensure_rscratch(ctx, qs, total);
-    if (e) return e;
-    for (int c0 = 0; c0 < n; c0 += B) {
-        const int m = std::min(B, n - c0);
-        HIPCHK(ctx, hipStreamWaitEvent(st, qs.rev, 0));   // the buffer's previous user
-        DevPlanes sc = src, rd[DTS_MAX_OUTPUTS];
+    if (ext)
+        for (int k = 0; k < s.nout; ++k)
+            if (s.out[k].quality && s.out[k].qref_method == DTS_QREF_EXTERNAL) qr[k] = at_c0(qref[k], s.out[k].fmt);
+    if (rq) {                                    // the reference renditions of these frames, into scratch
+        dts_graph *r = g->ref;
+        size_t off[DTS_MAX_OUTPUTS], total = 0;
+        for (int j = 0; j < g->nrq; ++j) {
+            off[j] = total;
+            total += (size_t)g->batch * (size_t)r->lay_out[j].fstride;
+        }
+        int e = ensure_rscratch(ctx, qs, total);
+        if (e) return e;
+        HIPCHK(ctx, hipStreamWaitEvent(st, qs.rev, 0));        // the buffer's previous user
+        DevPlanes rd[DTS_MAX_OUTPUTS];
         int rf[DTS_MAX_OUTPUTS];
-        for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src.fstride);
         for (int j = 0; j < g->nrq; ++j) {
             rd[j] = r->lay_out[j].planes(static_cast<uint8_t *>(qs.rp) + off[j]);
             rf[j] = r->spec.out[j].fmt;
+            qr[g->rq_out[j]] = rd[j];
         }
-        e = enqueue_ladder(r, sc, rd, rf, m, st);
+        e = enqueue_ladder(r, src, rd, rf, m, st);
         if (e) return e;
-        for (int j = 0; j < g->nrq; ++j) {
-            const int k = g->rq_out[j];
+    }
+    int e = g->hdr ? DTS_E_UNSUPPORTED : enqueue_ladder_q(g, qs, src, dst, m, qr, out_q, qstride, st);
+    if (e == DTS_E_UNSUPPORTED) {                // the separate pass: the ladder, then k_quality per output
+        e = g->hdr ? enqueue_hdr(g, src, dst, m, st) : enqueue_ladder(g, src, dst, dfmt, m, st);
+        for (int k = 0; k < s.nout && !e; ++k) {
+            if (!qr[k].data[0]) continue;
             const dts_output_spec &o = s.out[k];
-            dts_dev_frames a{}, b = dev_frames(static_cast<uint8_t *>(qs.rp) + off[j], r->lay_out[j]);
+            dts_dev_frames a{}, b{};
             for (int pl = 0; pl < 3; ++pl) {
-                a.data[pl] = dst[k].data[pl] ? reinterpret_cast<void *>(dst[k].data[pl] +
-                                                                        (uint64_t)((int64_t)(c0 + 0) * dst[k].fstride))
-                                             : nullptr;
+                a.data[pl] = dst[k].data[pl] ? reinterpret_cast<void *>(dst[k].data[pl]) : nullptr;
                 a.pitch[pl] = dst[k].pitch[pl];
+                b.data[pl] = qr[k].data[pl] ? reinterpret_cast<void *>(qr[k].data[pl]) : nullptr;
+                b.pitch[pl] = qr[k].pitch[pl];
             }
             a.frame_stride = dst[k].fstride;
-            e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, m, qraw + (int64_t)k * ntot + f0 + c0, st);
-            if (e) return e;
+            b.frame_stride = qr[k].fstride;
+            e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, m, out_q + (int64_t)k * qstride, st);
         }
-        HIPCHK(ctx, hipEventRecord(qs.rev, st));
     }
-    return DTS_OK;
+    if (!e && rq) HIPCHK(ctx, hipEventRecord(qs.rev, st));
+    return e;
 }
 
 static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int nframes, const dts_dev_frames *dst,
@@ -1614,9 +1748,13 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
     for (int k = 0; k < s.nout; ++k)
         if (!planes_ok(dst[k], s.out[k].w, s.out[k].h, s.out[k].fmt, 4)) return DTS_E_INVAL;
     if (s.src_fmt == DTS_FMT_YUV420P && src->pitch[1] != src->pitch[2]) return DTS_E_INVAL;
-    const bool want_q = s.quality && qref && qraw_dev;
-    if (want_q && !planes_ok(*qref, s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, 4))
+    if (s.quality && qref && qraw_dev &&
+        !planes_ok(*qref, s.out[s.quality_out].w, s.out[s.quality_out].h, s.out[s.quality_out].fmt, 4))
         return DTS_E_INVAL;
+    for (int k = 0; k < s.nout && qref && qraw_dev; ++k)       // external reference renditions
+        if (s.out[k].quality && s.out[k].qref_method == DTS_QREF_EXTERNAL &&
+            !planes_ok(qref[k], s.out[k].w, s.out[k].h, s.out[k].fmt, 4))
+            return DTS_E_INVAL;
     dts_ctx *ctx = g->ctx;
     hipSetDevice(ctx->device);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream[0];
@@ -1627,10 +1765,16 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
         ddst[k] = to_dev(dst[k], s.out[k].fmt);
         dfmt[k] = s.out[k].fmt;
     }
+    auto dst_at = [&](int c0, DevPlanes *dd) {
+        for (int k = 0; k < s.nout; ++k) {
+            dd[k] = ddst[k];
+            for (int pl = 0; pl < 3; ++pl) dd[k].data[pl] += (uint64_t)((int64_t)c0 * dst[k].frame_stride);
+        }
+    };
+    const int B = g->batch;
     if (s.deint) {
         // yadif into a batch of deinterlaced frames, then the ladder (and quality) from it;
         // src holds nframes + 2 frames (one context frame each side)
-        const int B = g->batch;
         int e = ensure_dscratch(ctx, qs, (size_t)B * g->lay_src.fstride);
         if (e) return e;
         const dts_dev_frames dbuf = dev_frames(static_cast<uint8_t *>(qs.dp), g->lay_src);
@@ -1640,40 +1784,23 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
             e = yadif_enqueue(ctx, s.src_w, s.src_h, s.deint_mode, s.deint_tff, *src, nframes + 2, 1 + c0, m, dbuf, st);
             if (e) return e;
             DevPlanes dd[DTS_MAX_OUTPUTS];
-            for (int k = 0; k < s.nout; ++k) {
-                dd[k] = ddst[k];
-                for (int pl = 0; pl < 3; ++pl) dd[k].data[pl] += (uint64_t)((int64_t)c0 * dst[k].frame_stride);
-            }
-            e = enqueue_ladder(g, to_dev(dbuf, s.src_fmt), dd, dfmt, m, st);
+            dst_at(c0, dd);
+            e = ladder_quality(g, qs, to_dev(dbuf, s.src_fmt), dd, dfmt, c0, m, nframes, qref, qraw_dev, st);
             if (e) return e;
-            if (g->ref && qraw_dev) {
-                e = rung_quality(g, qs, to_dev(dbuf, s.src_fmt), dd, c0, m, nframes, qraw_dev, st);
-                if (e) return e;
-            }
-            if (want_q) {
-                const dts_output_spec &o = s.out[s.quality_out];
-                dts_dev_frames qa = dst[s.quality_out], qb = *qref;
-                for (int pl = 0; pl < 3; ++pl) {
-                    if (qa.data[pl]) qa.data[pl] = static_cast<uint8_t *>(qa.data[pl]) + (int64_t)c0 * qa.frame_stride;
-                    if (qb.data[pl]) qb.data[pl] = static_cast<uint8_t *>(qb.data[pl]) + (int64_t)c0 * qb.frame_stride;
-                }
-                e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, qa, qb, m, qraw_dev + c0, st);
-                if (e) return e;
-            }
             HIPCHK(ctx, hipEventRecord(qs.dev, st));
         }
         return DTS_OK;
     }
     const DevPlanes dsrc = to_dev(*src, s.src_fmt);
-    int e = g->hdr ? enqueue_hdr(g, dsrc, ddst, nframes, st) : enqueue_ladder(g, dsrc, ddst, dfmt, nframes, st);
-    if (e) return e;
-    if (g->ref && qraw_dev) {
-        e = rung_quality(g, qs, dsrc, ddst, 0, nframes, nframes, qraw_dev, st);
+    if (!(g->ref && qraw_dev))                   // no reference renditions to make: one call
+        return ladder_quality(g, qs, dsrc, ddst, dfmt, 0, nframes, nframes, qref, qraw_dev, st);
+    for (int c0 = 0; c0 < nframes; c0 += B) {    // reference renditions: one batch of scratch at a time
+        const int m = std::min(B, nframes - c0);
+        DevPlanes sc = dsrc, dd[DTS_MAX_OUTPUTS];
+        for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src->frame_stride);
+        dst_at(c0, dd);
+        const int e = ladder_quality(g, qs, sc, dd, dfmt, c0, m, nframes, qref, qraw_dev, st);
         if (e) return e;
-    }
-    if (want_q) {
-        const dts_output_spec &o = s.out[s.quality_out];
-        return quality_enqueue(ctx, qs, o.w, o.h, o.fmt, dst[s.quality_out], *qref, nframes, qraw_dev, st);
     }
     return DTS_OK;
 }

@@ -81,6 +81,7 @@ struct Plan5Rung {
     const SwsFilter *fh;             // the libswscale H filter
     const VTable *v;                 // the packed V table
     int dstW, dstH, fmt;             // plane size and the rendition's output format
+    bool qual = false;               // vf_psnr / vf_ssim fused into k_ladder7's V epilogue
 };
 
 struct Plan5In {
@@ -136,6 +137,8 @@ struct Plan7 {
     std::vector<uint32_t> frag;
     std::vector<int32_t> fire;
     std::vector<FragOp7> fsched;     // decoupled groups: each staging wave's V fragment DMAs
+    std::vector<QRend7> qrend;       // fused quality: per (rendition, plane) unit lists and boundaries
+    std::vector<int32_t> qunit, qbound;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
     int hsplit = 256;                // H tap split of the fragments (ladder7.hip walk7 HS)
 };

@@ -82,6 +82,10 @@
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
 #endif
+#ifndef DTS_L7_QEARLY
+#define DTS_L7_QEARLY 0     // fused quality: where the reference rows are loaded -- 2 before the V MFMAs, 1
+                            // before the store exchange (latency hidden, 4 more VGPRs live: spills), 0 after
+#endif
 #ifndef DTS_L7_DECOUPLE
 #define DTS_L7_DECOUPLE 0   // who issues the group's loads (Group7::st0; plan7_graph): 0 every wave deals the
                             // source pieces (a group's spare waves, if any, stage them all) and the first
@@ -406,6 +410,173 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
     return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
 }
 
+// ---- fused vf_psnr / vf_ssim (QF walks; vf_psnr.c compute_images_mse, vf_ssim.c ssim_4x4xn /
+// ssim_end1 / ssim_plane restated in kernels.hip k_quality) ----
+// After the store exchange lane L holds bytes of output row m = L >> 2 of the row block (the
+// store's row segment, quarter q4 = L & 3): 1..4 slices of 4 pixels, each one row of a 4x4
+// block.  The reference rendition is loaded in the same layout, the slices' sums (s1, s2, ss,
+// s12) of the four rows of a block meet in the lane of its last row (DPP row shifts by 4 and 8
+// lanes), which adds the block's SSE and parks the sums in the wave's LDS block table
+// (plane-major, 5 block rows: the previous row block's last and this one's 4, BW block columns);
+// then every 8x8 window at stride 4 whose four blocks lie in this unit and whose top row is the
+// previous row block's last or one of this row block's first three is scored (ssim_end1).
+// Windows straddling two units are k_qfix7's; per unit the sums go to a QPart7.
+
+// NB reference bytes at byte `at` of a row with `room` bytes left (the plane's last columns
+// byte by byte; the rest zero)
+template <int NB>
+__device__ __forceinline__ void get_row7(uint64_t rowp, int at, int room, uint32_t (&w)[4])
+{
+    const g_u8 *p = GP6(const g_u8, rowp + (uint64_t)(int64_t)at);
+    w[0] = w[1] = w[2] = w[3] = 0;
+    if (room >= NB) {
+        if (NB == 16) {
+            const u32x4 v = *GP6(const g_u32x4, p);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else if (NB == 8) {
+            const u32x2 v = *GP6(const g_u32x2, p);
+            w[0] = v.x; w[1] = v.y;
+        } else {
+            w[0] = *GP6(const g_u32, p);
+        }
+    } else {
+        asm volatile("" : "+v"(room));
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+            if (i < room) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+    }
+}
+
+// the reference bytes of this lane's share of row block j: the rows and byte offsets vstore7 writes
+template <int VAR, class UT>
+__device__ __forceinline__ void qload7(const UT &U, int j, const uint64_t (&qb)[2], const uint32_t (&qp)[2], int lane,
+                                       uint32_t (&r)[4])
+{
+    using W = Walk6<VAR>;
+    asm volatile("" : "+v"(lane));                       // (qrb7: nothing hoisted out of the walk)
+    const int y = 16 * j + (lane >> 2), q4 = lane & 3;
+    r[0] = r[1] = r[2] = r[3] = 0;
+    if (y >= U.dstH) return;
+    if (W::NP == 1) {
+        if (W::CT == 4) get_row7<16>(qb[0] + (uint64_t)y * qp[0], U.col0 + 16 * q4, U.dstW - U.col0 - 16 * q4, r);
+        else get_row7<8>(qb[0] + (uint64_t)y * qp[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, r);
+    } else if (U.fmt == DTS_FMT_NV12) {
+        const int at = 2 * U.col0 + 8 * W::CT * q4;
+        if (W::CT == 2) get_row7<16>(qb[0] + (uint64_t)y * qp[0], at, 2 * U.dstW - at, r);
+        else get_row7<8>(qb[0] + (uint64_t)y * qp[0], at, 2 * U.dstW - at, r);
+    } else {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            uint32_t t[4];
+            const int at = U.col0 + 4 * W::CT * q4;
+            if (W::CT == 2) get_row7<8>(qb[p] + (uint64_t)y * qp[p], at, U.dstW - at, t);
+            else get_row7<4>(qb[p] + (uint64_t)y * qp[p], at, U.dstW - at, t);
+            r[W::CT * p] = t[0];
+            if (W::CT == 2) r[2 * p + 1] = t[1];
+        }
+    }
+}
+
+// v + v of the lane 4 (8) below in the same 16-lane row (bound_ctrl: lanes without one add 0)
+__device__ __forceinline__ uint32_t rsum4x(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    return v;
+}
+
+__device__ __forceinline__ float ssim_end1_7(int s1, int s2, int ss, int s12)
+{
+    const int c1 = (int)(.01 * .01 * 255 * 255 * 64 + .5);
+    const int c2 = (int)(.03 * .03 * 255 * 255 * 64 * 63 + .5);
+    const int vars = ss * 64 - s1 * s1 - s2 * s2;
+    const int covar = s12 * 64 - s1 * s2;
+    return (float)(2 * s1 * s2 + c1) * (float)(2 * covar + c2) *
+           __builtin_amdgcn_rcpf((float)(s1 * s1 + s2 * s2 + c1) * (float)(vars + c2));
+}
+
+// row block j's quality: x = output bytes after the exchange (xchg7), rr = reference (qload7).
+// The block sums of rows 1..4 go to the wave's exchange scratch (free once xchg7 has read it),
+// row 0 (the previous row block's last block row) and the running sums to the wave's kQ7Wave
+// area: sse / ssim slots of u64, added by LDS atomics (integers: the same sums whatever the
+// lane order; ssim_end1 values in 2^-24 fixed point)
+template <int VAR, class UT>
+__device__ __forceinline__ void qrb7(const UT &U, int j, const uint32_t (&x)[4], const uint32_t (&rr)[4], uint8_t *scr,
+                                     uint8_t *qw, int lane)
+{
+    using W = Walk6<VAR>;
+    constexpr int NP = W::NP, BW = 4 * W::CT;           // planes, block columns per plane
+    constexpr int NS = (NP == 1 && W::CT == 4) || (NP == 2 && W::CT == 2) ? 4 : 2;   // slices per lane
+    // every lane-dependent term below is formed here, per row block: the lane index goes through an
+    // empty asm so nothing is hoisted out of the walk (it would hold ~20 VGPRs across every granule)
+    asm volatile("" : "+v"(lane));
+    const int q4 = lane & 3, m = lane >> 2, y = 16 * j + m;
+    const bool last = (m & 3) == 3;                      // the lane holding its block's sums
+    const bool il = NP == 2 && U.fmt == DTS_FMT_NV12;
+    uint32_t sse[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        // slice k: plane pk, block column bk (of the unit); nv12: dwords 2 h, 2 h + 1 hold the U V
+        // pairs of 4 columns, slice 2 h is their U, 2 h + 1 their V
+        const int pk = NP == 1 ? 0 : (il ? (k & 1) : k / (NS / 2));
+        const int bk = NP == 1 ? NS * q4 + k : (NS / 2) * q4 + (il ? k >> 1 : k % (NS / 2));
+        uint32_t ak, bk8;
+        if (il) {
+            const uint32_t sel = (k & 1) ? 0x07050301u : 0x06040200u;
+            ak = __builtin_amdgcn_perm(x[(k & ~1) + 1], x[k & ~1], sel);
+            bk8 = __builtin_amdgcn_perm(rr[(k & ~1) + 1], rr[k & ~1], sel);
+        } else {
+            ak = x[k];
+            bk8 = rr[k];
+        }
+        const int vb = min(max(U.dstW - U.col0 - 4 * bk, 0), 4);
+        const uint32_t msk = y < U.dstH ? (vb >= 4 ? 0xffffffffu : (1u << (8 * vb)) - 1u) : 0u;
+        ak &= msk;
+        bk8 &= msk;
+        const uint32_t s1 = __builtin_amdgcn_udot4(ak, 0x01010101u, 0u, false);
+        const uint32_t s2 = __builtin_amdgcn_udot4(bk8, 0x01010101u, 0u, false);
+        const uint32_t p12 = rsum4x(s1 + (s2 << 16));
+        const uint32_t ss = rsum4x(__builtin_amdgcn_udot4(bk8, bk8, __builtin_amdgcn_udot4(ak, ak, 0u, false), false));
+        const uint32_t s12 = rsum4x(__builtin_amdgcn_udot4(ak, bk8, 0u, false));
+        if (last) {
+            sse[pk] += ss - 2u * s12;
+            *reinterpret_cast<u32x4 *>(scr + 16 * ((pk * 4 + (m >> 2)) * BW + bk)) = (u32x4){p12, ss, s12, 0u};
+        }
+    }
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(qw + kQ7Acc);
+    if (last) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) atomicAdd(acc + p, (unsigned long long)sse[p]);
+    }
+    // windows: plane wp, top block row wy (0: the previous row block's last, in qw), block column wx
+    constexpr int NW = NP * 4 * (BW - 1);
+    static_assert(NW <= 64, "one window per lane");
+    if (lane < NW) {
+        const int wp = lane / (4 * (BW - 1)), rem = lane - wp * 4 * (BW - 1);
+        const int wy = rem / (BW - 1), wx = rem - wy * (BW - 1);
+        const int gy = 4 * j + wy - 1, gx = (U.col0 >> 2) + wx;
+        const uint8_t *t0 = wy ? scr + 16 * ((wp * 4 + wy - 1) * BW + wx) : qw + 16 * (wp * BW + wx);
+        const uint8_t *t1 = scr + 16 * ((wp * 4 + wy) * BW + wx);
+        uint32_t sp = 0, sq = 0, sc = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = *reinterpret_cast<const u32x4 *>((i >> 1 ? t1 : t0) + 16 * (i & 1));
+            sp += v.x;
+            sq += v.y;
+            sc += v.z;
+        }
+        const float v = ssim_end1_7((int)(sp & 0xffffu), (int)(sp >> 16), (int)sq, (int)sc);
+        if (gy >= 0 && gy + 1 < (U.dstH >> 2) && gx + 1 < (U.dstW >> 2))
+            atomicAdd(acc + 2 + wp, (unsigned long long)(long long)(int)(v * 16777216.f));
+    }
+    // this row block's last block row becomes the next one's row 0
+    if (lane < NP * BW) {
+        const int cp = lane / BW, cxb = lane - cp * BW;
+        *reinterpret_cast<u32x4 *>(qw + 16 * (cp * BW + cxb)) =
+            *reinterpret_cast<const u32x4 *>(scr + 16 * ((cp * 4 + 3) * BW + cxb));
+    }
+}
+
 // V of one row block over the whole ring, as vcalc (ladder_mfma.h): 65536 hh + 256 (hl +
 // lh) + ll as three chained accumulations; the bias enters as b1 << 16 (the chain's start)
 // and b2 << 8 (added with the first shift), so a per-lane bias (the ordered dither of
@@ -563,7 +734,7 @@ __device__ __forceinline__ void idle7(const Ladder7Params &P, const Group7 &G, c
 // p010 sources add the ordered dither ff_dither_8x8_128[y & 7][(x + off) & 7] << 12 (off 3
 // for V) instead of the flat 64; p010 outputs (any source) are yuv2p010lX / cX:
 // av_clip_uintp2((sum + (1 << 16)) >> 17, 10) << 6.
-template <int VAR, bool RC, int HS, int SK>
+template <int VAR, bool RC, int HS, int SK, bool QF>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -588,6 +759,22 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             op[p] = (uint32_t)(U.kind ? D.pitch[1 + p] : D.pitch[0]);
         }
     }
+    // fused quality (QF): the rendition's reference planes of this frame, the wave's block table
+    // and its running sums
+    uint8_t *qtab = lds7 + G.qscr + kQ7Wave * wave;
+    const bool qon = QF && U.qual;
+    if (qon && lane < 4) reinterpret_cast<unsigned long long *>(qtab + kQ7Acc)[lane] = 0ull;
+    // the rendition's reference planes of this frame (re-read from the kernel arguments at each
+    // row block: nothing held across the walk)
+    auto qref7 = [&](uint64_t (&qbp)[2], uint32_t (&qpp)[2]) {
+        const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
+        const DevPlanes R = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, qref)) + U.rung);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            qbp[p] = (U.kind ? R.data[1 + p] : R.data[0]) + (uint64_t)f * (uint64_t)R.fstride;
+            qpp[p] = (uint32_t)(U.kind ? R.pitch[1 + p] : R.pitch[0]);
+        }
+    };
     const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
     // H B operands of the walk (p010: bh = the M fragments, bl = L, ba = A of put6p)
     constexpr int BC = P10 ? RKB : HKB;
@@ -767,6 +954,14 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     p010out = true;
                 }
             }
+            uint32_t qr[4] = {0, 0, 0, 0};
+            if (qon && DTS_L7_QEARLY == 2) {            // the reference row segments, in flight during V
+                uint64_t qbp[2];
+                uint32_t qpp[2];
+                qref7(qbp, qpp);
+                qload7<VAR>(U, j, qbp, qpp, lane, qr);
+                ++Z.ops;
+            }
             if (!p010out) {
                 uint32_t w[T];
                 if (DTS_L7_ABLATE & 128) {
@@ -776,12 +971,27 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
                 }
                 flush();
+                if (qon && DTS_L7_QEARLY == 1) {        // the reference row segments, in flight during the exchange
+                    uint64_t qbp[2];
+                    uint32_t qpp[2];
+                    qref7(qbp, qpp);
+                    qload7<VAR>(U, j, qbp, qpp, lane, qr);
+                    ++Z.ops;
+                }
                 if (DTS_L7_ABLATE & 64) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) asm volatile("" ::"v"(w[t]));
                 } else {
                     xchg7<VAR>(U, w, scr, m, g, lane, px);
                 }
+                if (qon && DTS_L7_QEARLY == 0) {        // the reference row segments
+                    uint64_t qbp[2];
+                    uint32_t qpp[2];
+                    qref7(qbp, qpp);
+                    qload7<VAR>(U, j, qbp, qpp, lane, qr);
+                    ++Z.ops;
+                }
+                if (qon) qrb7<VAR>(U, j, px, qr, scr, qtab, lane);
             }
             pj = (DTS_L7_ABLATE & 96) ? -1 : j;
             if (!DEFER_ST) flush();
@@ -1009,6 +1219,18 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     }
     if (DTS_L7_DEFER) vfire(ngran - 1);
     flush();
+    if (qon) {                                          // the unit's partial record (fixed-order lane sums)
+        const unsigned long long *acc = reinterpret_cast<const unsigned long long *>(qtab + kQ7Acc);
+        const uint64_t e0 = acc[0], e1 = acc[1];
+        const double s0 = (double)(long long)acc[2] * (1.0 / 16777216.0), s1 = (double)(long long)acc[3] * (1.0 / 16777216.0);
+        if (lane == 0) {
+            QPart7 *qp = P.qpart + (int64_t)f * P.nunits + (G.u0 + wave);
+            qp->sse[0] = e0;
+            qp->sse[1] = e1;
+            qp->ssim[0] = s0;
+            qp->ssim[1] = s1;
+        }
+    }
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1021,7 +1243,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 
 // RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
 // the common kernel keeps its register allocation)
-template <bool RC, int HS, int SK>
+template <bool RC, int HS, int SK, bool QF = false>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -1044,28 +1266,28 @@ void k_ladder7(Ladder7Params P)
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
     if constexpr ((SK == 2) == ((DTS_L7_ONLYVAR & 16) != 0)) {
-        walk7<DTS_L7_ONLYVAR, RC, HS, SK>(P, G, U, S, f, wave, waves);
+        walk7<DTS_L7_ONLYVAR, RC, HS, SK, QF>(P, G, U, S, f, wave, waves);
         return;
     }
 #endif
     if constexpr (SK == 2) {                // p010 sources: the 16-bit one-K-block variants
         switch (U.variant) {
-        case 16: walk7<16, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-        case 17: walk7<17, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-        default: walk7<20, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        case 16: walk7<16, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+        case 17: walk7<17, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+        default: walk7<20, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
         }
     } else {
     switch (U.variant) {
-    case 0: walk7<0, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
     }
     }
 }
@@ -1094,10 +1316,21 @@ void ladder7_compiled(int *stages, int *batch, int *decouple)
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          int src_kind, hipStream_t s)
+                          int src_kind, hipStream_t s, bool quality)
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
+    if (quality) {                       // fused vf_psnr / vf_ssim: 8-bit sources, no range conversion
+        if (range_conv || src_kind == kSrcP010 || !p.qpart) return hipErrorInvalidValue;
+        if (src_kind == kSrcNV12) {
+            if (hsplit == 128) hipLaunchKernelGGL((k_ladder7<false, 128, 1, true>), g, b, lds_bytes, s, p);
+            else hipLaunchKernelGGL((k_ladder7<false, 256, 1, true>), g, b, lds_bytes, s, p);
+        } else {
+            if (hsplit == 128) hipLaunchKernelGGL((k_ladder7<false, 128, 0, true>), g, b, lds_bytes, s, p);
+            else hipLaunchKernelGGL((k_ladder7<false, 256, 0, true>), g, b, lds_bytes, s, p);
+        }
+        return hipGetLastError();
+    }
     if (src_kind == kSrcP010) {          // p010 sources (no range conversion: dts_graph_create refuses it)
         if (range_conv) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_ladder7<false, 256, 2>), g, b, lds_bytes, s, p);

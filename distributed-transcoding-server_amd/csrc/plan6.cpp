@@ -516,6 +516,9 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                     v.lead = 1;
                 }
                 v.flds = flds[w.rung];
+                // fused quality: 8-bit renditions (yuv420p / nv12) of 8-bit sources
+                v.qual = kinds[kind].rungs[(size_t)w.rung].qual ? 1 : 0;
+                if (v.qual && (kinds[kind].p10 || (v.fmt != DTS_FMT_YUV420P && v.fmt != DTS_FMT_NV12))) return false;
                 if (w.ngran != g.ngran) return false;
                 out.units.push_back(v);
             }
@@ -563,7 +566,46 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     // planner put the heaviest units first)
     for (Group7 &g : out.groups)
         g.st0 = g.nwaves < out.waves ? g.nwaves : (decouple == 2 ? g.nwaves / 2 : 0);
-    for (const Group7 &g : out.groups) out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
+    // fused quality: per wave the 4x4-block sums of its row blocks after the store exchange
+    bool anyq = false;
+    for (const Unit7 &u : out.units) anyq = anyq || u.qual;
+    for (Group7 &g : out.groups) {
+        g.qscr = g.scr + out.waves * 1024;
+        out.lds_bytes = std::max(out.lds_bytes, g.qscr + (anyq ? out.waves * kQ7Wave : 0));
+    }
+    if (anyq) {
+        // per (rendition, plane): its units left to right and the boundaries between them (the
+        // block column left of each: k_qfix7 scores the windows straddling it)
+        int nr = 0;
+        for (int kind = 0; kind < 2; ++kind) nr = std::max(nr, (int)kinds[kind].rungs.size());
+        for (int r = 0; r < nr; ++r)
+            for (int kind = 0; kind < 2; ++kind) {
+                if (r >= (int)kinds[kind].rungs.size() || !kinds[kind].rungs[(size_t)r].qual) continue;
+                std::vector<std::pair<int, int>> us;           // (col0, unit)
+                for (int i = 0; i < (int)out.units.size(); ++i)
+                    if (out.units[(size_t)i].kind == kind && out.units[(size_t)i].rung == r)
+                        us.push_back({out.units[(size_t)i].col0, i});
+                std::sort(us.begin(), us.end());
+                const Plan5Rung &R = kinds[kind].rungs[(size_t)r];
+                for (int pl = kind ? 1 : 0; pl <= (kind ? 2 : 0); ++pl) {
+                    QRend7 q{};
+                    q.rung = r;
+                    q.plane = pl;
+                    q.w = R.dstW;
+                    q.h = R.dstH;
+                    q.u0 = (int)out.qunit.size();
+                    q.nu = (int)us.size();
+                    for (const auto &e : us) out.qunit.push_back(e.second);
+                    q.b0 = (int)out.qbound.size() / 2;
+                    for (size_t i = 1; i < us.size(); ++i) {
+                        out.qbound.push_back(us[i].first / 4 - 1);
+                        out.qbound.push_back((int)out.qrend.size());
+                    }
+                    q.nb = (int)out.qbound.size() / 2 - q.b0;
+                    out.qrend.push_back(q);
+                }
+            }
+    }
     return out.lds_bytes <= 160 * 1024;
 }
 

@@ -26,6 +26,7 @@ METHODS = {"bilinear": SCALE_BILINEAR, "bicubic": SCALE_BICUBIC, "x": SCALE_X, "
            "lanczos": SCALE_LANCZOS}
 PARAM_DEFAULT = 123456.0
 Q_NONE, Q_PSNR, Q_SSIM, Q_BOTH = 0, 1, 2, 3
+QREF_EXTERNAL = -1           # dts_output_spec.qref_method: references passed with every run (dts.h)
 # vf_tonemap.c enum TonemapAlgorithm
 TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS = range(7)
 TM_MODES = {"none": TM_NONE, "linear": TM_LINEAR, "gamma": TM_GAMMA, "clip": TM_CLIP, "reinhard": TM_REINHARD,
@@ -380,9 +381,14 @@ class Graph:
         return outs, ([qs[i].as_dict() for i in range(n)] if qs is not None else None)
 
     def run_device(self, src, nframes, dsts, qref=None, qraw_ptr=0, stream=None):
+        """qref: the quality_out reference batch (DevFrames), or with rendition quality against
+        external references (qref_method QREF_EXTERNAL) a list of one DevFrames per output"""
         k = len(dsts)
         arr = (DevFrames * k)(*dsts)
-        check(lib().dts_graph_run_device(self.h, ctypes.byref(src), nframes, arr,
-                                         ctypes.byref(qref) if qref is not None else None,
+        if isinstance(qref, (list, tuple)):
+            qarg = (DevFrames * len(qref))(*[q if q is not None else DevFrames() for q in qref])
+        else:
+            qarg = ctypes.byref(qref) if qref is not None else None
+        check(lib().dts_graph_run_device(self.h, ctypes.byref(src), nframes, arr, qarg,
                                          ctypes.c_void_p(qraw_ptr), ctypes.c_void_p(stream or 0)),
               "graph_run_device")

@@ -110,8 +110,12 @@ typedef struct dts_output_spec {
      * filtergraph.  DTS_Q_* (0 = off); 8-bit outputs, no HDR graph, and not together
      * with dts_graph_spec.quality (an external reference). */
     int32_t quality;
-    int32_t qref_method;
+    int32_t qref_method;    /* DTS_SCALE_*, or DTS_QREF_EXTERNAL: the reference renditions come
+                               with every dts_graph_run_device call (its qref then points to nout
+                               batches; entries of outputs without quality are not read) */
 } dts_output_spec;
+
+#define DTS_QREF_EXTERNAL (-1)
 
 typedef struct dts_graph_spec {
     int32_t src_w, src_h, src_fmt;      /* source segment frames */
