@@ -229,6 +229,12 @@ struct dts_graph {
     hipEvent_t hdr_ev[2] = {nullptr, nullptr};   // k_tonemap done reading intermediate sl
     hipEvent_t hdr_mid_ev[2] = {nullptr, nullptr};   // the ladder wrote intermediate sl
     hipEvent_t hdr_go = nullptr, hdr_end = nullptr;
+    // the separate quality pass on its own stream (DTS_QSTREAM): k_quality of chunk i beside the
+    // ladder of chunk i + 1 (qs_ev[i % kQEv]: chunk i's outputs are written)
+    static constexpr int kQEv = 8;
+    hipStream_t q_st = nullptr;
+    hipEvent_t q_ev[kQEv] = {}, q_go = nullptr, q_end = nullptr;
+    unsigned q_next = 0;
     hipStream_t hdr_tm = nullptr;         // k_tonemap's own stream: the ladder of chunk i + 1 runs
                                           // beside the tonemap of chunk i (nullptr: one stream)
     int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk
@@ -579,7 +585,24 @@ bool wants_quality(const dts_graph_spec &s, int k)
     return (s.quality && k == s.quality_out) || s.out[k].quality;
 }
 
-// quality fused into k_ladder7's V epilogue (DTS_QFUSE=1; else the separate k_quality pass)
+// the separate quality pass on a stream of its own beside the next chunk's ladder (DTS_QSTREAM=1;
+// measured slower than one stream: cfg4 41.5k vs 45.5k, cfg5 111.3k vs 116.2k fps -- DESIGN.md §4)
+bool qstream_enabled()
+{
+    const char *f = std::getenv("DTS_QSTREAM");
+    return f && f[0] == '1';
+}
+
+// frames per ladder -> quality chunk on two streams (DTS_QCHUNK; default a quarter of the call, >= 16)
+int qchunk_frames(int n)
+{
+    const char *f = std::getenv("DTS_QCHUNK");
+    const int c = f ? std::atoi(f) : std::max(16, (n + 3) / 4);
+    return std::max(1, c);
+}
+
+// quality fused into k_ladder7's V epilogue (DTS_QFUSE=1; else the separate k_quality pass).  Bit-exact
+// records, measured slower (cfg4 20.8k vs 45.5k, cfg5 51.8k vs 116.2k fps -- DESIGN.md §4)
 bool qfuse_enabled()
 {
     const char *f = std::getenv("DTS_QFUSE");
@@ -1199,6 +1222,21 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
                 o.quality = 0;
                 g->rq_out[rs.nout++] = k;
             }
+        bool anyq = s.quality != 0;
+        for (int k = 0; k < s.nout; ++k) anyq = anyq || s.out[k].quality;
+        if (anyq && !s.hdr_to_sdr && qstream_enabled()) {
+            e = DTS_OK;
+            if (hipStreamCreateWithFlags(&g->q_st, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&g->q_go, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&g->q_end, hipEventDisableTiming) != hipSuccess)
+                e = DTS_E_HIP;
+            for (int i = 0; i < dts_graph::kQEv && !e; ++i)
+                if (hipEventCreateWithFlags(&g->q_ev[i], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
+            if (e) {
+                dts_graph_destroy(g);
+                return e;
+            }
+        }
         if (rs.nout) {
             for (int k = rs.nout; k < DTS_MAX_OUTPUTS; ++k) rs.out[k] = dts_output_spec{};
             e = dts_graph_create(ctx, &rs, &g->ref);
@@ -1246,6 +1284,14 @@ void dts_graph_destroy(dts_graph *g)
         hipStreamSynchronize(g->hdr_tm);
         hipStreamDestroy(g->hdr_tm);
     }
+    if (g->q_st) {
+        hipStreamSynchronize(g->q_st);
+        hipStreamDestroy(g->q_st);
+    }
+    for (int i = 0; i < dts_graph::kQEv; ++i)
+        if (g->q_ev[i]) hipEventDestroy(g->q_ev[i]);
+    if (g->q_go) hipEventDestroy(g->q_go);
+    if (g->q_end) hipEventDestroy(g->q_end);
     if (g->hdr_go) hipEventDestroy(g->hdr_go);
     if (g->hdr_end) hipEventDestroy(g->hdr_end);
     for (int sl = 0; sl < 2; ++sl) {
@@ -1718,20 +1764,51 @@ static int ladder_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, cons
     }
     int e = g->hdr ? DTS_E_UNSUPPORTED : enqueue_ladder_q(g, qs, src, dst, m, qr, out_q, qstride, st);
     if (e == DTS_E_UNSUPPORTED) {                // the separate pass: the ladder, then k_quality per output
-        e = g->hdr ? enqueue_hdr(g, src, dst, m, st) : enqueue_ladder(g, src, dst, dfmt, m, st);
-        for (int k = 0; k < s.nout && !e; ++k) {
-            if (!qr[k].data[0]) continue;
-            const dts_output_spec &o = s.out[k];
-            dts_dev_frames a{}, b{};
-            for (int pl = 0; pl < 3; ++pl) {
-                a.data[pl] = dst[k].data[pl] ? reinterpret_cast<void *>(dst[k].data[pl]) : nullptr;
-                a.pitch[pl] = dst[k].pitch[pl];
-                b.data[pl] = qr[k].data[pl] ? reinterpret_cast<void *>(qr[k].data[pl]) : nullptr;
-                b.pitch[pl] = qr[k].pitch[pl];
+        // in chunks, the quality of chunk i on the graph's quality stream beside the ladder of chunk
+        // i + 1 (both in the CUs at once where the ladder leaves room: cfg4's one group per CU)
+        e = DTS_OK;
+        const bool two = g->q_st && !g->hdr;
+        const int C = two ? qchunk_frames(m) : m;
+        hipStream_t qst = two ? g->q_st : st;
+        if (two) {                               // the outputs' / references' earlier users on st first
+            HIPCHK(ctx, hipEventRecord(g->q_go, st));
+            HIPCHK(ctx, hipStreamWaitEvent(qst, g->q_go, 0));
+        }
+        for (int c0 = 0; c0 < m && !e; c0 += C) {
+            const int mc = std::min(C, m - c0);
+            DevPlanes sc = src, dc[DTS_MAX_OUTPUTS];
+            for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src.fstride);
+            for (int k = 0; k < s.nout; ++k) {
+                dc[k] = dst[k];
+                for (int pl = 0; pl < 3; ++pl) dc[k].data[pl] += (uint64_t)((int64_t)c0 * dst[k].fstride);
             }
-            a.frame_stride = dst[k].fstride;
-            b.frame_stride = qr[k].fstride;
-            e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, m, out_q + (int64_t)k * qstride, st);
+            e = g->hdr ? enqueue_hdr(g, sc, dc, mc, st) : enqueue_ladder(g, sc, dc, dfmt, mc, st);
+            if (e) break;
+            if (two) {
+                hipEvent_t ev = g->q_ev[g->q_next++ % dts_graph::kQEv];
+                HIPCHK(ctx, hipEventRecord(ev, st));
+                HIPCHK(ctx, hipStreamWaitEvent(qst, ev, 0));
+            }
+            for (int k = 0; k < s.nout && !e; ++k) {
+                if (!qr[k].data[0]) continue;
+                const dts_output_spec &o = s.out[k];
+                dts_dev_frames a{}, b{};
+                for (int pl = 0; pl < 3; ++pl) {
+                    a.data[pl] = dc[k].data[pl] ? reinterpret_cast<void *>(dc[k].data[pl]) : nullptr;
+                    a.pitch[pl] = dst[k].pitch[pl];
+                    b.data[pl] = qr[k].data[pl] ? reinterpret_cast<void *>(qr[k].data[pl] +
+                                                                           (uint64_t)((int64_t)c0 * qr[k].fstride))
+                                                : nullptr;
+                    b.pitch[pl] = qr[k].pitch[pl];
+                }
+                a.frame_stride = dst[k].fstride;
+                b.frame_stride = qr[k].fstride;
+                e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, mc, out_q + (int64_t)k * qstride + c0, qst);
+            }
+        }
+        if (two && !e) {                         // the caller's stream sees the records
+            HIPCHK(ctx, hipEventRecord(g->q_end, qst));
+            HIPCHK(ctx, hipStreamWaitEvent(st, g->q_end, 0));
         }
     }
     if (!e && rq) HIPCHK(ctx, hipEventRecord(qs.rev, st));

@@ -51,7 +51,7 @@ def _qraws(t, n, off=0):
 def _batch(w, h, fmt, n):
     import torch
     from bench import dev_batch, frame_bytes
-    t = torch.empty((n, frame_bytes(w, h, fmt)), dtype=torch.uint8, device="cuda")
+    t = torch.zeros((n, frame_bytes(w, h, fmt)), dtype=torch.uint8, device="cuda")   # (row padding compared too)
     return t, dev_batch(t, w, h, fmt)[0]
 
 
