@@ -614,9 +614,11 @@ __device__ __forceinline__ void vcalc7(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<VA
         for (int t = 0; t < W::T; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(rl[kb][t], vl[kb], acc[t], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < W::T; ++t) {
-        const uint32_t lo = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][0], acc[t][1], 19);
-        const uint32_t hi = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][2], acc[t][3], 19);
-        w[t] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+        // the two 16-bit packs as one u16x2 (a v_perm of their low halves: no zero-extension of each)
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const unsigned short lo = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][0], acc[t][1], 19);
+        const unsigned short hi = __builtin_amdgcn_ashr_pk_u8_i32(acc[t][2], acc[t][3], 19);
+        w[t] = __builtin_bit_cast(uint32_t, (u16x2){lo, hi});
     }
 }
 
