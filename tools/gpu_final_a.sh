@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3 pass, part 1: tests + smoke, then the cfg2 (with SQ counters), cfg3 and cfg1 lines with
+# round-end pass, part 1: tests + smoke, then the cfg2 (with SQ counters), cfg3 and cfg1 lines with
 # their rocprofv3 passes, all from this build on this box (tools/prof_wl.sh)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3 pass, part 2: cfg4, cfg5 (8 steps), yadif and cfg2nv12 lines with their rocprofv3 passes,
+# round-end pass, part 2: cfg4, cfg5 (8 steps), yadif and cfg2nv12 lines with their rocprofv3 passes,
 # then the host-memory end-to-end line (cfg2)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

@@ -1,11 +1,11 @@
 #!/bin/bash
 # PMC passes of the cfg2 bench (one rocprofv3 --pmc run per pass, no tracing) for
-# the kernel named by $KERNEL (default k_ladder6); per-launch averages printed.
+# the kernel named by $KERNEL (default k_ladder7); per-launch averages printed.
 # usage: tools/pmc6.sh <tag> [lib suffixes; "" = lib/libdts.so].  Diagnostic only.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 tag=${1:-p6}; shift
-K=${KERNEL:-k_ladder6}
+K=${KERNEL:-k_ladder7}
 out=gpurun_out/pmc_$tag
 mkdir -p $out
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS"
