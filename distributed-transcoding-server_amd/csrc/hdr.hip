@@ -25,6 +25,9 @@
 #ifndef DTS_TM_OETF_POW
 #define DTS_TM_OETF_POW 0   // 1: BT.709 OETF by v_log / v_exp instead of the LDS table (A/B knob)
 #endif
+#ifndef DTS_TM_ABLATE
+#define DTS_TM_ABLATE 0     // diagnostic bits (wrong output): 1 no ring pass, 2 no chroma 2:1 pass, 4 no pixel math
+#endif
 #ifndef DTS_TM_UNROLL
 #define DTS_TM_UNROLL 0     // 1: both block iterations of a lane unrolled (8 pixels in flight; A/B knob)
 #endif
@@ -93,6 +96,11 @@ template <int MODE, bool DESAT>
 __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, float y10, float2 c, float &Y,
                                       float2 &C)
 {
+    if (DTS_TM_ABLATE & 4) {
+        Y = y10 * (1.f / 1024.f);
+        C = c;
+        return;
+    }
     const float2 *pq = tl, *oetf = tl + kTmLutN + 1;          // pq already scaled by 10000 / npl
     constexpr float N = (float)kTmLutN;
     constexpr float kr2 = 0.2627f, kb2 = 0.0593f, kg2 = 1.f - kr2 - kb2;
@@ -108,7 +116,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     // vf_tonemap.c tonemap()
     if (DESAT) {
         const float luma = kr7 * r + kg7 * g + kb7 * b;
-        const float ob = fmaxf(luma - P.desat, 1e-6f) / fmaxf(luma, 1e-6f);
+        const float ob = fmaxf(luma - P.desat, 1e-6f) * rcp(fmaxf(luma, 1e-6f));   // (v_rcp: an IEEE divide is ~10 VALU)
         r = r * (1.f - ob) + luma * ob;
         g = g * (1.f - ob) + luma * ob;
         b = b * (1.f - ob) + luma * ob;
@@ -163,6 +171,8 @@ template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
     constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
+    constexpr int kRow = 129;                       // ring row: columns x0 - 1 .. x0 + 127
+    constexpr int kCin = kTmCH * kTmCW;             // staged chroma samples per tile (660: 3 per thread)
     __shared__ float2 tl[kTabs * (kTmLutN + 1)];
     __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
     __shared__ __attribute__((aligned(16))) float2 cc[kTmLH][kTmLP];   // output (Cb, Cr) at full resolution
@@ -171,26 +181,86 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     const int cx0 = blockIdx.x * 64;
     const int x0 = 2 * cx0;
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
+    const uint64_t sy0 = P.src.data[0] + sf, sc0 = P.src.data[1] + sf;
+    const int lp = P.src.pitch[0], cp = P.src.pitch[1];
     const bool a4 = ((P.src.data[0] + sf) & 3) == 0 && (P.src.pitch[0] & 3) == 0;
     for (int i = t; i < kTabs * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
+    // a thread's staged chroma samples (rows / columns fixed over the tiles) and block positions
+    int cr[3], cxo[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int i = t + 256 * k, r = i / kTmCW, c = i - r * kTmCW;
+        cr[k] = r;
+        cxo[k] = 4 * min(max(cx0 - 1 + c, 0), cw - 1);
+    }
+    const int byl0 = t >> 6, bxl = t & 63;          // block items t and t + 256: rows byl0, byl0 + 4
+    // ring item t of a tile: (lx, ly) of the ring -- rows y0 - 1 (first tile only) and y0 + 16,
+    // columns x0 - 1 .. x0 + 127, and column x0 - 1 of the 16 rows between
+    auto ring_at = [&](int i, int top, int &lx, int &ly) {
+        if (i < top) {
+            ly = 0;
+            lx = i;
+        } else if (i < top + kRow) {
+            ly = kTmLH - 1;
+            lx = i - top;
+        } else {
+            ly = 1 + (i - top - kRow);
+            lx = 0;
+        }
+    };
+    auto luma_at = [&](int xr, int yr) -> float {
+        const int x = min(max(xr, 0), P.w - 1), y = min(max(yr, 0), P.h - 1);
+        return (float)(gld<uint16_t>(sy0 + (uint64_t)y * lp + 2 * x) >> 6);
+    };
+    // loads of tile `tile` into registers: its staged chroma, its block path luma, its ring item t
+    uint32_t ncin[3] = {0, 0, 0}, nl[4] = {0, 0, 0, 0};
+    float nring = 0.f;
+    auto fetch = [&](int tile) {
+        const int cy0 = (blockIdx.y * kTmTiles + tile) * kTmCRows, y0 = 2 * cy0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (k < 2 || t + 512 < kCin)
+                ncin[k] = gld<uint32_t>(sc0 + (uint64_t)min(max(cy0 - 1 + cr[k], 0), ch - 1) * cp + cxo[k]);
+        if (a4 && x0 + 128 <= P.w && y0 + 16 <= P.h) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const uint64_t ys = sy0 + (uint64_t)(y0 + 2 * (byl0 + 4 * kb)) * lp + 4 * (x0 / 2 + bxl);
+                nl[2 * kb] = gld<uint32_t>(ys);
+                nl[2 * kb + 1] = gld<uint32_t>(ys + lp);
+            }
+        }
+        const int top = tile ? 0 : kRow;
+        if (t < top + kRow + 2 * kTmCRows) {
+            int lx, ly;
+            ring_at(t, top, lx, ly);
+            nring = luma_at(x0 - 1 + lx, y0 - 1 + ly);
+        }
+    };
+    fetch(0);
     for (int tile = 0; tile < kTmTiles; ++tile) {
     const int cy0 = (blockIdx.y * kTmTiles + tile) * kTmCRows, y0 = 2 * cy0;
     if (cy0 >= ch) break;
+    const bool blk = a4 && x0 + 128 <= P.w && y0 + 16 <= P.h;
+    uint32_t l[4], vc[3];
+    float yring = nring;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) l[k] = nl[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vc[k] = ncin[k];
     if (tile) __syncthreads();                      // the previous tile's chroma pass is done with cin / cc
-    for (int i = t; i < kTmCH * kTmCW; i += 256) {
-        const int r = i / kTmCW, c = i - r * kTmCW;
-        const int sy = min(max(cy0 - 1 + r, 0), ch - 1), sx = min(max(cx0 - 1 + c, 0), cw - 1);
-        const uint32_t v = gld<uint32_t>(P.src.data[1] + sf + (uint64_t)sy * P.src.pitch[1] +
-                                                                4 * sx);
-        cin[r][c] = make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f),
-                                (float)((int)(v >> 22) - 512) * (1.f / 896.f));
-    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (k < 2 || t + 512 < kCin)
+            (&cin[0][0])[t + 256 * k] = make_float2((float)((int)((vc[k] & 0xffffu) >> 6) - 512) * (1.f / 896.f),
+                                                     (float)((int)(vc[k] >> 22) - 512) * (1.f / 896.f));
     if (tile)                                       // top ring row = the previous tile's luma row y0 - 1
         for (int i = t; i < kTmLP; i += 256) cc[0][i] = cc[kTmLH - 2][i];
     __syncthreads();
+    // the next tile's loads fly during this tile's conversion
+    if (tile + 1 < kTmTiles && cy0 + kTmCRows < ch) fetch(tile + 1);
     // one luma pixel (clamped into the picture): zimg bilinear up (chroma location left:
     // columns j, j + 1 at weights 1 - fx, fx; rows k, k2 at 3/4, 1/4) + the conversion
-    auto pix = [&](int xr, int yr, float &Yv, float2 &C) {
+    auto pixc = [&](int xr, int yr, float y10, float &Yv, float2 &C) {
         const int x = min(max(xr, 0), P.w - 1), y = min(max(yr, 0), P.h - 1);
         const int ky = y >> 1, k = min(ky, ch - 1), k2 = min(max((y & 1) ? ky + 1 : ky - 1, 0), ch - 1);
         const int j = x >> 1, j1 = min(min(j + 1, cw - 1), cx0 + 64);   // (x even: j1 unused, fx = 0)
@@ -199,19 +269,16 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         const float2 a0 = cin[lk][lj], a1 = cin[lk][lj1], b0 = cin[lk2][lj], b1 = cin[lk2][lj1];
         const float2 c = make_float2(0.75f * (a0.x + fx * (a1.x - a0.x)) + 0.25f * (b0.x + fx * (b1.x - b0.x)),
                                      0.75f * (a0.y + fx * (a1.y - a0.y)) + 0.25f * (b0.y + fx * (b1.y - b0.y)));
-        const int y10 = (int)(gld<uint16_t>(P.src.data[0] + sf + (uint64_t)y * P.src.pitch[0] +
-                                                                  2 * x) >> 6);
-        pixel<MODE, DESAT>(P, tl, (float)y10, c, Yv, C);
+        pixel<MODE, DESAT>(P, tl, y10, c, Yv, C);
     };
-    if (a4 && x0 + 128 <= P.w && y0 + 16 <= P.h) {
+    if (blk) {
         // block path: the 2 x 2 luma block of chroma sample (cx0 + bxl, cy0 + byl); staged
         // rows byl .. byl + 2 = chroma rows by - 1 .. by + 1, columns bxl + 1, bxl + 2 = bx, bx + 1
 #if DTS_TM_UNROLL
 #pragma unroll
 #endif
         for (int kb = 0; kb < 64 * kTmCRows / 256; ++kb) {
-            const int i = t + 256 * kb;
-            const int byl = i >> 6, bxl = i & 63;
+            const int byl = byl0 + 4 * kb;
             const float2 m0 = cin[byl][bxl + 1], m1 = cin[byl][bxl + 2];
             const float2 a0 = cin[byl + 1][bxl + 1], a1 = cin[byl + 1][bxl + 2];
             const float2 p0 = cin[byl + 2][bxl + 1], p1 = cin[byl + 2][bxl + 2];
@@ -223,9 +290,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
                                  make_float2(0.75f * a0.x + 0.25f * p0.x, 0.75f * a0.y + 0.25f * p0.y),
                                  make_float2(0.75f * ah.x + 0.25f * ph.x, 0.75f * ah.y + 0.25f * ph.y)};
             const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
-            const uint64_t ys = P.src.data[0] + sf + (uint64_t)ya * P.src.pitch[0] + 2 * xa;
-            const uint32_t l0 = gld<uint32_t>(ys);
-            const uint32_t l1 = gld<uint32_t>(ys + P.src.pitch[0]);
+            const uint32_t l0 = l[2 * kb], l1 = l[2 * kb + 1];
             const float y10[4] = {(float)__builtin_amdgcn_ubfe(l0, 6, 10), (float)(l0 >> 22),
                                   (float)__builtin_amdgcn_ubfe(l1, 6, 10), (float)(l1 >> 22)};
             float Yv[4];
@@ -244,14 +309,17 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
         // per-pixel path (edge tiles): out-of-picture blocks keep the clamped values the
         // 2:1 filter of the last chroma row / column reads
         for (int i = t; i < 64 * kTmCRows; i += 256) {
-            const int byl = i >> 6, bxl = i & 63;
+            const int byl = i >> 6, bx = i & 63;
             float Yv[4];
             float2 C[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) pix(x0 + 2 * bxl + (q & 1), y0 + 2 * byl + (q >> 1), Yv[q], C[q]);
+            for (int q = 0; q < 4; ++q) {
+                const int xr = x0 + 2 * bx + (q & 1), yr = y0 + 2 * byl + (q >> 1);
+                pixc(xr, yr, luma_at(xr, yr), Yv[q], C[q]);
+            }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cc[1 + 2 * byl + (q >> 1)][2 + 2 * bxl + (q & 1)] = C[q];
-            const int xa = x0 + 2 * bxl, ya = y0 + 2 * byl;
+            for (int q = 0; q < 4; ++q) cc[1 + 2 * byl + (q >> 1)][2 + 2 * bx + (q & 1)] = C[q];
+            const int xa = x0 + 2 * bx, ya = y0 + 2 * byl;
             if (xa < P.w && ya < P.h) {                     // w, h even: the whole block is inside
                 const uint64_t yd = P.dst.data[0] + df + (uint64_t)ya * P.dst.pitch[0] + xa;
                 gst<uint16_t>(yd, (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)));
@@ -259,26 +327,16 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             }
         }
     }
-    // ... and the ring the 2:1 filter reads (chroma only): rows y0 - 1 (first tile only)
-    // and y0 + 16, columns x0 - 1 .. x0 + 127, and column x0 - 1 of the 16 rows between
-    {
-        constexpr int kRow = 129;
-        const int top = tile ? 0 : kRow;
-        for (int i = t; i < top + kRow + 2 * kTmCRows; i += 256) {
+    // ... and the ring the 2:1 filter reads (chroma only), in the same phase: item t with its
+    // luma fetched a tile ahead; the first tile's 274 items leave 18 for a second round
+    if (!(DTS_TM_ABLATE & 1)) {
+        const int top = tile ? 0 : kRow, nr = top + kRow + 2 * kTmCRows;
+        for (int i = t; i < nr; i += 256) {
             int lx, ly;
-            if (i < top) {
-                ly = 0;
-                lx = i;
-            } else if (i < top + kRow) {
-                ly = kTmLH - 1;
-                lx = i - top;
-            } else {
-                ly = 1 + (i - top - kRow);
-                lx = 0;
-            }
+            ring_at(i, top, lx, ly);
             float Yv;
             float2 C;
-            pix(x0 - 1 + lx, y0 - 1 + ly, Yv, C);
+            pixc(x0 - 1 + lx, y0 - 1 + ly, i == t ? yring : luma_at(x0 - 1 + lx, y0 - 1 + ly), Yv, C);
             cc[ly][1 + lx] = C;
         }
     }
@@ -286,7 +344,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     // chroma 2:1 (location left): columns 2 bx - 1 .. 2 bx + 1 (indices 2 rx + 1 .. 2 rx + 3),
     // rows 2 by - 1 .. 2 by + 2 (ring row 0 = y0 - 1)
     constexpr float wy[4] = {0.125f, 0.375f, 0.375f, 0.125f};
-    for (int i = t; i < 64 * kTmCRows; i += 256) {
+    for (int i = t; i < ((DTS_TM_ABLATE & 2) ? 0 : 64 * kTmCRows); i += 256) {
         const int ry = i >> 6, rx = i & 63;
         const int bx = cx0 + rx, by = cy0 + ry;
         if (bx >= cw || by >= ch) continue;
