@@ -634,7 +634,23 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
     const int t = threadIdx.x;
     const int total = P.tile_base[3];
     const int frame = blockIdx.x / total;
-    const int gt = blockIdx.x % total;
+    int gt = blockIdx.x % total;
+    if (P.interleaved && gt >= P.tile_base[1]) {
+        // nv12: the U and V tiles of one chroma tile read the same interleaved rows; dispatch
+        // them 8 workgroups apart (workgroups go round robin over the 8 XCDs) so the second
+        // read hits the L2 the first one filled: groups of 16 = 8 U tiles, then their V tiles
+        const int nc = P.tile_base[2] - P.tile_base[1], jc = gt - P.tile_base[1], g8 = nc & ~7;
+        int comp, pt;
+        if (jc < 2 * g8) {
+            comp = (jc >> 3) & 1;
+            pt = ((jc >> 4) << 3) + (jc & 7);
+        } else {
+            const int r = jc - 2 * g8, m = nc - g8;
+            comp = r >= m;
+            pt = g8 + (comp ? r - m : r);
+        }
+        gt = (comp ? P.tile_base[2] : P.tile_base[1]) + pt;
+    }
     const int plane = gt >= P.tile_base[2] ? 2 : (gt >= P.tile_base[1] ? 1 : 0);
     const int tile = gt - P.tile_base[plane];
     const int tx = tile % P.tiles_x[plane], ty = tile / P.tiles_x[plane];
