@@ -1432,9 +1432,11 @@ static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, co
     q.pw[1] = q.pw[2] = (w + 1) >> 1;
     q.ph[1] = q.ph[2] = (h + 1) >> 1;
     int total = 0;
+    q.walk = fmt == DTS_FMT_NV12 ? kQWalkNV12 : kQWalk;
     for (int p = 0; p < 3; ++p) {
-        q.tiles_x[p] = (q.pw[p] + 4 * kQTileBX - 1) / (4 * kQTileBX);
-        q.tiles_y[p] = (q.ph[p] + 4 * kQTileBY - 1) / (4 * kQTileBY);
+        q.tbx[p] = fmt == DTS_FMT_NV12 && p > 0 ? kQTileBX / 2 : kQTileBX;
+        q.tiles_x[p] = (q.pw[p] + 4 * q.tbx[p] - 1) / (4 * q.tbx[p]);
+        q.tiles_y[p] = (q.ph[p] + 4 * kQTileBY * q.walk - 1) / (4 * kQTileBY * q.walk);
         q.tile_base[p] = total;
         total += q.tiles_x[p] * q.tiles_y[p];
     }

@@ -407,13 +407,23 @@ void ladder7_compiled(int *stages, int *batch, int *decouple);   // NS7 / PB7 / 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry
 // ---------------------------------------------------------------------------
-constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x
+constexpr int kQTileBX = 64;        // 4x4 blocks per tile, x (nv12 chroma: 32, the same bytes per row)
 constexpr int kQTileBY = 16;        // 4x4 blocks per tile, y
+#ifndef DTS_Q_WALK
+#define DTS_Q_WALK 4
+#endif
+#ifndef DTS_Q_WALK_NV12
+#define DTS_Q_WALK_NV12 DTS_Q_WALK
+#endif
+constexpr int kQWalk = DTS_Q_WALK;  // tiles per k_quality workgroup, walked top to bottom
+constexpr int kQWalkNV12 = DTS_Q_WALK_NV12;   // the same for nv12 renditions
 
 struct QualityParams {
     DevPlanes a, b;
     int32_t pw[3], ph[3];           // plane sizes
-    int32_t tiles_x[3], tiles_y[3];
+    int32_t tbx[3];                 // tile width in blocks (kQTileBX; nv12 chroma kQTileBX / 2)
+    int32_t tiles_x[3], tiles_y[3]; // tiles_y: walks of `walk` tiles
+    int32_t walk;                   // tiles per walk (kQWalk / kQWalkNV12)
     int32_t tile_base[4];           // prefix of tiles per plane
     int32_t interleaved;            // 1 = nv12 (plane 1 holds U,V interleaved)
     int32_t nframes;

@@ -597,12 +597,19 @@ int ladder_blocks_per_cu(int src_kind, int ndmax, int lds_bytes)
 }
 
 // ---------------------------------------------------------------------------
-// k_quality: vf_psnr + vf_ssim partials.  One workgroup per (frame, plane,
-// tile of 64x16 4x4-blocks).  Block sums (s1, s2, ss, s12) of the tile plus a
-// one-block apron go to LDS; each owned block adds ss - 2*s12 = sum((a-b)^2)
-// to the SSE; each 8x8 window (2x2 blocks at stride 4) evaluates ssim_end1 in
-// f32 exactly as vf_ssim.c and accumulates in f64.  Pixels outside whole
-// blocks (plane width/height not multiples of 4) add to the SSE directly.
+// k_quality: vf_psnr + vf_ssim partials.  One workgroup per (frame, plane, walk):
+// a column strip of TBX 4x4 blocks (64; nv12 chroma 32 -- 256 bytes of a row either
+// way) walked down kQWalk tiles of 16 block rows.  Per tile a thread owns one item: 4
+// (nv12 chroma 2) blocks of one block row, loaded as one 16-byte segment per pixel row
+// and image a tile ahead of their use; the blocks' sums (s1, s2, ss, s12) go to a
+// circular LDS image of 17 block rows (the previous tile's last row is carried, never
+// re-read); each owned block adds ss - 2*s12 = sum((a-b)^2) to the SSE; each 8x8
+// window (2x2 blocks at stride 4) whose top block row lies in the walk evaluates
+// ssim_end1 in f32 exactly as vf_ssim.c and accumulates in f64.  The strip's right
+// apron column and the walk's bottom apron row are read once.  Pixels outside whole
+// blocks (plane width/height not multiples of 4) add to the SSE directly.  An nv12
+// chroma workgroup scores U and V from one read of the interleaved rows (two block
+// images side by side in LDS; its partials go to the tile of plane 1 and of plane 2).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float ssim_end1(int s1, int s2, int ss, int s12)
 {
@@ -626,169 +633,214 @@ __device__ __forceinline__ int load1(const uint8_t *row, int x, bool inter, int 
     return inter ? row[2 * x + comp] : row[x];
 }
 
-__global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P)
+__device__ __forceinline__ int4 sums4(const uint32_t (&va)[4], const uint32_t (&vb)[4])
 {
-    __shared__ int4 bs[kQTileBY + 1][kQTileBX + 1];
-    __shared__ double red_s[kThreads / 64];
-    __shared__ unsigned long long red_e[kThreads / 64];
+    uint32_t s1 = 0, s2 = 0, ss = 0, s12 = 0;
+#pragma unroll
+    for (int yy = 0; yy < 4; ++yy) {
+        s1 = __builtin_amdgcn_udot4(va[yy], 0x01010101u, s1, false);
+        s2 = __builtin_amdgcn_udot4(vb[yy], 0x01010101u, s2, false);
+        ss = __builtin_amdgcn_udot4(va[yy], va[yy], ss, false);
+        ss = __builtin_amdgcn_udot4(vb[yy], vb[yy], ss, false);
+        s12 = __builtin_amdgcn_udot4(va[yy], vb[yy], s12, false);
+    }
+    return make_int4((int)s1, (int)s2, (int)ss, (int)s12);
+}
+
+#ifndef DTS_Q_PREFETCH
+#define DTS_Q_PREFETCH 1    // 0: a tile's rows loaded when the tile starts (fewer VGPRs; A/B knob)
+#endif
+
+// INTER: nv12 chroma workgroups (tiles of plane 1 scoring U and V); else one plane each
+template <bool INTER>
+__global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int gt0, int ngt)
+{
+    constexpr int RB = kQTileBY + 1;                // circular block rows: the carried row + one tile
+    constexpr int BW = kQTileBX + 2;                // columns: TBX + 1 (nv12 chroma: 2 x (TBX + 1))
+    __shared__ int4 bs[RB + 1][BW];                 // + the walk's apron row below (row RB)
+    __shared__ double red_s[2][kThreads / 64];
+    __shared__ unsigned long long red_e[2][kThreads / 64];
     const int t = threadIdx.x;
     const int total = P.tile_base[3];
-    const int frame = blockIdx.x / total;
-    int gt = blockIdx.x % total;
-    if (P.interleaved && gt >= P.tile_base[1]) {
-        // nv12: the U and V tiles of one chroma tile read the same interleaved rows; dispatch
-        // them 8 workgroups apart (workgroups go round robin over the 8 XCDs) so the second
-        // read hits the L2 the first one filled: groups of 16 = 8 U tiles, then their V tiles
-        const int nc = P.tile_base[2] - P.tile_base[1], jc = gt - P.tile_base[1], g8 = nc & ~7;
-        int comp, pt;
-        if (jc < 2 * g8) {
-            comp = (jc >> 3) & 1;
-            pt = ((jc >> 4) << 3) + (jc & 7);
-        } else {
-            const int r = jc - 2 * g8, m = nc - g8;
-            comp = r >= m;
-            pt = g8 + (comp ? r - m : r);
-        }
-        gt = (comp ? P.tile_base[2] : P.tile_base[1]) + pt;
-    }
+    const int frame = blockIdx.x / ngt;
+    const int gt = gt0 + blockIdx.x % ngt;
     const int plane = gt >= P.tile_base[2] ? 2 : (gt >= P.tile_base[1] ? 1 : 0);
     const int tile = gt - P.tile_base[plane];
-    const int tx = tile % P.tiles_x[plane], ty = tile / P.tiles_x[plane];
+    const int tx = tile % P.tiles_x[plane], tw = tile / P.tiles_x[plane];
     const int w = P.pw[plane], h = P.ph[plane];
     const int W4 = w >> 2, H4 = h >> 2;
-    const int bx0 = tx * kQTileBX, by0 = ty * kQTileBY;
-    const bool inter = P.interleaved && plane > 0;
-    const int comp = plane == 2 ? 1 : 0;
+    const int TBX = P.tbx[plane];
+    const int bx0 = tx * TBX;
+    constexpr bool inter = INTER;
+    constexpr int NC = INTER ? 2 : 1;               // components scored: U and V of nv12 chroma
     const int dp = inter ? 1 : plane;
     const uint8_t *A = reinterpret_cast<const uint8_t *>(P.a.data[dp]) + (int64_t)frame * P.a.fstride;
     const uint8_t *B = reinterpret_cast<const uint8_t *>(P.b.data[dp]) + (int64_t)frame * P.b.fstride;
     const int64_t pa = P.a.pitch[dp], pb = P.b.pitch[dp];
-
-    unsigned long long sse = 0;
-    // the 4x4 block's sums by v_dot4_u32_u8 (four byte products per instruction;
-    // exact: ss <= 16 * 2 * 255^2)
-    auto block = [&](int bx, int by) {
-        const int gx = bx0 + bx, gy = by0 + by;
-        int4 r = make_int4(0, 0, 0, 0);
-        if (gx < W4 && gy < H4) {
-            uint32_t s1 = 0, s2 = 0, ss = 0, s12 = 0;
-#pragma unroll
-            for (int yy = 0; yy < 4; ++yy) {
-                const uint32_t va = load4(A + (int64_t)(4 * gy + yy) * pa, 4 * gx, inter, comp);
-                const uint32_t vb = load4(B + (int64_t)(4 * gy + yy) * pb, 4 * gx, inter, comp);
-                s1 = __builtin_amdgcn_udot4(va, 0x01010101u, s1, false);
-                s2 = __builtin_amdgcn_udot4(vb, 0x01010101u, s2, false);
-                ss = __builtin_amdgcn_udot4(va, va, ss, false);
-                ss = __builtin_amdgcn_udot4(vb, vb, ss, false);
-                s12 = __builtin_amdgcn_udot4(va, vb, s12, false);
-            }
-            r = make_int4((int)s1, (int)s2, (int)ss, (int)s12);
-            if (bx < kQTileBX && by < kQTileBY) sse += (unsigned long long)((int)ss - 2 * (int)s12);
-        }
-        bs[by][bx] = r;
-    };
-    // 16-pixel runs of 4 blocks along a block row: one 16-byte load per row and image
-    // (interleaved chroma: two, de-interleaved by v_perm), then the apron column
-    constexpr int NQ = kQTileBX / 4;
     const bool vec16 = (((uintptr_t)A | (uintptr_t)B | (uint64_t)pa | (uint64_t)pb) & 15) == 0;
-    for (int i = t; i < (kQTileBY + 1) * (NQ + 1); i += kThreads) {
-        const int by = i / (NQ + 1), qx = i - by * (NQ + 1);
-        if (qx == NQ) {
-            block(kQTileBX, by);
-            continue;
-        }
-        const int gx = bx0 + 4 * qx, gy = by0 + by;
-        if (gy >= H4 || gx + 3 >= W4 || !vec16) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) block(4 * qx + k, by);
-            continue;
-        }
-        uint32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, ss[4] = {0, 0, 0, 0}, s12[4] = {0, 0, 0, 0};
+    constexpr int NB = INTER ? 2 : 4;               // blocks per item: 16 bytes of an image row
+    const int iby = t >> 4, iq = t & 15;            // item: blocks NB iq .. NB iq + NB - 1 of block row iby
+    const int by00 = tw * P.walk * kQTileBY;        // first block row of the walk
+    const int nk = min(P.walk, (h - 4 * by00 + 4 * kQTileBY - 1) / (4 * kQTileBY));
+
+    unsigned long long sse[2] = {0, 0};
+    double ssim[2] = {0.0, 0.0};
+    // one block by 4-byte loads (edges, the apron column, unaligned planes); zero outside
+    auto block = [&](int gx, int gy, int comp) {
+        if (gx >= W4 || gy >= H4 || gx < 0) return make_int4(0, 0, 0, 0);
+        uint32_t va[4], vb[4];
 #pragma unroll
         for (int yy = 0; yy < 4; ++yy) {
-            const uint8_t *ra = A + (int64_t)(4 * gy + yy) * pa, *rb = B + (int64_t)(4 * gy + yy) * pb;
-            uint32_t va[4], vb[4];
-            if (!inter) {
-                const uint4 x = *reinterpret_cast<const uint4 *>(ra + 4 * gx);
-                const uint4 y = *reinterpret_cast<const uint4 *>(rb + 4 * gx);
-                va[0] = x.x; va[1] = x.y; va[2] = x.z; va[3] = x.w;
-                vb[0] = y.x; vb[1] = y.y; vb[2] = y.z; vb[3] = y.w;
-            } else {
-                const uint4 x0 = *reinterpret_cast<const uint4 *>(ra + 8 * gx);
-                const uint4 x1 = *reinterpret_cast<const uint4 *>(ra + 8 * gx + 16);
-                const uint4 y0 = *reinterpret_cast<const uint4 *>(rb + 8 * gx);
-                const uint4 y1 = *reinterpret_cast<const uint4 *>(rb + 8 * gx + 16);
-                const uint32_t sel = comp ? 0x07050301u : 0x06040200u;
-                va[0] = perm(x0.y, x0.x, sel); va[1] = perm(x0.w, x0.z, sel);
-                va[2] = perm(x1.y, x1.x, sel); va[3] = perm(x1.w, x1.z, sel);
-                vb[0] = perm(y0.y, y0.x, sel); vb[1] = perm(y0.w, y0.z, sel);
-                vb[2] = perm(y1.y, y1.x, sel); vb[3] = perm(y1.w, y1.z, sel);
+            va[yy] = load4(A + (int64_t)(4 * gy + yy) * pa, 4 * gx, inter, comp);
+            vb[yy] = load4(B + (int64_t)(4 * gy + yy) * pb, 4 * gx, inter, comp);
+        }
+        return sums4(va, vb);
+    };
+    // the item's 4 pixel rows, both images, one 16-byte load each (when the item is whole)
+    uint4 ra[4], rb[4];
+    auto fetch = [&](int by0) {
+        const int gx = bx0 + NB * iq, gy = by0 + iby;
+        if (vec16 && gy < H4 && gx + NB <= W4) {
+#pragma unroll
+            for (int yy = 0; yy < 4; ++yy) {
+                ra[yy] = *reinterpret_cast<const uint4 *>(A + (int64_t)(4 * gy + yy) * pa + 4 * (inter ? 2 : 1) * gx);
+                rb[yy] = *reinterpret_cast<const uint4 *>(B + (int64_t)(4 * gy + yy) * pb + 4 * (inter ? 2 : 1) * gx);
             }
+        }
+    };
+    // the item's block sums into LDS row `row` (+ SSE of blocks inside the plane); slot
+    // k of 4: block NB iq + (k mod NB) of component k / NB (nv12 chroma: U U V V)
+    auto put = [&](int by0, int row) {
+        const int gx = bx0 + NB * iq, gy = by0 + iby;
+        if (vec16 && gy < H4 && gx + NB <= W4) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                s1[k] = __builtin_amdgcn_udot4(va[k], 0x01010101u, s1[k], false);
-                s2[k] = __builtin_amdgcn_udot4(vb[k], 0x01010101u, s2[k], false);
-                ss[k] = __builtin_amdgcn_udot4(va[k], va[k], ss[k], false);
-                ss[k] = __builtin_amdgcn_udot4(vb[k], vb[k], ss[k], false);
-                s12[k] = __builtin_amdgcn_udot4(va[k], vb[k], s12[k], false);
+                const int c = inter ? k >> 1 : 0, kb = inter ? k & 1 : k;
+                const uint32_t sel = c ? 0x07050301u : 0x06040200u;
+                uint32_t va[4], vb[4];
+#pragma unroll
+                for (int yy = 0; yy < 4; ++yy) {
+                    if (inter) {
+                        va[yy] = perm(kb ? ra[yy].w : ra[yy].y, kb ? ra[yy].z : ra[yy].x, sel);
+                        vb[yy] = perm(kb ? rb[yy].w : rb[yy].y, kb ? rb[yy].z : rb[yy].x, sel);
+                    } else {
+                        va[yy] = k == 0 ? ra[yy].x : k == 1 ? ra[yy].y : k == 2 ? ra[yy].z : ra[yy].w;
+                        vb[yy] = k == 0 ? rb[yy].x : k == 1 ? rb[yy].y : k == 2 ? rb[yy].z : rb[yy].w;
+                    }
+                }
+                const int4 r = sums4(va, vb);
+                bs[row][c * (TBX + 1) + NB * iq + kb] = r;
+                sse[c] += (unsigned long long)(r.z - 2 * r.w);
+            }
+        } else {
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const int c = inter ? k >> 1 : 0, kb = inter ? k & 1 : k;
+                const int4 r = block(gx + kb, gy, c + (plane == 2));
+                bs[row][c * (TBX + 1) + NB * iq + kb] = r;
+                if (gx + kb < W4 && gy < H4) sse[c] += (unsigned long long)(r.z - 2 * r.w);
             }
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            bs[by][4 * qx + k] = make_int4((int)s1[k], (int)s2[k], (int)ss[k], (int)s12[k]);
-            if (by < kQTileBY) sse += (unsigned long long)((int)ss[k] - 2 * (int)s12[k]);
-        }
-    }
-    // pixels outside whole blocks, inside this tile's pixel rectangle
-    {
-        const int px0 = tx * 4 * kQTileBX, py0 = ty * 4 * kQTileBY;
-        const int px1 = min(w, px0 + 4 * kQTileBX), py1 = min(h, py0 + 4 * kQTileBY);
-        // right strip: x >= 4*W4, y < 4*H4
-        const int ax0 = max(px0, 4 * W4), ay1 = min(py1, 4 * H4);
+    };
+    // pixels outside whole blocks, inside the tile's pixel rectangle
+    auto strips = [&](int py0) {
+        const int px0 = 4 * bx0;
+        const int px1 = min(w, px0 + 4 * TBX), py1 = min(h, py0 + 4 * kQTileBY);
+        const int ax0 = max(px0, 4 * W4), ay1 = min(py1, 4 * H4);     // right strip: x >= 4 W4, y < 4 H4
         const int aw = max(0, px1 - ax0), ah = max(0, ay1 - py0);
         for (int i = t; i < aw * ah; i += kThreads) {
             const int y = py0 + i / aw, x = ax0 + i % aw;
-            const int d = load1(A + (int64_t)y * pa, x, inter, comp) - load1(B + (int64_t)y * pb, x, inter, comp);
-            sse += (unsigned long long)(d * d);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int d = load1(A + (int64_t)y * pa, x, inter, c + (plane == 2)) -
+                              load1(B + (int64_t)y * pb, x, inter, c + (plane == 2));
+                sse[c] += (unsigned long long)(d * d);
+            }
         }
-        // bottom strip: y >= 4*H4
-        const int by0p = max(py0, 4 * H4);
+        const int by0p = max(py0, 4 * H4);                             // bottom strip: y >= 4 H4
         const int bw = max(0, px1 - px0), bh = max(0, py1 - by0p);
         for (int i = t; i < bw * bh; i += kThreads) {
             const int y = by0p + i / bw, x = px0 + i % bw;
-            const int d = load1(A + (int64_t)y * pa, x, inter, comp) - load1(B + (int64_t)y * pb, x, inter, comp);
-            sse += (unsigned long long)(d * d);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int d = load1(A + (int64_t)y * pa, x, inter, c + (plane == 2)) -
+                              load1(B + (int64_t)y * pb, x, inter, c + (plane == 2));
+                sse[c] += (unsigned long long)(d * d);
+            }
         }
+    };
+    // windows with top rows r0 .. r1 - 1 of the circular image (base b: top block row by0 - 1 + r)
+    auto windows = [&](int by0, int b, int r0, int r1, bool apron_row) {
+        const int rw = NC * TBX, nw = (r1 - r0) * rw;
+#pragma unroll 1
+        for (int i = t; i < nw; i += kThreads) {
+            const int r = r0 + i / rw, cx = i % rw, c = cx >= TBX, wx = cx - c * TBX;
+            if (bx0 + wx < W4 - 1 && by0 - 1 + r < H4 - 1) {
+                const int l0 = (b + r) % RB, l1 = apron_row ? RB : (b + r + 1) % RB, x = c * (TBX + 1) + wx;
+                const int4 p = bs[l0][x], q = bs[l0][x + 1], u = bs[l1][x], v = bs[l1][x + 1];
+                const double e = (double)ssim_end1(p.x + q.x + u.x + v.x, p.y + q.y + u.y + v.y,
+                                                   p.z + q.z + u.z + v.z, p.w + q.w + u.w + v.w);
+                if (NC == 1) {
+                    ssim[0] += e;
+                } else {
+                    ssim[0] += c ? 0.0 : e;
+                    ssim[1] += c ? e : 0.0;
+                }
+            }
+        }
+    };
+    if (DTS_Q_PREFETCH) fetch(by00);
+    int b = 0;                                      // circular base: the carried row
+    for (int k = 0; k < nk; ++k) {
+        const int by0 = by00 + k * kQTileBY;
+        if (!DTS_Q_PREFETCH) fetch(by0);
+        if (k) __syncthreads();                     // the previous windows are done with the rows
+        put(by0, (b + 1 + iby) % RB);
+        if (t < NC * kQTileBY) {                    // the apron column: block TBX of block row t
+            const int c = t >= kQTileBY, r = t - c * kQTileBY;
+            bs[(b + 1 + r) % RB][c * (TBX + 1) + TBX] = block(bx0 + TBX, by0 + r, c + (plane == 2));
+        }
+        strips(4 * by0);
+        __syncthreads();
+        if (DTS_Q_PREFETCH && k + 1 < nk) fetch(by0 + kQTileBY);   // the next tile's rows fly during the windows
+        windows(by0, b, k ? 0 : 1, kQTileBY, false);
+        b = (b + kQTileBY) % RB;                    // this tile's last row is the next tile's carried row
     }
-    __syncthreads();
-    double ssim = 0.0;
-    for (int i = t; i < kQTileBY * kQTileBX; i += kThreads) {
-        const int wy = i / kQTileBX, wx = i - wy * kQTileBX;
-        if (bx0 + wx < W4 - 1 && by0 + wy < H4 - 1) {
-            const int4 p = bs[wy][wx], q = bs[wy][wx + 1], r = bs[wy + 1][wx], s = bs[wy + 1][wx + 1];
-            ssim += (double)ssim_end1(p.x + q.x + r.x + s.x, p.y + q.y + r.y + s.y, p.z + q.z + r.z + s.z,
-                                      p.w + q.w + r.w + s.w);
+    {   // the apron row below the walk: windows with top row at the walk's last block row
+        const int by0 = by00 + nk * kQTileBY;       // (b now holds that row)
+        if (by0 < H4) {
+            __syncthreads();
+            for (int i = t; i < NC * (TBX + 1); i += kThreads) {
+                const int c = i > TBX, x = i - c * (TBX + 1);
+                bs[RB][i] = block(bx0 + x, by0, c + (plane == 2));
+            }
+            __syncthreads();
+            windows(by0 + 1, b, 0, 1, true);
         }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ssim += __shfl_xor(ssim, o);
-        sse += __shfl_xor(sse, o);
-    }
-    if ((t & 63) == 0) {
-        red_s[t >> 6] = ssim;
-        red_e[t >> 6] = sse;
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            ssim[c] += __shfl_xor(ssim[c], o);
+            sse[c] += __shfl_xor(sse[c], o);
+        }
+        if ((t & 63) == 0) {
+            red_s[c][t >> 6] = ssim[c];
+            red_e[c][t >> 6] = sse[c];
+        }
     }
     __syncthreads();
-    if (t == 0) {
+    if (t < NC) {
         double s = 0;
         unsigned long long e = 0;
         for (int i = 0; i < kThreads / 64; ++i) {
-            s += red_s[i];
-            e += red_e[i];
+            s += red_s[t][i];
+            e += red_e[t][i];
         }
-        P.partial_ssim[(int64_t)frame * total + gt] = s;
-        P.partial_sse[(int64_t)frame * total + gt] = e;
+        const int g = gt + t * (P.tile_base[2] - P.tile_base[1]);      // V: the same tile of plane 2
+        P.partial_ssim[(int64_t)frame * total + g] = s;
+        P.partial_sse[(int64_t)frame * total + g] = e;
     }
 }
 
@@ -867,7 +919,15 @@ hipError_t launch_qsum(const dts_qraw *raw, int n, dts_qraw *sum, hipStream_t s)
 
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_quality, dim3((unsigned)(total_tiles * p.nframes)), dim3(kThreads), 0, s, p);
+    if (!p.interleaved) {
+        hipLaunchKernelGGL(k_quality<false>, dim3((unsigned)(total_tiles * p.nframes)), dim3(kThreads), 0, s, p, 0,
+                           total_tiles);
+    } else {                                        // nv12: plane 1's workgroups score plane 2 as well
+        const int nl = p.tile_base[1], nc = p.tile_base[2] - p.tile_base[1];
+        hipLaunchKernelGGL(k_quality<false>, dim3((unsigned)(nl * p.nframes)), dim3(kThreads), 0, s, p, 0, nl);
+        if (nc > 0 && hipPeekAtLastError() == hipSuccess)
+            hipLaunchKernelGGL(k_quality<true>, dim3((unsigned)(nc * p.nframes)), dim3(kThreads), 0, s, p, nl, nc);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_qreduce, dim3((unsigned)(3 * p.nframes)), dim3(kThreads), 0, s, p);
