@@ -63,8 +63,8 @@ WORKLOADS = {
                      "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB)"},
     "cfg4": {"src": (7680, 4320, D.FMT_YUV420P), "outs": [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)],
              "tonemap": None, "quality": True, "batch": 64,
-             "desc": "cfg4: 8K30 yuv420p -> 4K lanczos + per-frame vf_psnr/vf_ssim of the output vs a 4K "
-                     "reference"},
+             "desc": "cfg4: 8K30 yuv420p -> 4K lanczos + per-frame vf_psnr/vf_ssim of the output vs its own 4K "
+                     "reference frame (a device-resident reference ring as long as the source ring)"},
     # BASELINE config 5 on one GPU: a step is one 600-frame segment of the cfg2 ladder plus
     # vf_psnr/vf_ssim of every rendition against a reference rendition of the same size
     # (the source scaled with lanczos: computed once, outside the timed region); the
@@ -431,7 +431,7 @@ def main():
     yadif = wl.get("yadif")
     if yadif is None:
         # cfg5: every rendition scored against its reference batch (DTS_QREF_EXTERNAL), in the graph:
-        # vf_psnr / vf_ssim fused into the ladder kernel's V epilogue
+        # the ladder launch, then the k_quality pass over each rendition and its reference
         gouts = [(w, h, fmt, m, None, (D.Q_BOTH, D.QREF_EXTERNAL)) if rungq else (w, h, fmt, m)
                  for (w, h, fmt, m) in wl["outs"]]
         g = D.Graph(ctx, D.make_spec(sw, sh, sfmt, gouts, quality=D.Q_BOTH if wl["quality"] else D.Q_NONE,
@@ -457,12 +457,14 @@ def main():
         outs.append(t)
         ods.append(d)
     qref = qrd = qraw = None
-    if wl["quality"]:                      # the 4K reference the output is scored against (one frame, reused)
+    if wl["quality"]:
+        # cfg4: every source frame has its own 4K reference frame (reference i = synthetic frame
+        # first + i, seed 0x0EF), a device-resident ring as long as the source ring (R x 12.6 MB
+        # >> the 256 MB Infinity Cache): the reference streams from HBM like the source does
         w, h, fmt, _m = wl["outs"][0]
-        qref = torch.empty((B, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
+        qref = torch.empty((R, frame_bytes(w, h, fmt)), dtype=torch.uint8, device=dev)
         qrd, _ = dev_batch(qref, w, h, fmt)
-        qrd.frame_stride = 0
-        ctx.synth_device(w, h, fmt, 0, 0x0EF, 0, qrd, 1, sptr)
+        ctx.synth_device(w, h, fmt, 0, 0x0EF, first, qrd, R, sptr)
         qraw = torch.zeros((B, ctypes.sizeof(D.QRaw)), dtype=torch.uint8, device=dev)
 
     # cfg5: reference renditions (the ring scaled with lanczos) and per-rung quality records
@@ -505,14 +507,17 @@ def main():
         dd.frame_stride = d.frame_stride
         return dd
 
-    def batch_src(step):
+    def ring_at(ring, step):
         i0 = (step * B) % R
         d = D.DevFrames()
         for p in range(3):
-            d.data[p] = (sd.data[p] or 0) + i0 * sd.frame_stride
-            d.pitch[p] = sd.pitch[p]
-        d.frame_stride = sd.frame_stride
+            d.data[p] = (ring.data[p] or 0) + i0 * ring.frame_stride if ring.data[p] else None
+            d.pitch[p] = ring.pitch[p]
+        d.frame_stride = ring.frame_stride
         return d
+
+    def batch_src(step):
+        return ring_at(sd, step)
 
     def step(i):
         if g is None:                      # prev/next of the batch's frames come from the same ring
@@ -522,8 +527,8 @@ def main():
             g.run_device(batch_src(i), B, ods, qref=[qref_batch(k, i) for k in range(len(ods))],
                          qraw_ptr=qall.data_ptr(), stream=sptr)
         else:
-            g.run_device(batch_src(i), B, ods, qref=qrd, qraw_ptr=qraw.data_ptr() if qraw is not None else 0,
-                         stream=sptr)
+            g.run_device(batch_src(i), B, ods, qref=ring_at(qrd, i) if qrd is not None else None,
+                         qraw_ptr=qraw.data_ptr() if qraw is not None else 0, stream=sptr)
         if rungq:
             # the segment's record (computed in warmup too, so torch's reduction kernels are
             # loaded before the timed region)
@@ -566,9 +571,9 @@ def main():
     if rank == 0 and not args.no_verify:
         last = args.warmup + args.steps - 1
         qhost = None
-        if wl["quality"]:
+        if wl["quality"]:                  # the reference of the batch's frame 0
             w, h, fmt, _m = wl["outs"][0]
-            qhost = D.synth_host(w, h, fmt, 0, 0x0EF, 0)
+            qhost = D.synth_host(w, h, fmt, 0, 0x0EF, first + (last * B) % R)
         verified = verify_first_frame(wl, first + (last * B) % R, outs, qhost, qraw, ring_first=first,
                                       rung_qraws=qraws if rungq else None)
     if rank == 0:
@@ -601,6 +606,12 @@ def main():
         }
         if jq is not None:
             line["quality"] = jq
+        if wl["quality"]:
+            # cfg4: the three streams of the algorithmic bytes, per frame (the reference now streams
+            # from HBM too: one distinct reference frame per source frame)
+            rb = g.info.out_frame_bytes[0]
+            line["roofline"]["bytes_per_frame_split"] = {
+                "source_read": g.info.src_frame_bytes, "output_write": rb, "reference_read": rb}
         if world == 1 and not args.no_cpu:
             threads = cpu_share()
             line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, threads)

@@ -716,8 +716,43 @@ static napi_value js_fps_map(napi_env env, napi_callback_info info)
     return arr;
 }
 
+/* The library this addon loads must have the ABI and struct layouts of the header it was
+ * compiled against (dts.h DTS_ABI_VERSION); a mismatch would pass misaligned specs. */
+static int abi_mismatch(char *msg, size_t cap)
+{
+    static const struct { int id; int64_t size; const char *name; } st[] = {
+        {DTS_STRUCT_TONEMAP_SPEC, (int64_t)sizeof(dts_tonemap_spec), "dts_tonemap_spec"},
+        {DTS_STRUCT_OUTPUT_SPEC, (int64_t)sizeof(dts_output_spec), "dts_output_spec"},
+        {DTS_STRUCT_GRAPH_SPEC, (int64_t)sizeof(dts_graph_spec), "dts_graph_spec"},
+        {DTS_STRUCT_FRAME, (int64_t)sizeof(dts_frame), "dts_frame"},
+        {DTS_STRUCT_DEV_FRAMES, (int64_t)sizeof(dts_dev_frames), "dts_dev_frames"},
+        {DTS_STRUCT_QRAW, (int64_t)sizeof(dts_qraw), "dts_qraw"},
+        {DTS_STRUCT_QSTAT, (int64_t)sizeof(dts_qstat), "dts_qstat"},
+        {DTS_STRUCT_GRAPH_INFO, (int64_t)sizeof(dts_graph_info), "dts_graph_info"},
+    };
+    const int v = dts_abi_version();
+    if (v != DTS_ABI_VERSION) {
+        snprintf(msg, cap, "libdts ABI %d, the addon was built for ABI %d", v, DTS_ABI_VERSION);
+        return 1;
+    }
+    for (size_t i = 0; i < sizeof st / sizeof st[0]; ++i) {
+        const int64_t n = dts_abi_struct_size(st[i].id);
+        if (n != st[i].size) {
+            snprintf(msg, cap, "libdts sizeof(%s) = %lld, the addon's %lld", st[i].name, (long long)n,
+                     (long long)st[i].size);
+            return 1;
+        }
+    }
+    return 0;
+}
+
 static napi_value init(napi_env env, napi_value exports)
 {
+    char msg[160];
+    if (abi_mismatch(msg, sizeof msg)) {
+        napi_throw_error(env, "DTS_ABI", msg);
+        return NULL;
+    }
     napi_property_descriptor props[] = {
         {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
         {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_default, NULL},

@@ -67,10 +67,10 @@ constexpr int kSwsAccurateRnd = 0x40000;
 constexpr int kQueueSlots = 64;
 constexpr int kQueueWidth = 8;            // counters per slot: one per XCD for k_ladder4
 
-// k_ladder4 work queues: one per XCD unless DTS_XCD=0 (A/B runs)
+// k_ladder4 work queues: one per XCD unless DTS_XCD=0 (diagnostic A/B builds)
 int ladder4_queues()
 {
-    const char *f = std::getenv("DTS_XCD");
+    const char *f = diag_env("DTS_XCD");
     return (f && f[0] == '0') ? 1 : kQueueWidth;
 }
 constexpr int kSwsBitexact = 0x80000;
@@ -196,13 +196,7 @@ struct dts_graph {
     const Unit7 *dev_units7 = nullptr;
     const uint32_t *dev_frag7 = nullptr;
     const int32_t *dev_fire7 = nullptr;
-    const FragOp7 *dev_fsched7 = nullptr;
     int ngroups7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
-    // fused quality (GraphPlan::qf): the per (rendition, plane) unit lists and boundaries
-    bool qf7 = false;
-    const QRend7 *dev_qrend7 = nullptr;
-    const int32_t *dev_qunit7 = nullptr, *dev_qbound7 = nullptr;
-    int nqrend7 = 0, nunits7 = 0, nqbound7 = 0, qmax_h4 = 0;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -222,22 +216,12 @@ struct dts_graph {
     dts_qstat *p_q = nullptr;
     int p_chunk_first[2] = {-1, -1}, p_chunk_n[2] = {0, 0};
     // HDR10 -> SDR: per output a p010 intermediate of `batch` frames, double-buffered
-    // (an event per buffer orders reuse across streams)
+    // (an event per buffer orders reuse across the host path's two streams)
     bool hdr = false;
     DevLayout lay_mid[DTS_MAX_OUTPUTS];
     uint8_t *hdr_mid[2][DTS_MAX_OUTPUTS] = {};
     hipEvent_t hdr_ev[2] = {nullptr, nullptr};   // k_tonemap done reading intermediate sl
-    hipEvent_t hdr_mid_ev[2] = {nullptr, nullptr};   // the ladder wrote intermediate sl
-    hipEvent_t hdr_go = nullptr, hdr_end = nullptr;
-    // the separate quality pass on its own stream (DTS_QSTREAM): k_quality of chunk i beside the
-    // ladder of chunk i + 1 (qs_ev[i % kQEv]: chunk i's outputs are written)
-    static constexpr int kQEv = 8;
-    hipStream_t q_st = nullptr;
-    hipEvent_t q_ev[kQEv] = {}, q_go = nullptr, q_end = nullptr;
-    unsigned q_next = 0;
-    hipStream_t hdr_tm = nullptr;         // k_tonemap's own stream: the ladder of chunk i + 1 runs
-                                          // beside the tonemap of chunk i (nullptr: one stream)
-    int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk
+    int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk (the graph's batch)
     unsigned hdr_next = 0;
     TonemapParams tm{};
     float *dev_tm_lut = nullptr;          // the transfer-curve tables of tm (TonemapParams::lut)
@@ -459,7 +443,6 @@ struct GraphPlan {
     std::vector<Job5> jobs5;
     int lds5 = 0;
     bool v7 = false;                      // ... and on k_ladder7 where frames are 16-byte aligned
-    bool qf = false;                      // ... with vf_psnr / vf_ssim fused into it (Unit7::qual)
     Plan7 p7;
     dts_graph_info info{};
 };
@@ -521,92 +504,45 @@ bool v7_enabled()
     return !(f && (f[0] == '3' || f[0] == '4' || f[0] == '5' || f[0] == '6'));
 }
 
-// waves per k_ladder7 group (DTS_L7_W, 1..16; default 8: two groups of 8 waves per CU)
+// waves per k_ladder7 group (diagnostic DTS_L7_W, 1..16; default 8: two groups of 8 waves per CU)
 int l7_waves()
 {
-    const char *f = std::getenv("DTS_L7_W");
+    const char *f = diag_env("DTS_L7_W");
     const int w = f ? std::atoi(f) : 8;
     return std::min(std::max(w, 1), kL7MaxWaves);
 }
 
 // Staging batches per k_ladder7 group and granules per batch: what the linked kernel was
 // compiled with (ladder7.hip NS7 / PB7; diagnostic builds change them with -DDTS_L7_NS /
-// -DDTS_L7_PAIR).  The planner sizes the stage buffers and the V fragment slots from these,
-// so DTS_L7_NS / DTS_L7_PB may only restate them: a graph asked for any other value is
-// refused (l7_knobs_ok), never planned for a kernel that would overrun its slots.
+// -DDTS_L7_PAIR).  The planner sizes the stage buffers and the V fragment slots from these.
 int l7_stages()
 {
-    int ns, pb, dc;
-    ladder7_compiled(&ns, &pb, &dc);
+    int ns, pb;
+    ladder7_compiled(&ns, &pb);
     return ns;
 }
 
 // granules per k_ladder7 staging batch (see l7_stages)
 int l7_pb()
 {
-    int ns, pb, dc;
-    ladder7_compiled(&ns, &pb, &dc);
+    int ns, pb;
+    ladder7_compiled(&ns, &pb);
     return pb;
 }
 
-bool l7_knobs_ok()
-{
-    const char *ns = std::getenv("DTS_L7_NS"), *pb = std::getenv("DTS_L7_PB");
-    return (!ns || std::atoi(ns) == l7_stages()) && (!pb || std::atoi(pb) == l7_pb());
-}
-
-// k_ladder7 groups: one rendition per group (DTS_L7_GROUP=r) or every rendition of a
-// source strip (m)
+// k_ladder7 groups: one rendition per group (diagnostic DTS_L7_GROUP=r) or every rendition of a
+// source strip (the default)
 bool l7_by_rung()
 {
-    const char *f = std::getenv("DTS_L7_GROUP");
+    const char *f = diag_env("DTS_L7_GROUP");
     return f ? f[0] == 'r' : false;
 }
 
-// decoupled staging (what the linked kernel was compiled with, ladder7.hip DTS_L7_DECOUPLE): one wave
-// of every group stages every source piece and V fragment, the others never wait on vmcnt
-int l7_decouple()
-{
-    int ns, pb, dc;
-    ladder7_compiled(&ns, &pb, &dc);
-    return dc;
-}
-
-// k_ladder7 one-K-block walks with half the tiles (DTS_L7_NARROW=1)
+// k_ladder7 one-K-block walks with half the tiles (diagnostic DTS_L7_NARROW=1)
 bool l7_narrow()
 {
-    const char *f = std::getenv("DTS_L7_NARROW");
+    const char *f = diag_env("DTS_L7_NARROW");
     return f ? f[0] == '1' : false;
-}
-
-// vf_psnr / vf_ssim of output k: the graph's quality output or a rendition with quality
-bool wants_quality(const dts_graph_spec &s, int k)
-{
-    return (s.quality && k == s.quality_out) || s.out[k].quality;
-}
-
-// the separate quality pass on a stream of its own beside the next chunk's ladder (DTS_QSTREAM=1;
-// measured slower than one stream: cfg4 41.5k vs 45.5k, cfg5 111.3k vs 116.2k fps -- DESIGN.md §4)
-bool qstream_enabled()
-{
-    const char *f = std::getenv("DTS_QSTREAM");
-    return f && f[0] == '1';
-}
-
-// frames per ladder -> quality chunk on two streams (DTS_QCHUNK; default a quarter of the call, >= 16)
-int qchunk_frames(int n)
-{
-    const char *f = std::getenv("DTS_QCHUNK");
-    const int c = f ? std::atoi(f) : std::max(16, (n + 3) / 4);
-    return std::max(1, c);
-}
-
-// quality fused into k_ladder7's V epilogue (DTS_QFUSE=1; else the separate k_quality pass).  Bit-exact
-// records, measured slower (cfg4 20.8k vs 45.5k, cfg5 51.8k vs 116.2k fps -- DESIGN.md §4)
-bool qfuse_enabled()
-{
-    const char *f = std::getenv("DTS_QFUSE");
-    return f && f[0] == '1';
 }
 
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
@@ -625,7 +561,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
         if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         for (int k = 0; k < s.nout; ++k) {
             const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
-            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt, false});
+            in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
         }
         if (!plan5_kind(in, gp.p5[kind])) return false;
     }
@@ -639,21 +575,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.v5 = true;
     // k_ladder7 takes planar and nv12 sources (k_ladder5: the fallback for frames that are
     // not 16-byte aligned)
-    gp.v7 = false;
-    if (v7_enabled() && qfuse_enabled()) {        // quality fused into the V epilogue where asked for
-        Plan5In iq[2] = {ins[0], ins[1]};
-        bool any = false;
-        for (int kind = 0; kind < 2; ++kind)
-            for (int k = 0; k < s.nout; ++k) {
-                iq[kind].rungs[(size_t)k].qual = wants_quality(s, k);
-                any = any || iq[kind].rungs[(size_t)k].qual;
-            }
-        gp.qf = gp.v7 = any && plan7_graph(iq, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
-                                           l7_decouple(), gp.p7);
-    }
-    if (!gp.v7)
-        gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(),
-                                            l7_decouple(), gp.p7);
+    gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), gp.p7);
     return true;
 }
 
@@ -679,7 +601,7 @@ bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
                                          s.hdr_to_sdr ? (int)DTS_FMT_P010LE : s.out[k].fmt});
         }
     }
-    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, l7_decouple(), gp.p7);
+    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, gp.p7);
 }
 
 bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
@@ -699,7 +621,6 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 {
     int e = validate_spec(s);
     if (e) return e;
-    if (!l7_knobs_ok()) return DTS_E_INVAL;      // DTS_L7_NS / DTS_L7_PB differ from the linked kernel
     gp.src_kind = s.src_fmt == DTS_FMT_P010LE ? kSrcP010 : (s.src_fmt == DTS_FMT_NV12 ? kSrcNV12 : kSrcPlanar8);
     const bool p010 = s.src_fmt == DTS_FMT_P010LE;
     const bool use4 = v4_enabled();
@@ -784,12 +705,12 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     // together, so the items a queue hands out back to back walk the same source rows
     // and re-read them from L2 (r01: +3 % over heaviest-first at 256 frames per launch).
     // A single rendition keeps heaviest-first (H tap pairs x columns x source rows),
-    // which shortens the launch tail (cfg4: 26.1k vs 25.0k fps); DTS_ORDER=h / c force one.
+    // which shortens the launch tail (cfg4: 26.1k vs 25.0k fps); diagnostic DTS_ORDER=h / c force one.
     auto cost4 = [&](const Job4 &j) {
         return (int64_t)(2 * gp.p4[j.rk].N + 8) * j.ncols * gp.kts[j.rk].srcH;
     };
     std::stable_sort(gp.jobs4.begin(), gp.jobs4.end(), [&](const Job4 &a, const Job4 &b) { return cost4(a) > cost4(b); });
-    const char *order = std::getenv("DTS_ORDER");
+    const char *order = diag_env("DTS_ORDER");
     const bool by_column = order ? order[0] == 'c' : s.nout > 1;   // one rendition: no source re-reads to share
     if (by_column) {
         auto srcx = [&](const Job4 &j) { return (double)(j.x0 + 0.5 * j.ncols) / gp.kts[j.rk].dstW; };
@@ -823,7 +744,26 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
 
 extern "C" {
 
-const char *dts_version(void) { return "dts-mi355x 0.6 (gfx950; abi 6)"; }
+#define DTS_STR2(x) #x
+#define DTS_STR(x) DTS_STR2(x)
+const char *dts_version(void) { return "dts-mi355x 0.7 (gfx950; abi " DTS_STR(DTS_ABI_VERSION) ")"; }
+
+int dts_abi_version(void) { return DTS_ABI_VERSION; }
+
+int64_t dts_abi_struct_size(int which)
+{
+    switch (which) {
+    case DTS_STRUCT_TONEMAP_SPEC: return (int64_t)sizeof(dts_tonemap_spec);
+    case DTS_STRUCT_OUTPUT_SPEC: return (int64_t)sizeof(dts_output_spec);
+    case DTS_STRUCT_GRAPH_SPEC: return (int64_t)sizeof(dts_graph_spec);
+    case DTS_STRUCT_FRAME: return (int64_t)sizeof(dts_frame);
+    case DTS_STRUCT_DEV_FRAMES: return (int64_t)sizeof(dts_dev_frames);
+    case DTS_STRUCT_QRAW: return (int64_t)sizeof(dts_qraw);
+    case DTS_STRUCT_QSTAT: return (int64_t)sizeof(dts_qstat);
+    case DTS_STRUCT_GRAPH_INFO: return (int64_t)sizeof(dts_graph_info);
+    default: return DTS_E_INVAL;
+    }
+}
 
 const char *dts_strerror(int err)
 {
@@ -1093,10 +1033,6 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     const size_t u_off = push_blob(blob, gp.p7.units);
     const size_t f_off = push_blob(blob, gp.p7.frag);
     const size_t r_off = push_blob(blob, gp.p7.fire);
-    const size_t s_off = push_blob(blob, gp.p7.fsched);
-    const size_t qr_off = push_blob(blob, gp.p7.qrend);
-    const size_t qu_off = push_blob(blob, gp.p7.qunit);
-    const size_t qb_off = push_blob(blob, gp.p7.qbound);
     HIPCHK(ctx, hipMalloc(&g->dev_tables7, blob.size()));
     HIPCHK(ctx, hipMemcpy(g->dev_tables7, blob.data(), blob.size(), hipMemcpyHostToDevice));
     const uint8_t *base = static_cast<const uint8_t *>(g->dev_tables7);
@@ -1104,15 +1040,6 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_units7 = reinterpret_cast<const Unit7 *>(base + u_off);
     g->dev_frag7 = reinterpret_cast<const uint32_t *>(base + f_off);
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
-    g->dev_fsched7 = gp.p7.fsched.empty() ? nullptr : reinterpret_cast<const FragOp7 *>(base + s_off);
-    g->qf7 = gp.qf;
-    g->dev_qrend7 = reinterpret_cast<const QRend7 *>(base + qr_off);
-    g->dev_qunit7 = reinterpret_cast<const int32_t *>(base + qu_off);
-    g->dev_qbound7 = reinterpret_cast<const int32_t *>(base + qb_off);
-    g->nqrend7 = (int)gp.p7.qrend.size();
-    g->nunits7 = (int)gp.p7.units.size();
-    g->nqbound7 = (int)gp.p7.qbound.size() / 2;
-    for (const QRend7 &q : gp.p7.qrend) g->qmax_h4 = std::max(g->qmax_h4, q.h >> 2);
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
     g->waves7 = gp.p7.waves;
@@ -1162,35 +1089,19 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         if (s.hdr_to_sdr) {
             g->hdr = true;
             g->tm = tonemap_params(s.tonemap);
-            // Chunks of `batch` frames on one stream.  Diagnostic A/B knobs (r03, cfg3: no
-            // gain): DTS_HDR_CHUNK = frames per chunk (7 frames keep both intermediates in the
-            // Infinity Cache: 25.2k fps, 16: 32.5k, 256: 44.8k -- k_ladder4's persistent grid
-            // pays a tail per launch), DTS_HDR_STREAMS=2 tonemaps on a second stream beside
-            // the next chunk's ladder (44.4k vs 44.8k)
-            int64_t mid_bytes = 0;
-            for (int k = 0; k < s.nout; ++k) {
-                g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
-                mid_bytes += g->lay_mid[k].fstride;
-            }
-            const char *hc = std::getenv("DTS_HDR_CHUNK");
-            g->hdr_chunk = hc ? std::atoi(hc) : g->batch;
-            g->hdr_chunk = std::min(std::max(g->hdr_chunk, 1), g->batch);
-            (void)mid_bytes;
-            const char *hs = std::getenv("DTS_HDR_STREAMS");
-            const bool two = hs && hs[0] == '2';
+            // chunks of `batch` frames: the ladder writes a chunk's p010 intermediates, k_tonemap
+            // converts them on the same stream (measured in round 3: smaller chunks, which keep the
+            // intermediates in the Infinity Cache, or the tonemap on a second stream beside the next
+            // chunk's ladder are no faster -- DESIGN.md §4 k_tonemap)
+            e = DTS_OK;
+            for (int k = 0; k < s.nout; ++k) g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
+            g->hdr_chunk = g->batch;
             for (int sl = 0; sl < 2 && !e; ++sl) {
                 for (int k = 0; k < s.nout && !e; ++k)
                     if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->hdr_chunk * g->lay_mid[k].fstride) != hipSuccess)
                         e = DTS_E_NOMEM;
-                if (!e && (hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess ||
-                           hipEventCreateWithFlags(&g->hdr_mid_ev[sl], hipEventDisableTiming) != hipSuccess))
-                    e = DTS_E_HIP;
+                if (!e && hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
             }
-            if (!e && two &&
-                (hipStreamCreateWithFlags(&g->hdr_tm, hipStreamNonBlocking) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->hdr_go, hipEventDisableTiming) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->hdr_end, hipEventDisableTiming) != hipSuccess))
-                e = DTS_E_HIP;
             if (!e) {
                 const std::vector<float> luts = tonemap_luts(s.tonemap);
                 const size_t nb = luts.size() * sizeof(float);
@@ -1222,21 +1133,6 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
                 o.quality = 0;
                 g->rq_out[rs.nout++] = k;
             }
-        bool anyq = s.quality != 0;
-        for (int k = 0; k < s.nout; ++k) anyq = anyq || s.out[k].quality;
-        if (anyq && !s.hdr_to_sdr && qstream_enabled()) {
-            e = DTS_OK;
-            if (hipStreamCreateWithFlags(&g->q_st, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&g->q_go, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&g->q_end, hipEventDisableTiming) != hipSuccess)
-                e = DTS_E_HIP;
-            for (int i = 0; i < dts_graph::kQEv && !e; ++i)
-                if (hipEventCreateWithFlags(&g->q_ev[i], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
-            if (e) {
-                dts_graph_destroy(g);
-                return e;
-            }
-        }
         if (rs.nout) {
             for (int k = rs.nout; k < DTS_MAX_OUTPUTS; ++k) rs.out[k] = dts_output_spec{};
             e = dts_graph_create(ctx, &rs, &g->ref);
@@ -1280,22 +1176,7 @@ void dts_graph_destroy(dts_graph *g)
     if (!g) return;
     hipSetDevice(g->ctx->device);
     free_host_path(g);
-    if (g->hdr_tm) {
-        hipStreamSynchronize(g->hdr_tm);
-        hipStreamDestroy(g->hdr_tm);
-    }
-    if (g->q_st) {
-        hipStreamSynchronize(g->q_st);
-        hipStreamDestroy(g->q_st);
-    }
-    for (int i = 0; i < dts_graph::kQEv; ++i)
-        if (g->q_ev[i]) hipEventDestroy(g->q_ev[i]);
-    if (g->q_go) hipEventDestroy(g->q_go);
-    if (g->q_end) hipEventDestroy(g->q_end);
-    if (g->hdr_go) hipEventDestroy(g->hdr_go);
-    if (g->hdr_end) hipEventDestroy(g->hdr_end);
     for (int sl = 0; sl < 2; ++sl) {
-        if (g->hdr_mid_ev[sl]) hipEventDestroy(g->hdr_mid_ev[sl]);
         if (g->hdr_ev[sl]) {
             hipEventSynchronize(g->hdr_ev[sl]);
             hipEventDestroy(g->hdr_ev[sl]);
@@ -1522,7 +1403,6 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.units = g->dev_units7;
             q.frag = g->dev_frag7;
             q.fire = g->dev_fire7;
-            q.fsched = g->dev_fsched7;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
             HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
@@ -1578,87 +1458,14 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
     return DTS_OK;
 }
 
-// The ladder with vf_psnr / vf_ssim fused into k_ladder7 (GraphPlan::qf): per chunk of at most
-// g->batch frames one k_ladder7<QF> launch (each quality unit scores its row blocks against
-// qref[k] in its V epilogue), k_qfix7 (the windows straddling two units) and k_qfin7 (per
-// frame and rendition, out_q[k * qstride + f]).  DTS_E_UNSUPPORTED when a batch cannot run on
-// k_ladder7 (planes not 16 / 4-byte aligned): the caller then takes the separate pass.
-static int enqueue_ladder_q(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, int nframes,
-                            const DevPlanes *qref, dts_qraw *out_q, int64_t qstride, hipStream_t st)
-{
-    const dts_graph_spec &s = g->spec;
-    dts_ctx *ctx = g->ctx;
-    if (!g->qf7 || !planes_aligned7(src)) return DTS_E_UNSUPPORTED;
-    for (int k = 0; k < s.nout; ++k)
-        if (!planes_aligned4(dst[k]) || (qref[k].data[0] && !planes_aligned4(qref[k]))) return DTS_E_UNSUPPORTED;
-    const int B = g->batch, nsp = qfuse7_spans(g->qmax_h4);
-    const size_t part = (size_t)B * g->nunits7 * sizeof(QPart7);
-    const size_t need = part + (size_t)B * std::max(g->nqbound7, 1) * nsp * sizeof(double);
-    int e = ensure_qscratch(ctx, qs, need);
-    if (e) return e;
-    for (int f0 = 0; f0 < nframes; f0 += B) {
-        const int n = std::min(B, nframes - f0);
-        HIPCHK(ctx, hipStreamWaitEvent(st, qs.ev, 0));         // the previous user of the partials
-        Ladder7Params q{};
-        q.src = src;
-        for (int pl = 0; pl < 3; ++pl) q.src.data[pl] += (uint64_t)((int64_t)f0 * src.fstride);
-        QFinParams fp{};
-        for (int k = 0; k < kMaxRungs; ++k) {
-            const int kk = k < s.nout ? k : 0;
-            q.dst[k] = dst[kk];
-            for (int pl = 0; pl < 3; ++pl) q.dst[k].data[pl] += (uint64_t)((int64_t)f0 * dst[kk].fstride);
-            if (k < s.nout && qref[k].data[0]) {
-                q.qref[k] = qref[k];
-                for (int pl = 0; pl < 3; ++pl)
-                    if (q.qref[k].data[pl]) q.qref[k].data[pl] += (uint64_t)((int64_t)f0 * qref[k].fstride);
-            }
-            fp.out[k] = q.dst[k];
-            fp.ref[k] = q.qref[k];
-            fp.fmt[k] = k < s.nout ? s.out[k].fmt : 0;
-        }
-        q.ngroups = g->ngroups7;
-        q.nframes = n;
-        q.groups = g->dev_groups7;
-        q.units = g->dev_units7;
-        q.frag = g->dev_frag7;
-        q.fire = g->dev_fire7;
-        q.fsched = g->dev_fsched7;
-        q.qpart = static_cast<QPart7 *>(qs.p);
-        q.nunits = g->nunits7;
-        const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
-        if (grid > INT32_MAX) return DTS_E_RANGE;
-        HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, false, g->hsplit7, g->src_kind, st, true));
-        fp.rend = g->dev_qrend7;
-        fp.qunit = g->dev_qunit7;
-        fp.qbound = g->dev_qbound7;
-        fp.qpart = q.qpart;
-        fp.fixp = reinterpret_cast<double *>(static_cast<uint8_t *>(qs.p) + part);
-        fp.out_q = out_q + f0;
-        fp.nrend = g->nqrend7;
-        fp.nunits = g->nunits7;
-        fp.nbound = g->nqbound7;
-        fp.nframes = n;
-        fp.qstride = qstride;
-        HIPCHK(ctx, launch_qfuse7(fp, s.nout, g->qmax_h4, st));
-        HIPCHK(ctx, hipEventRecord(qs.ev, st));
-    }
-    return DTS_OK;
-}
-
 // HDR10 -> SDR: per chunk of hdr_chunk frames, the bit-exact ladder into a p010
-// intermediate (two, alternating), then k_tonemap from it into the caller's output.  The
-// tonemaps run on the graph's second stream: the ladder of chunk i + 1 overlaps the
-// tonemap of chunk i, and a chunk's intermediate is still in the Infinity Cache when the
-// tonemap reads it.  The caller's stream waits for the last tonemap before returning.
+// intermediate (two, alternating: a chunk's ladder may run while the other buffer's tonemap
+// of the host path's other stream still reads), then k_tonemap from it into the caller's
+// output, both on the caller's stream.
 static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, int nframes, hipStream_t st)
 {
     const dts_graph_spec &s = g->spec;
     dts_ctx *ctx = g->ctx;
-    hipStream_t tm = g->hdr_tm ? g->hdr_tm : st;
-    if (g->hdr_tm) {                                  // the outputs' earlier users on st come first
-        HIPCHK(ctx, hipEventRecord(g->hdr_go, st));
-        HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_go, 0));
-    }
     for (int f0 = 0; f0 < nframes; f0 += g->hdr_chunk) {
         const int n = std::min(g->hdr_chunk, nframes - f0);
         const int sl = (int)(g->hdr_next++ & 1u);
@@ -1672,10 +1479,6 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
         }
         int e = enqueue_ladder(g, sc, mid, mid_fmt, n, st);
         if (e) return e;
-        if (g->hdr_tm) {
-            HIPCHK(ctx, hipEventRecord(g->hdr_mid_ev[sl], st));
-            HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_mid_ev[sl], 0));
-        }
         for (int k = 0; k < s.nout; ++k) {
             TonemapParams tp = g->tm;
             tp.src = mid[k];
@@ -1685,13 +1488,9 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
             tp.w = s.out[k].w;
             tp.h = s.out[k].h;
             tp.nframes = n;
-            HIPCHK(ctx, launch_tonemap(tp, tm));
+            HIPCHK(ctx, launch_tonemap(tp, st));
         }
-        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], tm));
-    }
-    if (g->hdr_tm) {
-        HIPCHK(ctx, hipEventRecord(g->hdr_end, tm));
-        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_end, 0));
+        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], st));
     }
     return DTS_OK;
 }
@@ -1716,8 +1515,7 @@ static int ensure_rscratch(dts_ctx *ctx, QScratch &q, size_t bytes)
 // frame c0) and its quality: graph quality (qref = the quality_out reference batch, records
 // qraw[c0 + f]), rendition quality against references the graph makes (g->ref, into scratch)
 // or that come with the call (DTS_QREF_EXTERNAL: qref = nout batches), records
-// qraw[k * ntot + c0 + f].  Fused into k_ladder7 where the graph planned it, else the separate
-// k_quality pass.  m <= g->batch when the graph makes references.
+// qraw[k * ntot + c0 + f].  m <= g->batch when the graph makes references.
 static int ladder_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, const DevPlanes *dst, const int *dfmt,
                           int c0, int m, int ntot, const dts_dev_frames *qref, dts_qraw *qraw, hipStream_t st)
 {
@@ -1764,54 +1562,22 @@ static int ladder_quality(dts_graph *g, QScratch &qs, const DevPlanes &src, cons
         e = enqueue_ladder(r, src, rd, rf, m, st);
         if (e) return e;
     }
-    int e = g->hdr ? DTS_E_UNSUPPORTED : enqueue_ladder_q(g, qs, src, dst, m, qr, out_q, qstride, st);
-    if (e == DTS_E_UNSUPPORTED) {                // the separate pass: the ladder, then k_quality per output
-        // in chunks, the quality of chunk i on the graph's quality stream beside the ladder of chunk
-        // i + 1 (both in the CUs at once where the ladder leaves room: cfg4's one group per CU)
-        e = DTS_OK;
-        const bool two = g->q_st && !g->hdr;
-        const int C = two ? qchunk_frames(m) : m;
-        hipStream_t qst = two ? g->q_st : st;
-        if (two) {                               // the outputs' / references' earlier users on st first
-            HIPCHK(ctx, hipEventRecord(g->q_go, st));
-            HIPCHK(ctx, hipStreamWaitEvent(qst, g->q_go, 0));
+    // the ladder, then k_quality per output with a reference (a separate pass: fused into
+    // k_ladder7's V epilogue it measured 2.3x slower, DESIGN.md §4 k_quality)
+    int e = g->hdr ? enqueue_hdr(g, src, dst, m, st) : enqueue_ladder(g, src, dst, dfmt, m, st);
+    for (int k = 0; k < s.nout && !e; ++k) {
+        if (!qr[k].data[0]) continue;
+        const dts_output_spec &o = s.out[k];
+        dts_dev_frames a{}, b{};
+        for (int pl = 0; pl < 3; ++pl) {
+            a.data[pl] = dst[k].data[pl] ? reinterpret_cast<void *>(dst[k].data[pl]) : nullptr;
+            a.pitch[pl] = dst[k].pitch[pl];
+            b.data[pl] = qr[k].data[pl] ? reinterpret_cast<void *>(qr[k].data[pl]) : nullptr;
+            b.pitch[pl] = qr[k].pitch[pl];
         }
-        for (int c0 = 0; c0 < m && !e; c0 += C) {
-            const int mc = std::min(C, m - c0);
-            DevPlanes sc = src, dc[DTS_MAX_OUTPUTS];
-            for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src.fstride);
-            for (int k = 0; k < s.nout; ++k) {
-                dc[k] = dst[k];
-                for (int pl = 0; pl < 3; ++pl) dc[k].data[pl] += (uint64_t)((int64_t)c0 * dst[k].fstride);
-            }
-            e = g->hdr ? enqueue_hdr(g, sc, dc, mc, st) : enqueue_ladder(g, sc, dc, dfmt, mc, st);
-            if (e) break;
-            if (two) {
-                hipEvent_t ev = g->q_ev[g->q_next++ % dts_graph::kQEv];
-                HIPCHK(ctx, hipEventRecord(ev, st));
-                HIPCHK(ctx, hipStreamWaitEvent(qst, ev, 0));
-            }
-            for (int k = 0; k < s.nout && !e; ++k) {
-                if (!qr[k].data[0]) continue;
-                const dts_output_spec &o = s.out[k];
-                dts_dev_frames a{}, b{};
-                for (int pl = 0; pl < 3; ++pl) {
-                    a.data[pl] = dc[k].data[pl] ? reinterpret_cast<void *>(dc[k].data[pl]) : nullptr;
-                    a.pitch[pl] = dst[k].pitch[pl];
-                    b.data[pl] = qr[k].data[pl] ? reinterpret_cast<void *>(qr[k].data[pl] +
-                                                                           (uint64_t)((int64_t)c0 * qr[k].fstride))
-                                                : nullptr;
-                    b.pitch[pl] = qr[k].pitch[pl];
-                }
-                a.frame_stride = dst[k].fstride;
-                b.frame_stride = qr[k].fstride;
-                e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, mc, out_q + (int64_t)k * qstride + c0, qst);
-            }
-        }
-        if (two && !e) {                         // the caller's stream sees the records
-            HIPCHK(ctx, hipEventRecord(g->q_end, qst));
-            HIPCHK(ctx, hipStreamWaitEvent(st, g->q_end, 0));
-        }
+        a.frame_stride = dst[k].fstride;
+        b.frame_stride = qr[k].fstride;
+        e = quality_enqueue(ctx, qs, o.w, o.h, o.fmt, a, b, m, out_q + (int64_t)k * qstride, st);
     }
     if (!e && rq) HIPCHK(ctx, hipEventRecord(qs.rev, st));
     return e;
@@ -2216,6 +1982,11 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
     if (g->pending) return DTS_E_BUSY;
     const dts_graph_spec &s = g->spec;
     if (s.quality && !qref) return DTS_E_INVAL;
+    // external reference renditions (DTS_QREF_EXTERNAL) come with dts_graph_run_device only:
+    // the host path has no way to take nout reference batches, so it refuses the graph rather
+    // than return records it never computed
+    for (int k = 0; k < s.nout; ++k)
+        if (s.out[k].quality && s.out[k].qref_method == DTS_QREF_EXTERNAL) return DTS_E_UNSUPPORTED;
     dts_ctx *ctx = g->ctx;
     hipSetDevice(ctx->device);
     try {

@@ -5,10 +5,26 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dts.h"
 
 namespace dts {
+
+// Diagnostic A/B knobs (DTS_L7_W, DTS_L7_SORT, DTS_ORDER ...): read from the environment only
+// in the diagnostic builds of tools/ (-DDTS_DIAG_KNOBS).  The default libdts.so reads two
+// documented settings and nothing else: DTS_HOST_THREADS (host-path packing threads) and
+// DTS_LADDER (kernel selection for the fallback parity tests; include/dts.h).
+inline const char *diag_env(const char *name)
+{
+#ifdef DTS_DIAG_KNOBS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 
 // ---------------------------------------------------------------------------
 // Ladder (scale + format convert) launch geometry
@@ -315,8 +331,6 @@ struct Unit7 {                      // one wave of a group
     int32_t rc_sh;                  // range conversion of the 15-bit H output (0: none):
     int32_t rc_cap, rc_mul, rc_add; //   y = (min(y, cap) * mul + add) >> sh, as swscale.c's lum/chr
                                     //   RangeToJpeg_c / RangeFromJpeg_c (int16 store)
-    int32_t qual;                   // 1: vf_psnr / vf_ssim of this rendition fused into the V epilogue
-                                    //   (k_ladder7 QF: reference Ladder7Params::qref[rung])
     int32_t pad_;
 };
 
@@ -332,38 +346,8 @@ struct Group7 {                     // one workgroup's strip of one frame
     int32_t bpc;                    // staged bytes per source column: 1 (8-bit planes; chroma: U and V
                                     // planes), 2 (nv12 chroma: U V byte pairs; p010 luma), 4 (p010
                                     // chroma: U V 16-bit pairs); bpc npc pieces per plane and granule
-    int32_t fs0, nfs;               // decoupled groups: the staging wave's V fragment DMAs (FragOp7)
-    int32_t st0;                    // first staging wave: waves st0.. deal the source pieces (and, decoupled,
-                                    // wave st0 issues the FragOp7 schedule); the waves before issue no loads
-    int32_t qscr;                   // LDS offset of the per-wave 4x4-block sums of fused quality (kQ7Wave each)
-};
-
-// Fused quality (k_ladder7 QF, ladder7.hip qrb7): per wave the previous row block's last row of
-// 4x4-block sums (s1 | s2 << 16, ss, s12; 16 B per block, 16 block columns: one plane, or 8 of
-// each chroma plane) and the running sums; the row block's own 4 rows use the wave's store
-// exchange scratch; per unit and frame one QPart7
-constexpr int kQ7Acc = 256;         // row 0 of the block table ([plane][16 block columns] x 16 B), then the
-constexpr int kQ7Wave = kQ7Acc + 32; // running sums: u64 sse[2], ssim[2] (2^-24 fixed point)
-struct QPart7 {
-    uint64_t sse[2];                // the unit's planes (luma: [0]; chroma: U, V)
-    double ssim[2];                 // ssim_end1 sums of the windows inside the unit
-};
-// one plane of one rendition of a fused-quality graph: its units, and the unit boundaries whose
-// straddling 8x8 windows k_qfix7 scores
-struct QRend7 {
-    int32_t rung, plane;            // plane 0 Y, 1 U, 2 V
-    int32_t w, h;                   // plane size
-    int32_t u0, nu;                 // the plane kind's units of this rendition: qunit[u0 .. u0 + nu)
-    int32_t b0, nb;                 // boundaries b0 .. b0 + nb - 1 (qbound pairs: block column left of it, entry)
-};
-
-// Decoupled staging (ladder7.hip DTS_L7_DECOUPLE): one V fragment DMA of a group, issued by
-// its staging wave with the source pieces of staging batch `batch`, in batch order
-struct FragOp7 {
-    int32_t batch;
-    uint32_t pair;                  // fragment pair (2 KB: hi 1 KB, lo 1 KB; VKB pairs per row block)
-    int32_t lds;                    // LDS destination (the rendition's slot of this row block)
-    int32_t n1k;                    // 1-KB DMAs (2 VKB)
+    int32_t st0;                    // first staging wave: waves st0.. deal the source pieces (a group's spare
+                                    // waves when it has fewer units than the workgroup has waves, else all)
 };
 
 struct Ladder7Params {
@@ -374,35 +358,11 @@ struct Ladder7Params {
     const Unit7 *units;
     const uint32_t *frag;           // as Ladder6Params
     const int32_t *fire;
-    const FragOp7 *fsched;          // decoupled groups' fragment DMA schedules (Group7::fs0 / nfs)
-    DevPlanes qref[kMaxRungs];      // QF: each rendition's reference batch (Unit7::qual renditions)
-    QPart7 *qpart;                  // QF: [frame][unit] partial records
-    int32_t nunits, pad2_[3];
 };
-
-// Fused-quality epilogue launches (ladder7.hip): k_qfix7 scores the 8x8 windows straddling unit
-// boundaries from the outputs and references, k_qfin7 sums the units' and boundaries' partials
-// into one dts_qraw per (frame, rendition)
-struct QFinParams {
-    DevPlanes out[kMaxRungs], ref[kMaxRungs];
-    int32_t fmt[kMaxRungs];
-    const QRend7 *rend;             // nrend entries, rendition-major, planes 0..2
-    const int32_t *qunit;           // unit indices of each QRend7
-    const int32_t *qbound;          // per boundary: (block column left of it, QRend7 index)
-    const QPart7 *qpart;            // [frame][nunits]
-    double *fixp;                   // [frame][nbound_total] k_qfix7 window sums
-    dts_qraw *out_q;                // record (rung, frame) at out_q[rung * qstride + frame]
-    int32_t nrend, nunits, nbound, nframes;
-    int64_t qstride;
-};
-// k_qfix7 (spans of 63 window rows per boundary, the tallest plane's max_h4 block rows) then k_qfin7;
-// fixp holds nframes x nbound x qfuse7_spans(max_h4) doubles
-hipError_t launch_qfuse7(const QFinParams &p, int nrungs, int max_h4, hipStream_t s);
-int qfuse7_spans(int max_h4);
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          int src_kind, hipStream_t s, bool quality = false);   // src_kind: SrcKind
-void ladder7_compiled(int *stages, int *batch, int *decouple);   // NS7 / PB7 / DTS_L7_DECOUPLE of the linked k_ladder7
+                          int src_kind, hipStream_t s);   // src_kind: SrcKind
+void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

@@ -81,7 +81,6 @@ struct Plan5Rung {
     const SwsFilter *fh;             // the libswscale H filter
     const VTable *v;                 // the packed V table
     int dstW, dstH, fmt;             // plane size and the rendition's output format
-    bool qual = false;               // vf_psnr / vf_ssim fused into k_ladder7's V epilogue
 };
 
 struct Plan5In {
@@ -136,17 +135,11 @@ struct Plan7 {
     std::vector<Unit7> units;
     std::vector<uint32_t> frag;
     std::vector<int32_t> fire;
-    std::vector<FragOp7> fsched;     // decoupled groups: each staging wave's V fragment DMAs
-    std::vector<QRend7> qrend;       // fused quality: per (rendition, plane) unit lists and boundaries
-    std::vector<int32_t> qunit, qbound;
     int lds_bytes = 0, waves = 0;    // per workgroup: LDS, waves (max over groups)
     int hsplit = 256;                // H tap split of the fragments (ladder7.hip walk7 HS)
 };
-// decouple (ladder7.hip DTS_L7_DECOUPLE): 0 groups of wmax units whose waves deal the pieces (a
-// group's spare waves, if any, stage them all) and whose rendition leads DMA the fragments; 1 at
-// most wmax - 1 units and a staging wave that issues every piece and fragment; 2 groups of wmax
-// units whose lighter half (or spare waves) issue every piece and fragment
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, int decouple,
-                 Plan7 &out);
+// Groups of at most wmax units; a group's spare waves (if any) stage its pieces, else all its
+// waves deal them, and each rendition's lead wave DMAs its V fragments.
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out);
 
 } // namespace dts

@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
                 bs[RB][i] = block(bx0 + x, by0, c + (plane == 2));
             }
             __syncthreads();
-            windows(by0 + 1, b, 0, 1, true);
+            windows(by0, b, 0, 1, true);    // top block row by0 - 1 (held at b), bottom by0 (row RB)
         }
     }
 #pragma unroll

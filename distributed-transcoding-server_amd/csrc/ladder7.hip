@@ -64,9 +64,6 @@
 #ifndef DTS_L7_DEFER
 #define DTS_L7_DEFER 1      // row blocks run one granule after the one completing their window
 #endif
-#ifndef DTS_L7_DEFER_ST
-#define DTS_L7_DEFER_ST 0   // diagnostic: hold a row block's exchanged bytes and store them after the next H
-#endif
 #ifndef DTS_L7_SRC_AUX
 #define DTS_L7_SRC_AUX 0    // cache-policy bits of the source staging loads (diagnostic A/B)
 #endif
@@ -76,23 +73,8 @@
 #ifndef DTS_L7_PAIR
 #define DTS_L7_PAIR (kL7Batch == 2)  // 1: stage 2 granules per batch (one barrier per 2 granules); plan with DTS_L7_PB=2
 #endif
-#ifndef DTS_L7_DMAPOS
-#define DTS_L7_DMAPOS 0     // where a wave issues the next batch's pieces (walk7 issue())
-#endif
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
-#endif
-#ifndef DTS_L7_QEARLY
-#define DTS_L7_QEARLY 0     // fused quality: where the reference rows are loaded -- 2 before the V MFMAs, 1
-                            // before the store exchange (latency hidden, 4 more VGPRs live: spills), 0 after
-#endif
-#ifndef DTS_L7_DECOUPLE
-#define DTS_L7_DECOUPLE 0   // who issues the group's loads (Group7::st0; plan7_graph): 0 every wave deals the
-                            // source pieces (a group's spare waves, if any, stage them all) and the first
-                            // wave of each rendition DMAs its V fragments; 1 a staging-only wave per group
-                            // issues every piece and fragment (FragOp7 schedule); 2 the lighter half of the
-                            // unit waves (or the spare waves) issue them, so the heavy waves, which set the
-                            // group's pace at every barrier, issue no loads and never wait on vmcnt
 #endif
 
 namespace dts {
@@ -132,24 +114,9 @@ static_assert(NS7 >= 2 && NS7 <= 4, "stages (plan7_graph: V fragment slots for P
 
 // s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0: waiting for fewer outstanding
 // operations than were issued after the batch is never too short
-#ifndef DTS_L7_WAITTREE
-#define DTS_L7_WAITTREE 0   // 1: the run-time vmcnt wait as a 4-level binary tree of branches
-#endif
 __device__ __forceinline__ void vm_wait_rt7(int n)
 {
 #define DTS_W7I(k) __builtin_amdgcn_s_waitcnt((k) | (7 << 4) | (15 << 8))
-#if DTS_L7_WAITTREE
-    const int v = min(max(n, 0), 15);
-#define DTS_W7P(k) if (v == (k)) DTS_W7I(k); else DTS_W7I((k) + 1)
-    if (v < 8) {
-        if (v < 4) { if (v < 2) { DTS_W7P(0); } else { DTS_W7P(2); } }
-        else { if (v < 6) { DTS_W7P(4); } else { DTS_W7P(6); } }
-    } else {
-        if (v < 12) { if (v < 10) { DTS_W7P(8); } else { DTS_W7P(10); } }
-        else { if (v < 14) { DTS_W7P(12); } else { DTS_W7P(14); } }
-    }
-#undef DTS_W7P
-#else
 #define DTS_W7(k) \
     case k: DTS_W7I(k); break;
     switch (min(max(n, 0), 15)) {
@@ -158,7 +125,6 @@ __device__ __forceinline__ void vm_wait_rt7(int n)
     default: DTS_W7(15)
     }
 #undef DTS_W7
-#endif
 #undef DTS_W7I
 }
 
@@ -410,173 +376,6 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
     return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
 }
 
-// ---- fused vf_psnr / vf_ssim (QF walks; vf_psnr.c compute_images_mse, vf_ssim.c ssim_4x4xn /
-// ssim_end1 / ssim_plane restated in kernels.hip k_quality) ----
-// After the store exchange lane L holds bytes of output row m = L >> 2 of the row block (the
-// store's row segment, quarter q4 = L & 3): 1..4 slices of 4 pixels, each one row of a 4x4
-// block.  The reference rendition is loaded in the same layout, the slices' sums (s1, s2, ss,
-// s12) of the four rows of a block meet in the lane of its last row (DPP row shifts by 4 and 8
-// lanes), which adds the block's SSE and parks the sums in the wave's LDS block table
-// (plane-major, 5 block rows: the previous row block's last and this one's 4, BW block columns);
-// then every 8x8 window at stride 4 whose four blocks lie in this unit and whose top row is the
-// previous row block's last or one of this row block's first three is scored (ssim_end1).
-// Windows straddling two units are k_qfix7's; per unit the sums go to a QPart7.
-
-// NB reference bytes at byte `at` of a row with `room` bytes left (the plane's last columns
-// byte by byte; the rest zero)
-template <int NB>
-__device__ __forceinline__ void get_row7(uint64_t rowp, int at, int room, uint32_t (&w)[4])
-{
-    const g_u8 *p = GP6(const g_u8, rowp + (uint64_t)(int64_t)at);
-    w[0] = w[1] = w[2] = w[3] = 0;
-    if (room >= NB) {
-        if (NB == 16) {
-            const u32x4 v = *GP6(const g_u32x4, p);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else if (NB == 8) {
-            const u32x2 v = *GP6(const g_u32x2, p);
-            w[0] = v.x; w[1] = v.y;
-        } else {
-            w[0] = *GP6(const g_u32, p);
-        }
-    } else {
-        asm volatile("" : "+v"(room));
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-            if (i < room) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
-    }
-}
-
-// the reference bytes of this lane's share of row block j: the rows and byte offsets vstore7 writes
-template <int VAR, class UT>
-__device__ __forceinline__ void qload7(const UT &U, int j, const uint64_t (&qb)[2], const uint32_t (&qp)[2], int lane,
-                                       uint32_t (&r)[4])
-{
-    using W = Walk6<VAR>;
-    asm volatile("" : "+v"(lane));                       // (qrb7: nothing hoisted out of the walk)
-    const int y = 16 * j + (lane >> 2), q4 = lane & 3;
-    r[0] = r[1] = r[2] = r[3] = 0;
-    if (y >= U.dstH) return;
-    if (W::NP == 1) {
-        if (W::CT == 4) get_row7<16>(qb[0] + (uint64_t)y * qp[0], U.col0 + 16 * q4, U.dstW - U.col0 - 16 * q4, r);
-        else get_row7<8>(qb[0] + (uint64_t)y * qp[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, r);
-    } else if (U.fmt == DTS_FMT_NV12) {
-        const int at = 2 * U.col0 + 8 * W::CT * q4;
-        if (W::CT == 2) get_row7<16>(qb[0] + (uint64_t)y * qp[0], at, 2 * U.dstW - at, r);
-        else get_row7<8>(qb[0] + (uint64_t)y * qp[0], at, 2 * U.dstW - at, r);
-    } else {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            uint32_t t[4];
-            const int at = U.col0 + 4 * W::CT * q4;
-            if (W::CT == 2) get_row7<8>(qb[p] + (uint64_t)y * qp[p], at, U.dstW - at, t);
-            else get_row7<4>(qb[p] + (uint64_t)y * qp[p], at, U.dstW - at, t);
-            r[W::CT * p] = t[0];
-            if (W::CT == 2) r[2 * p + 1] = t[1];
-        }
-    }
-}
-
-// v + v of the lane 4 (8) below in the same 16-lane row (bound_ctrl: lanes without one add 0)
-__device__ __forceinline__ uint32_t rsum4x(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
-    return v;
-}
-
-__device__ __forceinline__ float ssim_end1_7(int s1, int s2, int ss, int s12)
-{
-    const int c1 = (int)(.01 * .01 * 255 * 255 * 64 + .5);
-    const int c2 = (int)(.03 * .03 * 255 * 255 * 64 * 63 + .5);
-    const int vars = ss * 64 - s1 * s1 - s2 * s2;
-    const int covar = s12 * 64 - s1 * s2;
-    return (float)(2 * s1 * s2 + c1) * (float)(2 * covar + c2) *
-           __builtin_amdgcn_rcpf((float)(s1 * s1 + s2 * s2 + c1) * (float)(vars + c2));
-}
-
-// row block j's quality: x = output bytes after the exchange (xchg7), rr = reference (qload7).
-// The block sums of rows 1..4 go to the wave's exchange scratch (free once xchg7 has read it),
-// row 0 (the previous row block's last block row) and the running sums to the wave's kQ7Wave
-// area: sse / ssim slots of u64, added by LDS atomics (integers: the same sums whatever the
-// lane order; ssim_end1 values in 2^-24 fixed point)
-template <int VAR, class UT>
-__device__ __forceinline__ void qrb7(const UT &U, int j, const uint32_t (&x)[4], const uint32_t (&rr)[4], uint8_t *scr,
-                                     uint8_t *qw, int lane)
-{
-    using W = Walk6<VAR>;
-    constexpr int NP = W::NP, BW = 4 * W::CT;           // planes, block columns per plane
-    constexpr int NS = (NP == 1 && W::CT == 4) || (NP == 2 && W::CT == 2) ? 4 : 2;   // slices per lane
-    // every lane-dependent term below is formed here, per row block: the lane index goes through an
-    // empty asm so nothing is hoisted out of the walk (it would hold ~20 VGPRs across every granule)
-    asm volatile("" : "+v"(lane));
-    const int q4 = lane & 3, m = lane >> 2, y = 16 * j + m;
-    const bool last = (m & 3) == 3;                      // the lane holding its block's sums
-    const bool il = NP == 2 && U.fmt == DTS_FMT_NV12;
-    uint32_t sse[2] = {0u, 0u};
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        // slice k: plane pk, block column bk (of the unit); nv12: dwords 2 h, 2 h + 1 hold the U V
-        // pairs of 4 columns, slice 2 h is their U, 2 h + 1 their V
-        const int pk = NP == 1 ? 0 : (il ? (k & 1) : k / (NS / 2));
-        const int bk = NP == 1 ? NS * q4 + k : (NS / 2) * q4 + (il ? k >> 1 : k % (NS / 2));
-        uint32_t ak, bk8;
-        if (il) {
-            const uint32_t sel = (k & 1) ? 0x07050301u : 0x06040200u;
-            ak = __builtin_amdgcn_perm(x[(k & ~1) + 1], x[k & ~1], sel);
-            bk8 = __builtin_amdgcn_perm(rr[(k & ~1) + 1], rr[k & ~1], sel);
-        } else {
-            ak = x[k];
-            bk8 = rr[k];
-        }
-        const int vb = min(max(U.dstW - U.col0 - 4 * bk, 0), 4);
-        const uint32_t msk = y < U.dstH ? (vb >= 4 ? 0xffffffffu : (1u << (8 * vb)) - 1u) : 0u;
-        ak &= msk;
-        bk8 &= msk;
-        const uint32_t s1 = __builtin_amdgcn_udot4(ak, 0x01010101u, 0u, false);
-        const uint32_t s2 = __builtin_amdgcn_udot4(bk8, 0x01010101u, 0u, false);
-        const uint32_t p12 = rsum4x(s1 + (s2 << 16));
-        const uint32_t ss = rsum4x(__builtin_amdgcn_udot4(bk8, bk8, __builtin_amdgcn_udot4(ak, ak, 0u, false), false));
-        const uint32_t s12 = rsum4x(__builtin_amdgcn_udot4(ak, bk8, 0u, false));
-        if (last) {
-            sse[pk] += ss - 2u * s12;
-            *reinterpret_cast<u32x4 *>(scr + 16 * ((pk * 4 + (m >> 2)) * BW + bk)) = (u32x4){p12, ss, s12, 0u};
-        }
-    }
-    unsigned long long *acc = reinterpret_cast<unsigned long long *>(qw + kQ7Acc);
-    if (last) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) atomicAdd(acc + p, (unsigned long long)sse[p]);
-    }
-    // windows: plane wp, top block row wy (0: the previous row block's last, in qw), block column wx
-    constexpr int NW = NP * 4 * (BW - 1);
-    static_assert(NW <= 64, "one window per lane");
-    if (lane < NW) {
-        const int wp = lane / (4 * (BW - 1)), rem = lane - wp * 4 * (BW - 1);
-        const int wy = rem / (BW - 1), wx = rem - wy * (BW - 1);
-        const int gy = 4 * j + wy - 1, gx = (U.col0 >> 2) + wx;
-        const uint8_t *t0 = wy ? scr + 16 * ((wp * 4 + wy - 1) * BW + wx) : qw + 16 * (wp * BW + wx);
-        const uint8_t *t1 = scr + 16 * ((wp * 4 + wy) * BW + wx);
-        uint32_t sp = 0, sq = 0, sc = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 v = *reinterpret_cast<const u32x4 *>((i >> 1 ? t1 : t0) + 16 * (i & 1));
-            sp += v.x;
-            sq += v.y;
-            sc += v.z;
-        }
-        const float v = ssim_end1_7((int)(sp & 0xffffu), (int)(sp >> 16), (int)sq, (int)sc);
-        if (gy >= 0 && gy + 1 < (U.dstH >> 2) && gx + 1 < (U.dstW >> 2))
-            atomicAdd(acc + 2 + wp, (unsigned long long)(long long)(int)(v * 16777216.f));
-    }
-    // this row block's last block row becomes the next one's row 0
-    if (lane < NP * BW) {
-        const int cp = lane / BW, cxb = lane - cp * BW;
-        *reinterpret_cast<u32x4 *>(qw + 16 * (cp * BW + cxb)) =
-            *reinterpret_cast<const u32x4 *>(scr + 16 * ((cp * 4 + 3) * BW + cxb));
-    }
-}
-
 // V of one row block over the whole ring, as vcalc (ladder_mfma.h): 65536 hh + 256 (hl +
 // lh) + ll as three chained accumulations; the bias enters as b1 << 16 (the chain's start)
 // and b2 << 8 (added with the first shift), so a per-lane bias (the ordered dither of
@@ -663,39 +462,15 @@ __device__ __forceinline__ void vcalc7p(const v4i (&rh)[Walk6<VAR>::VKB][Walk6<V
     }
 }
 
-// a wave with no unit: stage its pieces (decoupled groups: the first such wave also DMAs every
-// V fragment of the group, FragOp7 schedule in batch order), keep the group's barrier count
+// a wave with no unit: stage its pieces, keep the group's barrier count
 template <int SK>
-__device__ __forceinline__ void idle7(const Ladder7Params &P, const Group7 &G, const DevPlanes &S, int f, int wave,
-                                      int waves)
+__device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f, int wave, int waves)
 {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
-#ifdef DTS_L7_STAGER_PRIO
-    __builtin_amdgcn_s_setprio(DTS_L7_STAGER_PRIO);     // diagnostic: the staging wave issues first
-#endif
     Stage7 Z;
     Z.init(G, S, f, wave, waves, (int)threadIdx.x & 63, SK == 0 ? 1 : G.bpc);
-    const int lane = (int)threadIdx.x & 63;
-    // the fragment DMAs of batch bn (the first staging wave of a decoupled group)
-    const bool fw = DTS_L7_DECOUPLE && wave == G.st0;
-    const FragOp7 *fs = P.fsched + G.fs0, *fe = fs + (fw ? G.nfs : 0);
-    const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
-    auto frags = [&](int bn) {
-        for (; fs < fe; ++fs) {
-            const FragOp7 op = kld6(fs);
-            if (op.batch > bn) break;
-            if (DTS_L7_ABLATE & 256) continue;
-            const uint64_t src = fr + (uint64_t)op.pair * 2048u;
-            for (int h = 0; h < op.n1k; ++h)
-                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
-                                                 (__attribute__((address_space(3))) void *)(lds7 + op.lds + 1024 * h),
-                                                 16, 0, 0);
-            Z.ops += op.n1k;
-        }
-    };
 #pragma unroll
     for (int i = 0; i < NS7 - 1; ++i) {
-        frags(i);
         Z.pieces(lds7, i, i);
         Z.e[i] = Z.ops;
     }
@@ -708,7 +483,6 @@ __device__ __forceinline__ void idle7(const Ladder7Params &P, const Group7 &G, c
         group_barrier7();
         L7_STAMP(1);
         const int sn = sq == 0 ? NS7 - 1 : sq - 1;
-        frags(b + NS7 - 1);
         Z.pieces(lds7, b + NS7 - 1, sn);
         Z.shift();
         sq = sq + 1 == NS7 ? 0 : sq + 1;
@@ -736,7 +510,7 @@ __device__ __forceinline__ void idle7(const Ladder7Params &P, const Group7 &G, c
 // p010 sources add the ordered dither ff_dither_8x8_128[y & 7][(x + off) & 7] << 12 (off 3
 // for V) instead of the flat 64; p010 outputs (any source) are yuv2p010lX / cX:
 // av_clip_uintp2((sum + (1 << 16)) >> 17, 10) << 6.
-template <int VAR, bool RC, int HS, int SK, bool QF>
+template <int VAR, bool RC, int HS, int SK>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -761,22 +535,6 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             op[p] = (uint32_t)(U.kind ? D.pitch[1 + p] : D.pitch[0]);
         }
     }
-    // fused quality (QF): the rendition's reference planes of this frame, the wave's block table
-    // and its running sums
-    uint8_t *qtab = lds7 + G.qscr + kQ7Wave * wave;
-    const bool qon = QF && U.qual;
-    if (qon && lane < 4) reinterpret_cast<unsigned long long *>(qtab + kQ7Acc)[lane] = 0ull;
-    // the rendition's reference planes of this frame (re-read from the kernel arguments at each
-    // row block: nothing held across the walk)
-    auto qref7 = [&](uint64_t (&qbp)[2], uint32_t (&qpp)[2]) {
-        const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
-        const DevPlanes R = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, qref)) + U.rung);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            qbp[p] = (U.kind ? R.data[1 + p] : R.data[0]) + (uint64_t)f * (uint64_t)R.fstride;
-            qpp[p] = (uint32_t)(U.kind ? R.pitch[1 + p] : R.pitch[0]);
-        }
-    };
     const uint64_t fr = (uint64_t)(uintptr_t)P.frag + 16u * (uint32_t)lane;
     // H B operands of the walk (p010: bh = the M fragments, bl = L, ba = A of put6p)
     constexpr int BC = P10 ? RKB : HKB;
@@ -884,28 +642,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     const int FS = U.fs;
     int fsi = 0, fsu = 0;
     // the V fragments of the row blocks firing at granule <= upto (lead wave only)
-    // decoupled groups: staging waves (wave >= G.st0) issue the pieces, wave st0 the fragment
-    // schedule of the batch (FragOp7, as idle7); the other waves issue no loads and never wait
-    const bool stg = DTS_L7_DECOUPLE == 0 || (DTS_L7_DECOUPLE == 2 && wave >= G.st0);
-    const FragOp7 *fsp = P.fsched + G.fs0, *fse = fsp + (DTS_L7_DECOUPLE && wave == G.st0 ? G.nfs : 0);
-    auto fsched = [&](int bn) {
-        for (; fsp < fse; ++fsp) {
-            const FragOp7 op = kld6(fsp);
-            if (op.batch > bn) break;
-            if (DTS_L7_ABLATE & 256) continue;
-            const uint64_t src = fr + (uint64_t)op.pair * 2048u;
-            for (int h = 0; h < op.n1k; ++h)
-                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(src + 1024u * h),
-                                                 (__attribute__((address_space(3))) void *)(lds7 + op.lds + 1024 * h),
-                                                 16, 0, 0);
-            Z.ops += op.n1k;
-        }
-    };
     auto frags = [&](int upto) {
-        if (DTS_L7_DECOUPLE) {                          // the staging wave st0's schedule (batch upto / PB7)
-            fsched(upto / PB7);
-            return;
-        }
         while (fgf <= upto) {
             uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
             const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
@@ -922,18 +659,6 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             fgf1 = firev(jf + 1);
         }
     };
-    // a row block whose stores wait until after the next H (pj >= 0; DTS_L7_DEFER_ST,
-    // measured slower: cfg2 128.7k vs 145k fps; never for the 4-tile luma walk, whose H
-    // temporaries leave no room for the 4 held registers)
-    constexpr bool DEFER_ST = DTS_L7_DEFER && DTS_L7_DEFER_ST && !(CT == 4);
-    int pj = -1;
-    uint32_t px[4];
-    auto flush = [&]() {
-        if (pj >= 0) {
-            Z.ops += vstore7<VAR>(U, pj, px, ob, op, lane);
-            pj = -1;
-        }
-    };
     // the row blocks firing at granule qq (their window's last granule is in the ring)
     auto vfire = [&](int qq) {
         if (DTS_L7_ABLATE & 8) return;
@@ -946,23 +671,15 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 vl[kb] = *reinterpret_cast<const v4i *>(fu + 2048 * kb + 1024);
             }
             fsu = fsu + 1 == FS ? 0 : fsu + 1;
+            uint32_t px[4];
             bool p010out = false;
             if constexpr (CT == 1 && P10) {
                 if (U.fmt == DTS_FMT_P010LE) {              // p010 rendition
                     uint32_t w2[T][2];
                     vcalc7p<VAR>(rh, rl, vh, vl, w2);
-                    flush();
                     xchg7p<VAR>(U, w2, scr, m, g, lane, px);
                     p010out = true;
                 }
-            }
-            uint32_t qr[4] = {0, 0, 0, 0};
-            if (qon && DTS_L7_QEARLY == 2) {            // the reference row segments, in flight during V
-                uint64_t qbp[2];
-                uint32_t qpp[2];
-                qref7(qbp, qpp);
-                qload7<VAR>(U, j, qbp, qpp, lane, qr);
-                ++Z.ops;
             }
             if (!p010out) {
                 uint32_t w[T];
@@ -972,38 +689,21 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 } else {
                     vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
                 }
-                flush();
-                if (qon && DTS_L7_QEARLY == 1) {        // the reference row segments, in flight during the exchange
-                    uint64_t qbp[2];
-                    uint32_t qpp[2];
-                    qref7(qbp, qpp);
-                    qload7<VAR>(U, j, qbp, qpp, lane, qr);
-                    ++Z.ops;
-                }
                 if (DTS_L7_ABLATE & 64) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) asm volatile("" ::"v"(w[t]));
                 } else {
                     xchg7<VAR>(U, w, scr, m, g, lane, px);
                 }
-                if (qon && DTS_L7_QEARLY == 0) {        // the reference row segments
-                    uint64_t qbp[2];
-                    uint32_t qpp[2];
-                    qref7(qbp, qpp);
-                    qload7<VAR>(U, j, qbp, qpp, lane, qr);
-                    ++Z.ops;
-                }
-                if (qon) qrb7<VAR>(U, j, px, qr, scr, qtab, lane);
             }
-            pj = (DTS_L7_ABLATE & 96) ? -1 : j;
-            if (!DEFER_ST) flush();
+            if (!(DTS_L7_ABLATE & 96)) Z.ops += vstore7<VAR>(U, j, px, ob, op, lane);
             ++j;
             fg = fg1;
             fg1 = firev(j + 1);
         }
     };
 #pragma unroll
-    for (int i = 0; i < NS7 - 1 && stg; ++i) {
+    for (int i = 0; i < NS7 - 1; ++i) {
         frags(PB7 * i + PB7 - 1);
         Z.pieces(lds7, i, i);
         Z.e[i] = Z.ops;
@@ -1016,11 +716,6 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     static_assert(8 % R == 0, "ring periods divide the unroll");
     const int ngran = G.ngran;
     int sq = 0;
-#ifdef DTS_L7_HEAVY_PRIO
-    // diagnostic: the heaviest walks (4-tile one-K-block: the 1080p luma / chroma units) set
-    // the group's pace at every barrier; give them the issue port first
-    if (CT * HKB * W::NP >= 4) __builtin_amdgcn_s_setprio(DTS_L7_HEAVY_PRIO);
-#endif
     L7_STAMP_INIT;
     for (int q0 = 0; q0 < ngran; q0 += 8) {
 #pragma unroll
@@ -1028,7 +723,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             const int q = q0 + s;
             if (q >= ngran) break;
             if (s % PB7 == 0) {
-                if (stg) Z.wait_batch();
+                Z.wait_batch();
                 L7_STAMP(0);
                 group_barrier7();
                 L7_STAMP(1);
@@ -1097,27 +792,15 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                     }
             }
-            // the next batch's pieces: right after the A reads (DTS_L7_DMAPOS 0), or after the
-            // deferred row blocks (1: the 16 waves of a CU then do not all queue their DMAs
-            // on the memory pipe at the moment they leave the barrier)
-#if DTS_L7_DMAPOS == 0
-            if (s % PB7 == 0 && stg) {
+            // the next batch's pieces, right after the A reads
+            if (s % PB7 == 0) {
                 const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
                 frags(PB7 * bn + PB7 - 1);
                 Z.pieces(lds7, bn, sn);
                 Z.shift();
             }
-#endif
             L7_STAMP(2);
             if (DTS_L7_DEFER) vfire(q - 1);
-#if DTS_L7_DMAPOS == 1
-            if (s % PB7 == 0 && stg) {
-                const int sn = sq == 0 ? NS7 - 1 : sq - 1, bn = q / PB7 + NS7 - 1;
-                frags(PB7 * bn + PB7 - 1);
-                Z.pieces(lds7, bn, sn);
-                Z.shift();
-            }
-#endif
             L7_STAMP(4);
             if (!(DTS_L7_ABLATE & 16)) {
                 v4i ah[T], al[T];
@@ -1212,27 +895,13 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     }
                 }
             }
-            flush();
             L7_STAMP(3);
-            if (!DTS_L7_DEFER) vfire(q), flush();
+            if (!DTS_L7_DEFER) vfire(q);
             L7_STAMP(4);
             if (s % PB7 == PB7 - 1) sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
     if (DTS_L7_DEFER) vfire(ngran - 1);
-    flush();
-    if (qon) {                                          // the unit's partial record (fixed-order lane sums)
-        const unsigned long long *acc = reinterpret_cast<const unsigned long long *>(qtab + kQ7Acc);
-        const uint64_t e0 = acc[0], e1 = acc[1];
-        const double s0 = (double)(long long)acc[2] * (1.0 / 16777216.0), s1 = (double)(long long)acc[3] * (1.0 / 16777216.0);
-        if (lane == 0) {
-            QPart7 *qp = P.qpart + (int64_t)f * P.nunits + (G.u0 + wave);
-            qp->sse[0] = e0;
-            qp->sse[1] = e1;
-            qp->ssim[0] = s0;
-            qp->ssim[1] = s1;
-        }
-    }
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1245,7 +914,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 
 // RC: the graph converts the YUV range in the H epilogue (a separate instantiation, so
 // the common kernel keeps its register allocation)
-template <bool RC, int HS, int SK, bool QF = false>
+template <bool RC, int HS, int SK>
 __global__ __launch_bounds__(64 * kL7MaxWaves)
 #if DTS_L7_WPE > 0
 __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
@@ -1262,34 +931,34 @@ void k_ladder7(Ladder7Params P)
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
     if (wave >= G.nwaves) {
-        idle7<SK>(P, G, S, f, wave, waves);
+        idle7<SK>(G, S, f, wave, waves);
         return;
     }
     const Unit7 U = kld6(P.units + G.u0 + wave);
 #ifdef DTS_L7_ONLYVAR                       // disassembly studies of one variant's walk
     if constexpr ((SK == 2) == ((DTS_L7_ONLYVAR & 16) != 0)) {
-        walk7<DTS_L7_ONLYVAR, RC, HS, SK, QF>(P, G, U, S, f, wave, waves);
+        walk7<DTS_L7_ONLYVAR, RC, HS, SK>(P, G, U, S, f, wave, waves);
         return;
     }
 #endif
     if constexpr (SK == 2) {                // p010 sources: the 16-bit one-K-block variants
         switch (U.variant) {
-        case 16: walk7<16, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-        case 17: walk7<17, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-        default: walk7<20, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+        case 16: walk7<16, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        case 17: walk7<17, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+        default: walk7<20, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
         }
     } else {
     switch (U.variant) {
-    case 0: walk7<0, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 1: walk7<1, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 2: walk7<2, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 3: walk7<3, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 4: walk7<4, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 5: walk7<5, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 6: walk7<6, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 7: walk7<7, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    case 8: walk7<8, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
-    default: walk7<12, RC, HS, SK, QF>(P, G, U, S, f, wave, waves); break;
+    case 0: walk7<0, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 1: walk7<1, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 2: walk7<2, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 3: walk7<3, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 4: walk7<4, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 5: walk7<5, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 6: walk7<6, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 7: walk7<7, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    case 8: walk7<8, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
+    default: walk7<12, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     }
     }
 }
@@ -1310,29 +979,17 @@ int ladder7_stamps(unsigned long long *out, bool reset)
 
 // the staging geometry this build of k_ladder7 was compiled with: the planner sizes the
 // stage buffers and the V fragment slots for exactly these, and refuses any other
-void ladder7_compiled(int *stages, int *batch, int *decouple)
+void ladder7_compiled(int *stages, int *batch)
 {
     *stages = NS7;
     *batch = PB7;
-    *decouple = DTS_L7_DECOUPLE;
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
-                          int src_kind, hipStream_t s, bool quality)
+                          int src_kind, hipStream_t s)
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
-    if (quality) {                       // fused vf_psnr / vf_ssim: 8-bit sources, no range conversion
-        if (range_conv || src_kind == kSrcP010 || !p.qpart) return hipErrorInvalidValue;
-        if (src_kind == kSrcNV12) {
-            if (hsplit == 128) hipLaunchKernelGGL((k_ladder7<false, 128, 1, true>), g, b, lds_bytes, s, p);
-            else hipLaunchKernelGGL((k_ladder7<false, 256, 1, true>), g, b, lds_bytes, s, p);
-        } else {
-            if (hsplit == 128) hipLaunchKernelGGL((k_ladder7<false, 128, 0, true>), g, b, lds_bytes, s, p);
-            else hipLaunchKernelGGL((k_ladder7<false, 256, 0, true>), g, b, lds_bytes, s, p);
-        }
-        return hipGetLastError();
-    }
     if (src_kind == kSrcP010) {          // p010 sources (no range conversion: dts_graph_create refuses it)
         if (range_conv) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_ladder7<false, 256, 2>), g, b, lds_bytes, s, p);

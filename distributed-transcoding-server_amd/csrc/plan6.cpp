@@ -327,12 +327,9 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, int decouple,
-                 Plan7 &out)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out)
 {
     out = Plan7{};
-    const int wtotal = wmax;
-    if (decouple == 1) --wmax;                             // one wave of every group only stages
     // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
     // granules (the batches in flight + the one-granule V deferral; ladder7.hip)
     if (wmax < 1 || wmax > kL7MaxWaves || stages < 2 || stages > 4 || pb < 1 || pb > 2) return false;
@@ -344,7 +341,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         out.hsplit = 256;
         if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
     }
-    if (const char *hs = std::getenv("DTS_L7_HSPLIT"))    // diagnostic A/B: force the 256 split
+    if (const char *hs = diag_env("DTS_L7_HSPLIT"))       // diagnostic A/B: force the 256 split
         if (std::atoi(hs) == 256 && out.hsplit == 128) {
             out.hsplit = 256;
             if (!plan6_graph(kinds, p6, 0, false, narrow, pb * (stages + 1), 256)) return false;
@@ -365,7 +362,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         // window start of a unit (its first tile's x0) orders the plane's units left to right;
         // by_rung: groups of one rendition each (their waves do the same work per granule)
         // (diagnostic DTS_L7_SORT: 1 = by window centre, 2 = by window end)
-        const char *se = std::getenv("DTS_L7_SORT");
+        const char *se = diag_env("DTS_L7_SORT");
         const int sort_key = se ? std::atoi(se) : 0;
         auto wkey = [&](const Unit6 &w) {
             if (!sort_key) return 2 * w.x0[0];
@@ -394,7 +391,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         }
         // runs of units grouped together: the whole plane kind, or one rendition
         std::vector<std::pair<int, int>> runs;
-        const char *dpe = std::getenv("DTS_L7_DP");
+        const char *dpe = diag_env("DTS_L7_DP");
         const int dp_slack = dpe ? std::atoi(dpe) : 0;
         for (int a = 0, n = (int)us.size(); a < n;) {
             int z = a + 1;
@@ -438,7 +435,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         // SIMDs in turn).  Within each group the heaviest units (MFMAs per granule: the
         // 1080p walks) take waves 0..3 and the lightest 4..7, so no SIMD carries two heavy
         // walks of one group (the heavy waves set the group's pace at every barrier).
-        const char *bal = std::getenv("DTS_L7_BAL");
+        const char *bal = diag_env("DTS_L7_BAL");
         if (!bal || std::atoi(bal) != 0)
             for (int gi = 0, u = 0; gi < (int)runs.size(); u += runs[gi].first, ++gi) {
                 const int cnt = runs[gi].first;
@@ -516,9 +513,6 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                     v.lead = 1;
                 }
                 v.flds = flds[w.rung];
-                // fused quality: 8-bit renditions (yuv420p / nv12) of 8-bit sources
-                v.qual = kinds[kind].rungs[(size_t)w.rung].qual ? 1 : 0;
-                if (v.qual && (kinds[kind].p10 || (v.fmt != DTS_FMT_YUV420P && v.fmt != DTS_FMT_NV12))) return false;
                 if (w.ngran != g.ngran) return false;
                 out.units.push_back(v);
             }
@@ -533,78 +527,15 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         const bool last = i + 1 == out.groups.size() || out.groups[i + 1].kind != g.kind;
         g.xown = last ? kinds[g.kind].srcW : std::max(out.groups[i + 1].X0, g.X0 + 64);
     }
-    if (std::getenv("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
+    if (diag_env("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
         for (const Group7 &g : out.groups)
             std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d\n", g.kind, g.X0, g.npc, g.nwaves);
-    // decoupled groups: the staging wave's V fragment DMAs, row block by row block of every
-    // rendition, each with the source pieces of the batch holding its fire granule (the batch
-    // a rendition's lead wave would issue it with: ladder7.hip walk7 frags())
-    if (decouple)
-        for (Group7 &g : out.groups) {
-            g.fs0 = (int)out.fsched.size();
-            for (int i = g.u0; i < g.u0 + g.nwaves; ++i) {
-                const Unit7 &v = out.units[(size_t)i];
-                if (!v.lead) continue;
-                const int vkb = l6_vkb(v.variant);
-                for (int j = 0; j < v.nrb; ++j) {
-                    FragOp7 op{};
-                    op.batch = out.fire[(size_t)v.fire + j] / pb;
-                    op.pair = v.vfrag + (uint32_t)(j * vkb);
-                    op.lds = v.flds + (j % v.fs) * vkb * 2048;
-                    op.n1k = 2 * vkb;
-                    out.fsched.push_back(op);
-                }
-            }
-            std::stable_sort(out.fsched.begin() + g.fs0, out.fsched.end(),
-                             [](const FragOp7 &a, const FragOp7 &b) { return a.batch < b.batch; });
-            g.nfs = (int)out.fsched.size() - g.fs0;
-        }
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
-    if (decouple == 1) out.waves = std::max(out.waves + 1, std::min(wtotal, kL7MaxWaves));
-    // the staging waves: a group's spare waves; else all its waves (0) or its lighter half (2: the
-    // planner put the heaviest units first)
-    for (Group7 &g : out.groups)
-        g.st0 = g.nwaves < out.waves ? g.nwaves : (decouple == 2 ? g.nwaves / 2 : 0);
-    // fused quality: per wave the 4x4-block sums of its row blocks after the store exchange
-    bool anyq = false;
-    for (const Unit7 &u : out.units) anyq = anyq || u.qual;
+    // the staging waves: a group's spare waves, else all of its waves
     for (Group7 &g : out.groups) {
-        g.qscr = g.scr + out.waves * 1024;
-        out.lds_bytes = std::max(out.lds_bytes, g.qscr + (anyq ? out.waves * kQ7Wave : 0));
-    }
-    if (anyq) {
-        // per (rendition, plane): its units left to right and the boundaries between them (the
-        // block column left of each: k_qfix7 scores the windows straddling it)
-        int nr = 0;
-        for (int kind = 0; kind < 2; ++kind) nr = std::max(nr, (int)kinds[kind].rungs.size());
-        for (int r = 0; r < nr; ++r)
-            for (int kind = 0; kind < 2; ++kind) {
-                if (r >= (int)kinds[kind].rungs.size() || !kinds[kind].rungs[(size_t)r].qual) continue;
-                std::vector<std::pair<int, int>> us;           // (col0, unit)
-                for (int i = 0; i < (int)out.units.size(); ++i)
-                    if (out.units[(size_t)i].kind == kind && out.units[(size_t)i].rung == r)
-                        us.push_back({out.units[(size_t)i].col0, i});
-                std::sort(us.begin(), us.end());
-                const Plan5Rung &R = kinds[kind].rungs[(size_t)r];
-                for (int pl = kind ? 1 : 0; pl <= (kind ? 2 : 0); ++pl) {
-                    QRend7 q{};
-                    q.rung = r;
-                    q.plane = pl;
-                    q.w = R.dstW;
-                    q.h = R.dstH;
-                    q.u0 = (int)out.qunit.size();
-                    q.nu = (int)us.size();
-                    for (const auto &e : us) out.qunit.push_back(e.second);
-                    q.b0 = (int)out.qbound.size() / 2;
-                    for (size_t i = 1; i < us.size(); ++i) {
-                        out.qbound.push_back(us[i].first / 4 - 1);
-                        out.qbound.push_back((int)out.qrend.size());
-                    }
-                    q.nb = (int)out.qbound.size() / 2 - q.b0;
-                    out.qrend.push_back(q);
-                }
-            }
+        g.st0 = g.nwaves < out.waves ? g.nwaves : 0;
+        out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
     }
     return out.lds_bytes <= 160 * 1024;
 }

@@ -32,6 +32,7 @@ TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS = range(
 TM_MODES = {"none": TM_NONE, "linear": TM_LINEAR, "gamma": TM_GAMMA, "clip": TM_CLIP, "reinhard": TM_REINHARD,
             "hable": TM_HABLE, "mobius": TM_MOBIUS}
 MAX_OUTPUTS = 4
+ABI_VERSION = 6              # include/dts.h DTS_ABI_VERSION this binding lays its structs out for
 
 E_INVAL, E_NOMEM, E_RANGE, E_UNSUPPORTED, E_BUSY, E_NODEV, E_HIP = -22, -12, -34, -95, -16, -19, -1000
 
@@ -96,7 +97,10 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
            "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device", "dts_quality_run_host",
-           "dts_qraw_sum_device", "dts_qstat_stream"]
+           "dts_qraw_sum_device", "dts_qstat_stream", "dts_abi_version", "dts_abi_struct_size"]
+
+# DTS_STRUCT_* ids of dts_abi_struct_size and the ctypes layout of each (filled below)
+STRUCT_IDS = {}
 
 _lib = None
 
@@ -143,8 +147,28 @@ def lib():
     L.dts_fps_map.restype = i64
     L.dts_yadif_run_device.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(DevFrames), i32, i32, i32,
                                        ctypes.POINTER(DevFrames), vp]
+    L.dts_abi_version.argtypes = []
+    L.dts_abi_struct_size.argtypes = [i32]
+    L.dts_abi_struct_size.restype = i64
+    abi_check(L)
     _lib = L
     return L
+
+
+def abi_check(L):
+    """Refuse a library whose ABI or struct layouts differ from this binding's (a binding
+    built against another dts.h would pass misaligned specs without an error)."""
+    v = L.dts_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"libdts ABI {v}, dtsffi expects {ABI_VERSION} ({LIB_PATH})")
+    for which, cls in STRUCT_IDS.items():
+        n = L.dts_abi_struct_size(which)
+        if n != ctypes.sizeof(cls):
+            raise RuntimeError(f"libdts sizeof({cls.__name__}) = {n}, dtsffi lays out {ctypes.sizeof(cls)}")
+
+
+STRUCT_IDS.update({0: TonemapSpec, 1: OutputSpec, 2: GraphSpec, 3: Frame, 4: DevFrames, 5: QRaw, 6: QStat,
+                   7: GraphInfo})
 
 
 class DtsError(RuntimeError):

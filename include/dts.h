@@ -25,6 +25,13 @@
  *
  * Conventions: every call returns 0 (DTS_OK) or a negative DTS_E_* code and
  * never throws or aborts across the ABI.  Plain pointers and sizes only.
+ *
+ * Environment: the library reads two settings.  DTS_HOST_THREADS = host threads that
+ * pack / unpack frames on the host path (default: the hardware threads, at most 16).
+ * DTS_LADDER = 5 / 4 / 3 keeps a graph off the default ladder kernel (k_ladder7) and on
+ * a fallback (k_ladder5 / k_ladder4 / the v3 kernel) -- the fallbacks run frames whose
+ * planes are not 16-byte aligned or geometries k_ladder7 does not plan; the parity tests
+ * force them with it.  Nothing else is read (diagnostic A/B builds under tools/ read more).
  * One dts_ctx per GPU; a ctx and its graphs are single-threaded (the caller
  * serialises calls); distinct ctxs may be driven from different threads.
  */
@@ -38,7 +45,10 @@
 extern "C" {
 #endif
 
-#define DTS_ABI_VERSION 5
+/* ABI 6: dts_output_spec gained quality / qref_method (rendition quality).  A binding
+ * compiled against this header checks dts_abi_version() == DTS_ABI_VERSION and
+ * dts_abi_struct_size() of every struct it lays out before any other call. */
+#define DTS_ABI_VERSION 6
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -212,6 +222,18 @@ typedef struct dts_graph_info {
 
 const char *dts_version(void);
 const char *dts_strerror(int err);
+/* The ABI the library was built with (its DTS_ABI_VERSION), and sizeof() of each struct
+ * above as the library sees it (DTS_STRUCT_*; DTS_E_INVAL for an unknown id). */
+int dts_abi_version(void);
+int64_t dts_abi_struct_size(int which);
+#define DTS_STRUCT_TONEMAP_SPEC 0
+#define DTS_STRUCT_OUTPUT_SPEC  1
+#define DTS_STRUCT_GRAPH_SPEC   2
+#define DTS_STRUCT_FRAME        3
+#define DTS_STRUCT_DEV_FRAMES   4
+#define DTS_STRUCT_QRAW         5
+#define DTS_STRUCT_QSTAT        6
+#define DTS_STRUCT_GRAPH_INFO   7
 
 int dts_device_count(int *count);
 int dts_ctx_create(int device, dts_ctx **out);
@@ -229,7 +251,9 @@ int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info);
  * frame-major (dst[f*nout + k]); src holds nframes (+ 2 with deint: see above).
  * qref/q may be NULL when quality is off.  With rendition quality (dts_output_spec
  * quality) q, if not NULL, holds nframes*nout statistics, frame-major like dst
- * (entries of outputs without quality are zeroed) and qref is not used.
+ * (entries of outputs without quality are zeroed) and qref is not used.  A graph with
+ * an output whose qref_method is DTS_QREF_EXTERNAL is refused (DTS_E_UNSUPPORTED):
+ * external references come with dts_graph_run_device only.
  * The caller keeps every buffer alive until dts_graph_wait returns. */
 int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes,
                      const dts_frame *dst, const dts_frame *qref, dts_qstat *q);

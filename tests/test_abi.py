@@ -46,3 +46,42 @@ def test_no_device_is_reported_not_fatal():
         return
     h = ctypes.c_void_p()
     assert D.lib().dts_ctx_create(0, ctypes.byref(h)) == D.E_NODEV
+
+
+def test_abi_version_matches_header():
+    """DTS_ABI_VERSION in include/dts.h == the library's == the binding's, and the version
+    string names it (the header stayed at 5 after the ABI-6 struct change)."""
+    src = open(os.path.join(ROOT, "include", "dts.h")).read()
+    hv = int(re.search(r"#define DTS_ABI_VERSION (\d+)", src).group(1))
+    L = D.lib()
+    assert L.dts_abi_version() == hv == D.ABI_VERSION
+    assert f"abi {hv}".encode() in L.dts_version()
+
+
+def test_struct_sizes_match_library():
+    """sizeof() of every ABI struct as the library sees it == the ctypes layout, and every
+    DTS_STRUCT_* id the header defines is answered (unknown ids -> DTS_E_INVAL)."""
+    src = open(os.path.join(ROOT, "include", "dts.h")).read()
+    ids = {int(v): n for n, v in re.findall(r"#define DTS_STRUCT_([A-Z_]+)\s+(\d+)", src)}
+    assert sorted(ids) == sorted(D.STRUCT_IDS)
+    L = D.lib()
+    for which, cls in D.STRUCT_IDS.items():
+        assert L.dts_abi_struct_size(which) == ctypes.sizeof(cls), (ids[which], cls.__name__)
+    assert L.dts_abi_struct_size(99) == D.E_INVAL
+    # the ABI-6 layout: dts_output_spec = 4 int32 + 2 double + 2 int32
+    assert ctypes.sizeof(D.OutputSpec) == 40
+
+
+def test_binding_refuses_abi_mismatch(monkeypatch):
+    """dtsffi.abi_check raises on a library reporting another ABI version."""
+    L = D.lib()
+
+    class Fake:
+        def dts_abi_version(self):
+            return D.ABI_VERSION + 1
+
+        def dts_abi_struct_size(self, which):
+            return L.dts_abi_struct_size(which)
+    import pytest
+    with pytest.raises(RuntimeError, match="ABI"):
+        D.abi_check(Fake())

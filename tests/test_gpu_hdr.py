@@ -22,14 +22,15 @@ BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
 MAX_OFF_BY_ONE = 0.01
 
 
-@pytest.fixture(params=["v7", "v4", "v3"])
+@pytest.fixture(params=["default", "v3"])
 def ladder_kernel(request, monkeypatch):
-    """The default choice (k_ladder7's 16-bit walks for p010 sources where they fit),
-    DTS_LADDER=4 (k_ladder4) and DTS_LADDER=3."""
-    if request.param == "v7":
+    """The library's choice (258-wide planes are not k_ladder7's: k_ladder5 runs the 8-bit
+    sources, k_ladder4 the p010 ones) and DTS_LADDER=3 (the v3 kernel, k_ladder4's own
+    fallback for geometries it does not plan)."""
+    if request.param == "default":
         monkeypatch.delenv("DTS_LADDER", raising=False)
-    else:
-        monkeypatch.setenv("DTS_LADDER", request.param[1])
+        return request.param
+    monkeypatch.setenv("DTS_LADDER", request.param[1])
     return request.param
 
 

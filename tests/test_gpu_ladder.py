@@ -17,12 +17,23 @@ pytestmark = pytest.mark.gpu
 BIC, BIL, LAN = D.SCALE_BICUBIC, D.SCALE_BILINEAR, D.SCALE_LANCZOS
 
 
-@pytest.fixture(autouse=True, params=["v7", "v5", "v4", "v3"])
+KERNELS = ["v7", "v5", "v4", "v3"]
+
+
+@pytest.fixture(autouse=True)
+def _default_kernel(monkeypatch):
+    """Every case runs on the library's own kernel choice: k_ladder7 wherever the graph fits
+    it and the planes are 16-byte aligned; k_ladder5 for 8-bit sources it does not plan (the
+    odd sizes below: plane widths not multiples of 16), k_ladder4 / the v3 kernel for such
+    p010 sources.  The fallbacks on geometries k_ladder7 would take are forced (DTS_LADDER)
+    only in the `ladder_kernel` tests."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+
+
+@pytest.fixture(params=KERNELS)
 def ladder_kernel(request, monkeypatch):
-    """Every parity case runs four times: the default kernel choice (v7, the
-    strip-staged matrix-core ladder, wherever the graph fits it and the planes are
-    16-byte aligned, else v5), DTS_LADDER=5 (v5 where it fits), DTS_LADDER=4 (v4 where the geometry fits it, else v3) and
-    DTS_LADDER=3 (v3 for every plane)."""
+    """The default choice (v7), DTS_LADDER=5 (v5 where it fits), DTS_LADDER=4 (v4 where the
+    geometry fits it, else v3) and DTS_LADDER=3 (v3 for every plane)."""
     if request.param == "v7":
         monkeypatch.delenv("DTS_LADDER", raising=False)
     else:
@@ -235,12 +246,10 @@ V7_GEOMS = [
 
 @pytest.mark.parametrize("sw,sh,outs", V7_GEOMS)
 @pytest.mark.parametrize("method", [BIC, LAN, BIL, D.SCALE_AREA])
-def test_v7_geometries(ctx, ladder_kernel, sw, sh, outs, method):
+def test_v7_geometries(ctx, sw, sh, outs, method):
     """Plane widths that are multiples of 16 (k_ladder7's domain): single-granule
     planes, upscales, tall / wide planes, 1:1 renditions; nv12 and yuv420p outputs,
-    bit-exact vs the oracle on every kernel."""
-    if ladder_kernel != "v7":
-        pytest.skip("the v5 / v4 / v3 kernels are covered by the other geometry tests")
+    bit-exact vs the oracle."""
     rng = np.random.default_rng(sw + 7 * sh + method)
     frames = [random_frame(sw, sh, D.FMT_YUV420P, rng), D.synth_host(sw, sh, D.FMT_YUV420P, 0, 5, 3)]
     run_and_check(ctx, sw, sh, D.FMT_YUV420P,
@@ -248,10 +257,11 @@ def test_v7_geometries(ctx, ladder_kernel, sw, sh, outs, method):
                   frames)
 
 
+@pytest.mark.parametrize("kernel", ["v7", "v5"])
 @pytest.mark.parametrize("src_range,dst_range", [(0, 1), (1, 0)])
 @pytest.mark.parametrize("method", [BIC, LAN, BIL])
 @pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12])
-def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method, sfmt):
+def test_range_conversion(ctx, monkeypatch, kernel, src_range, dst_range, method, sfmt):
     """`scale=in_range:out_range`: swscale.c's lum/chrRange{To,From}Jpeg_c on the
     15-bit H output, in k_ladder7's H epilogue, bit-exact vs the oracle (random and
     full-swing frames, nv12 and yuv420p renditions; planar and nv12 sources -- nv12
@@ -259,7 +269,8 @@ def test_range_conversion(ctx, ladder_kernel, src_range, dst_range, method, sfmt
     sw, sh = 384, 216
     outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_YUV420P, method), (384, 216, D.FMT_NV12, method)]
     spec = D.make_spec(sw, sh, sfmt, outs, src_range=src_range, dst_range=dst_range)
-    if ladder_kernel != "v7":
+    if kernel != "v7":
+        monkeypatch.setenv("DTS_LADDER", kernel[1])
         with pytest.raises(D.DtsError):
             D.Graph(ctx, spec)
         return
@@ -297,6 +308,29 @@ def test_clip_stress(ctx, method):
     frames = [[y, u, v], [255 - y, 255 - u, 255 - v]]
     run_and_check(ctx, w, h, D.FMT_YUV420P, [(128, 32, D.FMT_NV12, method), (85, 21, D.FMT_YUV420P, method),
                                              (300, 70, D.FMT_NV12, method)], frames)
+
+
+# A cross-section of the cases above on every kernel (the fallbacks forced onto geometries
+# k_ladder7 would take: what a device batch whose planes are not 16-byte aligned runs on)
+FALLBACK_CASES = [
+    ("ladder", 384, 216, D.FMT_YUV420P, [(192, 108, D.FMT_NV12, BIC), (128, 72, D.FMT_NV12, BIC),
+                                         (86, 48, D.FMT_NV12, BIC)]),
+    ("lanczos-up", 100, 60, D.FMT_YUV420P, [(150, 90, D.FMT_YUV420P, LAN), (150, 90, D.FMT_NV12, LAN)]),
+    ("odd", 333, 211, D.FMT_YUV420P, [(97, 55, D.FMT_YUV420P, D.SCALE_AREA), (97, 55, D.FMT_NV12, BIL)]),
+    ("nv12", 258, 146, D.FMT_NV12, [(130, 74, D.FMT_NV12, LAN), (97, 51, D.FMT_YUV420P, BIC)]),
+    ("p010", 258, 146, D.FMT_P010LE, [(130, 74, D.FMT_NV12, BIC), (258, 146, D.FMT_YUV420P, LAN)]),
+    ("downscale", 520, 300, D.FMT_YUV420P, [(346, 200, D.FMT_NV12, D.SCALE_GAUSS), (171, 97, D.FMT_NV12, BIC),
+                                            (104, 60, D.FMT_NV12, BIL)]),
+    ("tall", 256, 1000, D.FMT_YUV420P, [(64, 900, D.FMT_NV12, BIC), (128, 250, D.FMT_YUV420P, LAN)]),
+]
+
+
+@pytest.mark.parametrize("case", FALLBACK_CASES, ids=[c[0] for c in FALLBACK_CASES])
+def test_fallback_kernels(ctx, ladder_kernel, case):
+    _name, sw, sh, sfmt, outs = case
+    rng = np.random.default_rng(sw + sh + sfmt)
+    frames = [random_frame(sw, sh, sfmt, rng), D.synth_host(sw, sh, sfmt, 0, 0x5EED, 1)]
+    run_and_check(ctx, sw, sh, sfmt, outs, frames)
 
 
 def test_many_batches_device_queue(ctx):

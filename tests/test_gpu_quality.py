@@ -30,7 +30,10 @@ def check_q(got, want):
         assert got["ssim_all"] == pytest.approx(want["ssim_all"], abs=SSIM_TOL)
 
 
-@pytest.mark.parametrize("w,h", [(64, 36), (37, 23), (258, 146), (1001, 67), (8, 8), (4, 4)])
+# 64x260 / 128x520: a plane whose last block row is the apron row of a whole walk
+# ((h >> 2) - 1 a multiple of 4 tiles x 16 block rows; 128x520 hits it in the chroma)
+@pytest.mark.parametrize("w,h", [(64, 36), (37, 23), (258, 146), (1001, 67), (8, 8), (4, 4), (64, 260), (128, 520),
+                                 (66, 1030)])
 def test_quality_vs_oracle(ctx, w, h):
     import torch
     rng = np.random.default_rng(w * h)
@@ -97,7 +100,7 @@ def test_graph_quality_host_path(ctx):
         check_q(qs[f], orc.quality_frame(w, h, want_img, ref[f]))
 
 
-@pytest.mark.parametrize("w,h", [(64, 36), (130, 74), (854, 480)])
+@pytest.mark.parametrize("w,h", [(64, 36), (130, 74), (854, 480), (64, 260), (128, 520)])
 def test_quality_nv12_vs_oracle(ctx, w, h):
     """nv12 batches (cfg5's renditions): the kernel reads U / V from the interleaved
     plane; vf_psnr / vf_ssim take planar yuv420p, so the oracle gets the

@@ -5,6 +5,7 @@
 - fps map, synthetic source determinism, frame layout, qstat finishing.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -169,15 +170,13 @@ def test_plan_v4_falls_back_per_plane_kind(monkeypatch):
 
 def test_plan_v7_groups(monkeypatch):
     """cfg2 on v7: the work units (K windows on 16-column boundaries) in strip groups of
-    at most DTS_L7_W waves; planes whose widths are not multiples of 16 run on v5."""
+    at most 8 waves (13 luma + 13 chroma groups); planes whose widths are not multiples
+    of 16 run on v5."""
     monkeypatch.delenv("DTS_LADDER", raising=False)
-    for w, ngroups in [(8, 13 + 13), (16, 7 + 7), (4, 25 + 25)]:
-        monkeypatch.setenv("DTS_L7_W", str(w))
-        info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
-        assert info.ladder_v5 == 3
-        assert info.njobs == ngroups                      # 97 luma and 97 chroma units
-        assert info.lds_bytes <= 160 * 1024
-    monkeypatch.delenv("DTS_L7_W", raising=False)
+    info = D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K))
+    assert info.ladder_v5 == 3
+    assert info.njobs == 13 + 13                          # 97 luma and 97 chroma units
+    assert info.lds_bytes <= 160 * 1024
     assert D.graph_plan(D.make_spec(3848, 2160, D.FMT_YUV420P, LADDER4K)).ladder_v5 == 1
     assert D.graph_plan(D.make_spec(384, 216, D.FMT_YUV420P, [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC)])).ladder_v5 == 3
 
@@ -206,25 +205,31 @@ def test_plan_range_conversion(monkeypatch):
     assert D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1, dst_range=1)).ladder_v5 == 1
 
 
-@pytest.mark.parametrize("knob", [("DTS_L7_PB", "1"), ("DTS_L7_NS", "3"), ("DTS_L7_NS", "4")])
-def test_l7_staging_knobs_must_match_the_kernel(monkeypatch, knob):
-    """DTS_L7_PB / DTS_L7_NS may only restate the staging geometry the linked
-    k_ladder7 was compiled with (a planner sized for one
-    granule per batch let the kernel overrun its V fragment slots).  Any other
-    value is refused at planning time instead of miscomputed."""
-    spec = D.make_spec(3840, 2160, D.FMT_YUV420P, [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC)], max_batch=64)
-    assert D.graph_plan(spec).ladder_v5 == 3          # k_ladder7 without the knob
+@pytest.mark.parametrize("knob", [("DTS_L7_W", "4"), ("DTS_L7_NS", "3"), ("DTS_L7_GROUP", "r"),
+                                  ("DTS_L7_NARROW", "1"), ("DTS_ORDER", "h"), ("DTS_QFUSE", "1")])
+def test_diagnostic_knobs_do_not_reach_the_library(monkeypatch, knob):
+    """The default libdts.so reads DTS_HOST_THREADS and DTS_LADDER only (include/dts.h): the
+    A/B knobs of the diagnostic builds (tools/, -DDTS_DIAG_KNOBS) leave the plan unchanged."""
+    monkeypatch.delenv("DTS_LADDER", raising=False)
+    spec = D.make_spec(3840, 2160, D.FMT_YUV420P, LADDER4K, max_batch=64)
+    base = D.graph_plan(spec)
     monkeypatch.setenv(*knob)
-    with pytest.raises(D.DtsError) as e:
-        D.graph_plan(spec)
-    assert e.value.code == D.E_INVAL
+    info = D.graph_plan(spec)
+    assert (info.ladder_v5, info.njobs, info.lds_bytes) == (base.ladder_v5, base.njobs, base.lds_bytes) == \
+        (3, 26, base.lds_bytes)
 
 
-def test_l7_staging_knobs_restating_the_build_are_accepted(monkeypatch):
-    spec = D.make_spec(3840, 2160, D.FMT_YUV420P, [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC)], max_batch=64)
-    monkeypatch.setenv("DTS_L7_PB", "2")
-    monkeypatch.setenv("DTS_L7_NS", "2")
-    assert D.graph_plan(spec).ladder_v5 == 3
+def test_library_reads_only_documented_settings():
+    """No getenv in the product sources but the two documented settings (and diag_env, which
+    reads nothing unless built with -DDTS_DIAG_KNOBS)."""
+    import glob
+    import re
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "distributed-transcoding-server_amd", "csrc")
+    names = set()
+    for f in glob.glob(os.path.join(csrc, "*")):
+        names |= set(re.findall(r"getenv\(\"([A-Z0-9_]+)\"\)", open(f).read()))
+    assert names == {"DTS_HOST_THREADS", "DTS_LADDER"}, names
 
 
 def test_qstat_stream_is_vf_psnr_ssim_end_of_stream():

@@ -26,6 +26,7 @@ for s in "$@"; do
     all)    step tests_all 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 300 python -u bench.py --steps 20 --warmup 3 ;;
+    bench:*) wl=${s#bench:}; step bench_$wl 300 python -u bench.py --steps 10 --warmup 2 --workload $wl --no-cpu ;;
     benchq) step benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu ;;
     benchv3) DTS_LADDER=3 step benchv3 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
     benchw4) DTS_LIB=$PWD/distributed-transcoding-server_amd/lib/libdts_w4.so step benchw4 300 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-verify ;;
