@@ -1291,6 +1291,12 @@ static int yadif_enqueue(dts_ctx *ctx, int w, int h, int mode, int tff, const dt
     p.mode = mode;
     p.tff = tff ? 1 : 0;
     p.aligned = planes_ok(seq, w, h, DTS_FMT_YUV420P, 4) && planes_ok(dst, w, h, DTS_FMT_YUV420P, 4);
+    p.first = first;
+    p.dst = to_dev(dst, DTS_FMT_YUV420P);
+    if (yadif_t_ok(p) && !diag_env("DTS_YADIF_V1")) {    // the temporal walk (16-byte aligned frames)
+        HIPCHK(ctx, launch_yadif_t(p, count, st));
+        return DTS_OK;
+    }
     const int chunk = 32768;                              // outputs per launch (grid z)
     for (int j0 = 0; j0 < count; j0 += chunk) {
         const int n = std::min(chunk, count - j0);

@@ -311,6 +311,280 @@ __global__ void __launch_bounds__(256) k_yadif(const YadifParams P)
     for (int y = y0; y < y1; ++y) yadif_quad(P, p, w, h, y, x0, o, i, ip, in, is_second);
 }
 
+// ---------------------------------------------------------------------------
+// k_yadif_t: the temporal walk.  One workgroup = a kYtW x kYtH tile of one plane, walking
+// kYtWalk consecutive input frames (every field output of each).  Output frame i reads
+// frames i - 1, i, i + 1 (vf_yadif prev / cur / next), so the tile of frame i + 1 staged for
+// output i is output i + 1's cur and output i + 2's prev: a ring of four LDS slots holds
+// prev, cur, next and the frame in flight, and each step stages ONE new frame tile (its
+// rows y0 - 2 .. y1 + 1 and 16 columns each side: every row and column filter_line reads,
+// reflections at the plane's top / bottom included) by LDS-DMA, one step ahead of its use.
+// HBM and L2 see each source frame about once per output instead of the 2.5 frames the
+// per-output kernel above fetches.  A thread computes 16 pixels of one interpolated row
+// from LDS (cur rows y -+ 1 as 48-byte windows for the x -+ 3 spatial search) and copies 16
+// bytes of one kept row; the 3-byte window sums of the spatial search are v_sad_u8 of
+// v_perm-aligned operands.  Sources and outputs 16-byte aligned, w >= 16.
+// ---------------------------------------------------------------------------
+constexpr int kYtW = 512;                       // output columns per tile (32 lanes x 16)
+constexpr int kYtH = 32;                        // output rows per tile (16 interpolated + 16 kept)
+constexpr int kYtPitch = kYtW + 32;             // LDS row: 16 columns of halo each side
+constexpr int kYtRows = kYtH + 4;               // rows y0 - 2 .. y0 + kYtH + 1
+constexpr int kYtChunks = kYtPitch / 16;        // 16-byte chunks per LDS row (34)
+constexpr int kYtSlot = kYtRows * kYtPitch;     // one frame tile (19,584 B)
+constexpr int kYtPieces = (kYtRows * kYtChunks + 63) / 64;   // 1-KB LDS-DMA pieces per frame tile
+constexpr int kYtThreads = 512;
+#ifndef DTS_YADIF_WALK
+#define DTS_YADIF_WALK 16
+#endif
+constexpr int kYtWalk = DTS_YADIF_WALK;         // input frames per workgroup
+
+namespace {
+
+// s_waitcnt vmcnt(min(n, 15)) for a run-time n >= 0
+__device__ __forceinline__ void vm_wait_yt(int n)
+{
+#define DTS_WYT(k) \
+    case k: __builtin_amdgcn_s_waitcnt((k) | (7 << 4) | (15 << 8)); break;
+    switch (min(max(n, 0), 15)) {
+        DTS_WYT(0) DTS_WYT(1) DTS_WYT(2) DTS_WYT(3) DTS_WYT(4) DTS_WYT(5) DTS_WYT(6) DTS_WYT(7)
+        DTS_WYT(8) DTS_WYT(9) DTS_WYT(10) DTS_WYT(11) DTS_WYT(12) DTS_WYT(13) DTS_WYT(14)
+    default: DTS_WYT(15)
+    }
+#undef DTS_WYT
+}
+
+__device__ __forceinline__ int byte_at(const uint32_t *a, int i) { return (int)((a[i >> 2] >> (8 * (i & 3))) & 255u); }
+
+// bytes i, i + 1, i + 2 of a[] in the low three bytes of a dword (top byte 0)
+__device__ __forceinline__ uint32_t win3(const uint32_t *a, int i)
+{
+    const uint32_t b = (uint32_t)(i & 3);
+    const uint32_t sel = b | ((b + 1) << 8) | ((b + 2) << 16) | (0x0cu << 24);
+    return __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], sel);
+}
+
+__device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn_sad_u8((uint32_t)a, (uint32_t)b, 0u); }
+
+// vf_yadif.c filter_line_c / filter_edges for the 16 pixels x .. x + 15 of one interpolated
+// row.  cm / cp: cur rows mrefs / prefs, bytes x - 16 .. x + 31 (pixel k at byte 16 + k);
+// the rest bytes x .. x + 15: pm / pp prev rows mrefs / prefs, nm / np next, p2 / n2 prev2 /
+// next2 on this row, p2m .. n2p prev2 / next2 two rows away (mode 0 only).  ne: bit k set
+// when pixel k is not an edge pixel (3 <= x + k < w - 3).
+template <bool FAR>
+__device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t (&cp)[12], const uint32_t (&pm)[4],
+                                        const uint32_t (&pp)[4], const uint32_t (&nm)[4], const uint32_t (&np)[4],
+                                        const uint32_t (&p2)[4], const uint32_t (&n2)[4], const uint32_t (&p2m)[4],
+                                        const uint32_t (&p2p)[4], const uint32_t (&n2m)[4], const uint32_t (&n2p)[4],
+                                        uint32_t ne, uint32_t (&out)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int X = 16 + k;
+        const int c = byte_at(cm, X), e = byte_at(cp, X);
+        const int a2 = byte_at(p2, k), b2 = byte_at(n2, k);
+        const int d = (a2 + b2) >> 1;
+        const int td0 = absd(a2, b2);
+        const int td1 = (absd(byte_at(pm, k), c) + absd(byte_at(pp, k), e)) >> 1;
+        const int td2 = (absd(byte_at(nm, k), c) + absd(byte_at(np, k), e)) >> 1;
+        int diff = max(max(td0 >> 1, td1), td2);
+        int pred = (c + e) >> 1;
+        if ((ne >> k) & 1u) {
+            // CHECK(j): the 3-byte windows cm[x + j - 1 ..] vs cp[x - j - 1 ..]
+            int score = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 1), win3(cp, X - 1), 0u) - 1;
+            const int sm1 = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 2), win3(cp, X), 0u);
+            const int sm2 = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 3), win3(cp, X + 1), 0u);
+            const int s1 = (int)__builtin_amdgcn_sad_u8(win3(cm, X), win3(cp, X - 2), 0u);
+            const int s2 = (int)__builtin_amdgcn_sad_u8(win3(cm, X + 1), win3(cp, X - 3), 0u);
+            const bool b1 = sm1 < score;
+            score = b1 ? sm1 : score;
+            pred = b1 ? (byte_at(cm, X - 1) + byte_at(cp, X + 1)) >> 1 : pred;
+            const bool bb2 = b1 && sm2 < score;
+            score = bb2 ? sm2 : score;
+            pred = bb2 ? (byte_at(cm, X - 2) + byte_at(cp, X + 2)) >> 1 : pred;
+            const bool b3 = s1 < score;
+            score = b3 ? s1 : score;
+            pred = b3 ? (byte_at(cm, X + 1) + byte_at(cp, X - 1)) >> 1 : pred;
+            const bool b4 = b3 && s2 < score;
+            pred = b4 ? (byte_at(cm, X + 2) + byte_at(cp, X - 2)) >> 1 : pred;
+        }
+        if (FAR) {
+            const int b = (byte_at(p2m, k) + byte_at(n2m, k)) >> 1;
+            const int f = (byte_at(p2p, k) + byte_at(n2p, k)) >> 1;
+            const int mx = max(max(d - e, d - c), min(b - c, f - e));
+            const int mn = min(min(d - e, d - c), max(b - c, f - e));
+            diff = max(max(diff, mn), -mx);
+        }
+        // diff >= 0, so the reference's two-sided clamp is a median
+        pred = min(max(pred, d - diff), d + diff);
+        out[k >> 2] |= (uint32_t)pred << (8 * (k & 3));
+    }
+}
+
+typedef unsigned int u32x4y __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4y g_u32x4y;
+typedef __attribute__((address_space(1))) uint8_t g_u8y;
+__device__ __forceinline__ u32x4y lds16(const uint8_t *p) { return *reinterpret_cast<const u32x4y *>(p); }
+__device__ __forceinline__ void put16(uint64_t dst, u32x4y v, int room)
+{
+    if (room >= 16) {
+        *(g_u32x4y *)(uintptr_t)dst = v;
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int i = 0; i < room; ++i) ((g_u8y *)(uintptr_t)dst)[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+}
+__device__ __forceinline__ void unpack4(u32x4y v, uint32_t *o)
+{
+    o[0] = v.x;
+    o[1] = v.y;
+    o[2] = v.z;
+    o[3] = v.w;
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int tiles_l, int tiles_c, int txl, int txc,
+                                                        int count)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t yl[];
+    // tile of this workgroup: the tiles of one XCD (b mod 8) are consecutive in raster order,
+    // so neighbouring tiles' halo rows / columns meet in the same L2
+    const int ntiles = tiles_l + 2 * tiles_c, per = (ntiles + 7) >> 3;
+    const int b = (int)blockIdx.x, tix = (b & 7) * per + (b >> 3);
+    if (tix >= ntiles) return;
+    int p = 0, tl = tix, tx_n = txl;
+    if (tl >= tiles_l) {
+        tl -= tiles_l;
+        p = 1 + (tl >= tiles_c);
+        if (p == 2) tl -= tiles_c;
+        tx_n = txc;
+    }
+    const int w = p ? (P.w + 1) >> 1 : P.w, h = p ? (P.h + 1) >> 1 : P.h;
+    const int x0 = (tl % tx_n) * kYtW, y0 = (tl / tx_n) * kYtH;
+    const int fields = (P.mode & 1) ? 2 : 1;
+    const int j0 = (int)blockIdx.y * kYtWalk, j1 = min(count, j0 + kYtWalk);   // outputs' input frames, relative
+    const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t pitch = P.seq.pitch[p];
+    const uint64_t sbase = P.seq.data[p];
+    const int wr16 = (w + 15) & ~15;
+    // one frame tile (sequence frame clamped to [0, nseq)) into LDS slot s: this wave's pieces
+    int ops = 0;
+    auto stage = [&](int pos, int s) {
+        const int f = min(max(P.first + pos, 0), P.nseq - 1);
+        const uint64_t fb = sbase + (uint64_t)f * (uint64_t)P.seq.fstride;
+        for (int k = wave; k < kYtPieces; k += kYtThreads / 64) {
+            const int q = k * 64 + lane;
+            if (q < kYtRows * kYtChunks) {
+                const int r = q / kYtChunks, ch = q - r * kYtChunks;
+                const int yy = min(max(y0 - 2 + r, 0), h - 1);
+                const int xx = min(max(x0 - 16 + 16 * ch, 0), wr16 - 16);
+                __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)(fb + (uint64_t)((int64_t)yy * pitch) + (uint64_t)xx),
+                                                 (__attribute__((address_space(3))) void *)(yl + s * kYtSlot + 1024 * k),
+                                                 16, 0, 0);
+            }
+            ++ops;
+        }
+    };
+    // every output row of this tile is whole and every 16-byte segment inside the plane: the
+    // stores are exactly two wave-instructions per step (else their count is not tracked)
+    const bool whole = x0 + kYtW <= w && y0 + kYtH <= h;
+    stage(j0 - 1, 0);
+    stage(j0, 1);
+    stage(j0 + 1, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int nst = 0;                               // this wave's stores of the previous step (when counted)
+    const int ci = t & 31, ri = t >> 5;        // 16 columns of one interpolated and one kept row
+    const int x = x0 + 16 * ci;
+    const uint64_t obase0 = P.dst.data[p] + (uint64_t)x;
+    for (int j = j0; j < j1; ++j) {
+        const int s = j - j0;
+        if (s) __syncthreads();                // every wave is done with frame j - 2's slot
+        const int dma0 = ops;
+        if (j + 2 <= j1) stage(j + 2, (s + 3) & 3);
+        // frame j + 1's pieces: issued before the previous step's stores and these pieces
+        vm_wait_yt(nst + (ops - dma0));
+        __syncthreads();
+        const uint8_t *sl_p = yl + ((s + 0) & 3) * kYtSlot, *sl_c = yl + ((s + 1) & 3) * kYtSlot,
+                      *sl_n = yl + ((s + 2) & 3) * kYtSlot;
+        nst = 0;
+        for (int is2 = 0; is2 < fields; ++is2) {
+            const int td_parity = P.tff ^ !is2, parity = td_parity ^ P.tff;
+            const int o = j * fields + is2;
+            const uint64_t obase = obase0 + (uint64_t)o * (uint64_t)P.dst.fstride;
+            const int64_t dp = P.dst.pitch[p];
+            const int off = ((y0 ^ td_parity) & 1) ? 0 : 1;     // y0 + off: the tile's first interpolated row
+            // kept row: a copy of cur
+            {
+                const int y = y0 + 2 * ri + (1 - off);
+                if (y < h && x < w) {
+                    const u32x4y v = lds16(sl_c + (y - y0 + 2) * kYtPitch + 16 * ci + 16);
+                    put16(obase + (uint64_t)((int64_t)y * dp), v, w - x);
+                }
+            }
+            const int y = y0 + 2 * ri + off;
+            if (y < h && x < w) {
+                const int rm = y ? y - 1 : y + 1, rp = y + 1 < h ? y + 1 : y - 1;
+                const bool far = !((P.mode & 2) || y == 1 || y + 2 == h);
+                const uint8_t *prv = sl_p, *cur = sl_c, *nxt = sl_n;
+                const uint8_t *pv2 = parity ? prv : cur, *nx2 = parity ? cur : nxt;
+                auto row = [&](const uint8_t *sl, int yy) { return sl + (yy - y0 + 2) * kYtPitch + 16 * ci + 16; };
+                uint32_t cm[12], cp[12], pm[4], pp[4], nm[4], np[4], p2[4], n2[4], p2m[4], p2p[4], n2m[4], n2p[4];
+#pragma unroll
+                for (int h3 = 0; h3 < 3; ++h3) {
+                    unpack4(lds16(row(cur, rm) - 16 + 16 * h3), cm + 4 * h3);
+                    unpack4(lds16(row(cur, rp) - 16 + 16 * h3), cp + 4 * h3);
+                }
+                unpack4(lds16(row(prv, rm)), pm);
+                unpack4(lds16(row(prv, rp)), pp);
+                unpack4(lds16(row(nxt, rm)), nm);
+                unpack4(lds16(row(nxt, rp)), np);
+                unpack4(lds16(row(pv2, y)), p2);
+                unpack4(lds16(row(nx2, y)), n2);
+                uint32_t ne = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) ne |= (x + k >= 3 && x + k < w - 3) ? 1u << k : 0u;
+                uint32_t res[4];
+                if (far) {
+                    const int rm2 = 2 * rm - y, rp2 = 2 * rp - y;   // 2 mrefs / 2 prefs
+                    unpack4(lds16(row(pv2, rm2)), p2m);
+                    unpack4(lds16(row(pv2, rp2)), p2p);
+                    unpack4(lds16(row(nx2, rm2)), n2m);
+                    unpack4(lds16(row(nx2, rp2)), n2p);
+                    yadif16<true>(cm, cp, pm, pp, nm, np, p2, n2, p2m, p2p, n2m, n2p, ne, res);
+                } else {
+                    yadif16<false>(cm, cp, pm, pp, nm, np, p2, n2, p2m, p2p, n2m, n2p, ne, res);
+                }
+                put16(obase + (uint64_t)((int64_t)y * dp), (u32x4y){res[0], res[1], res[2], res[3]}, w - x);
+            }
+            nst += 2;
+        }
+        if (!whole) nst = 0;                   // (edge tiles: wait for their stores too)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool yadif_t_ok(const YadifParams &p)
+{
+    for (int pl = 0; pl < 3; ++pl)
+        if (((p.seq.data[pl] | (uint64_t)p.seq.pitch[pl]) & 15u) || ((p.dst.data[pl] | (uint64_t)p.dst.pitch[pl]) & 15u))
+            return false;
+    return ((p.seq.fstride | p.dst.fstride) & 15) == 0 && p.w >= 16 && p.h >= 4;
+}
+
+hipError_t launch_yadif_t(const YadifParams &p, int count, hipStream_t s)
+{
+    const int cw = (p.w + 1) >> 1, ch = (p.h + 1) >> 1;
+    const int txl = (p.w + kYtW - 1) / kYtW, txc = (cw + kYtW - 1) / kYtW;
+    const int tiles_l = txl * ((p.h + kYtH - 1) / kYtH), tiles_c = txc * ((ch + kYtH - 1) / kYtH);
+    const int ntiles = tiles_l + 2 * tiles_c;
+    const dim3 grid((unsigned)(8 * ((ntiles + 7) / 8)), (unsigned)((count + kYtWalk - 1) / kYtWalk));
+    hipLaunchKernelGGL(k_yadif_t, grid, dim3(kYtThreads), 4 * kYtSlot, s, p, tiles_l, tiles_c, txl, txc, count);
+    return hipGetLastError();
+}
+
 hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s)
 {
     const int ch = (p.h + 1) >> 1;

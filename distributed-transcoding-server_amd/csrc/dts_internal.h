@@ -422,6 +422,10 @@ struct YadifParams {
     int32_t aligned;                // every plane base / pitch of seq and dst is a multiple of 4
 };
 hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s);
+// the temporal walk (k_yadif_t): outputs of frames first .. first + count - 1 (x2 for the
+// field modes); every plane base / pitch of seq and dst 16-byte aligned (yadif_t_ok)
+bool yadif_t_ok(const YadifParams &p);
+hipError_t launch_yadif_t(const YadifParams &p, int count, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Synthetic source (testsrc2-like), identical on host and device

@@ -176,14 +176,21 @@ function fpsFrames(addon, n, srcFps, outFps) {
 // A segment's summed quality record from per-frame statistics (the addon's qstat
 // objects): {frames, sse: [y, u, v], ssimSum: [y, u, v]} -- the running sums vf_psnr /
 // vf_ssim keep (SSE exact; SSIM as the per-plane window sums), which add across segments.
+// The per-plane window sums come back as ssim x windows (exact to the f64 rounding of the
+// library's one division); a plane smaller than 8x8 has no SSIM window (vf_ssim scores none)
+// and adds 0 (ADVICE r03: its NaN / negative count poisoned the job's sums).
+function ssimWindows(pw, ph) {
+    return Math.max(0, (pw >> 2) - 1) * Math.max(0, (ph >> 2) - 1);
+}
+
 function rawQuality(stats, w, h) {
     const pw = [w, (w + 1) >> 1, (w + 1) >> 1], ph = [h, (h + 1) >> 1, (h + 1) >> 1];
-    const nw = [0, 1, 2].map(function (c) { return ((pw[c] >> 2) - 1) * ((ph[c] >> 2) - 1); });
+    const nw = [0, 1, 2].map(function (c) { return ssimWindows(pw[c], ph[c]); });
     const comp = ["y", "u", "v"], raw = { frames: stats.length, sse: [0, 0, 0], ssimSum: [0, 0, 0] };
     stats.forEach(function (q) {
         comp.forEach(function (c, i) {
             raw.sse[i] += q.sse[c];
-            raw.ssimSum[i] += q.ssim[c] * nw[i];
+            if (nw[i] > 0) raw.ssimSum[i] += q.ssim[c] * nw[i];
         });
     });
     return raw;
@@ -209,24 +216,27 @@ function summarizeRaw(raw, w, h) {
     const psnr = function (m) { return m === 0 ? "inf" : 10 * Math.log10(255 * 255 / m); };   // JSON has no Infinity
     const comp = ["y", "u", "v"], r = { frames: n, psnr: {}, ssim: {} };
     let mseAvg = 0, ssimAll = 0;
+    let noWindows = false;
     comp.forEach(function (c, i) {
         const mse = raw.sse[i] / (n * pw[i] * ph[i]);
-        const nw = ((pw[i] >> 2) - 1) * ((ph[i] >> 2) - 1);
+        const nw = ssimWindows(pw[i], ph[i]);
         r.psnr[c] = psnr(mse);
-        r.ssim[c] = raw.ssimSum[i] / (n * nw);
+        r.ssim[c] = nw > 0 ? raw.ssimSum[i] / (n * nw) : null;      // no 8x8 window: no SSIM (not NaN)
+        noWindows = noWindows || nw <= 0;
         mseAvg += mse * pw[i] * ph[i] / area;
-        ssimAll += r.ssim[c] * pw[i] * ph[i] / area;
+        if (nw > 0) ssimAll += r.ssim[c] * pw[i] * ph[i] / area;
     });
     r.psnr.avg = psnr(mseAvg);
-    r.ssim.all = ssimAll;
+    r.ssim.all = noWindows ? null : ssimAll;
     return r;
 }
 
 // the same from the addon's qstatStream() object
 function summaryOfStat(q, raw) {
     const f = function (x) { return x === Infinity ? "inf" : x; };
+    const g = function (x) { return typeof x === "number" && isFinite(x) ? x : null; };   // 0/0 windows -> null
     return { frames: raw.frames, psnr: { y: f(q.psnr.y), u: f(q.psnr.u), v: f(q.psnr.v), avg: f(q.psnrAvg) },
-             ssim: { y: q.ssim.y, u: q.ssim.u, v: q.ssim.v, all: q.ssimAll } };
+             ssim: { y: g(q.ssim.y), u: g(q.ssim.u), v: g(q.ssim.v), all: g(q.ssimAll) } };
 }
 
 // Segment summary of per-frame statistics, as vf_psnr / vf_ssim print at the end of

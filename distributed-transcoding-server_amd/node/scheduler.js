@@ -23,7 +23,13 @@
 //     outDir/job<id>/<chunkOffset>.y4m; once all of a job's chunks are done the
 //     segments are assembled into Jobs.assembledData = {size, chunk: [1 MiB block
 //     ids]} (assemble.js) and reported through `onJobUpdate(job, fields)`;
-//   * `result` carries per-phase timings (readMs, gpuMs, qualityMs, writeMs) and,
+//   * with an ffmpeg binary (opts.ffmpeg, $DTS_FFMPEG, ffmpeg-static or PATH; ffpipe.js), a
+//     source row may name a compressed file (`decode: "ffmpeg"`, or any path that is not
+//     .y4m): an ffmpeg child decodes it into a yuv4mpegpipe the worker reads in order; and
+//     with `encode` each rendition segment goes to an ffmpeg child encoding it with the Jobs
+//     row's codec / bitrate / codecSettings.encoderArgs (outDir/job<id>/<off>.mp4|webm|mkv),
+//     a finished job's segments stream-copied into one file before its blocks are cut;
+//   * `result` carries per-phase timings (readMs, gpuMs, qualityMs, writeMs; encodeMs) and,
 //     for rows whose codecSettings ask for it, the segment's PSNR / SSIM against
 //     the reference rendition (ladder.js qualityOf) with its summed record (`raw`);
 //     a job whose chunks are all done gets the whole stream's averages (Jobs row
@@ -40,6 +46,7 @@ const path = require("path");
 const ladder = require("./ladder");
 const y4m = require("./y4m");
 const assemble = require("./assemble");
+const ffpipe = require("./ffpipe");
 
 function planeShapes(w, h, fmt) {
     const cw = (w + 1) >> 1, ch = (h + 1) >> 1;
@@ -101,6 +108,23 @@ function y4mSource(readers) {
     return src;
 }
 
+// a regular file that starts with the YUV4MPEG2 signature, or anything that is not a regular
+// file (a pipe, a FIFO, "-": read as Y4M, never sniffed)
+function isY4MFile(p) {
+    if (p === "-") return true;
+    try {
+        if (!fs.statSync(p).isFile()) return true;
+        const fd = fs.openSync(p, "r"), b = Buffer.alloc(9);
+        try {
+            return fs.readSync(fd, b, 0, 9, 0) === 9 && b.toString("latin1") === "YUV4MPEG2";
+        } finally {
+            fs.closeSync(fd);
+        }
+    } catch (e) {
+        return true;                          // let the Y4M reader report it
+    }
+}
+
 class GpuSegmentScheduler extends EventEmitter {
     // opts: addon (dts_napi.node or a stand-in), gpus ([device...], default all),
     // workerId (WorkerAccounts id written to assignedTo), maxRetries (2),
@@ -119,6 +143,9 @@ class GpuSegmentScheduler extends EventEmitter {
         this._userSource = !!opts.source;
         this.sink = opts.sink || null;
         this.outDir = opts.outDir || null;
+        this.ffmpeg = ffpipe.ffmpegBinary(opts);              // null: Y4M files only
+        this.encode = !!opts.encode;
+        if (this.encode && !this.ffmpeg) throw new Error("encode needs an ffmpeg binary (DTS_FFMPEG / ffmpeg-static / PATH)");
         this.onUpdate = opts.onUpdate || function () {};
         this.onJobUpdate = opts.onJobUpdate || function () {};
         this.readers = {};
@@ -139,8 +166,8 @@ class GpuSegmentScheduler extends EventEmitter {
         return slot.graphs.get(plan.key);
     }
 
-    _segmentPath(jobId, off) {
-        return path.join(this.outDir, "job" + jobId, off + ".y4m");
+    _segmentPath(jobId, off, ext) {
+        return path.join(this.outDir, "job" + jobId, off + "." + (ext || "y4m"));
     }
 
     _update(row, fields) {
@@ -220,17 +247,32 @@ class GpuSegmentScheduler extends EventEmitter {
         }
         const t3 = Date.now();
         const files = outs.map(function () { return null; }), written = outs.map(function () { return 0; });
+        const encMs = outs.map(function () { return null; });
         if (this.sink) {
             await this.sink(plan, task.rows, o.per);
         } else if (this.outDir) {
+            const fps = plan.framerate ? ladder.rateOf(plan.framerate) : (plan.srcFps || [25, 1]);
+            const encs = [];
             task.rows.forEach(function (row, k) {
                 if (!row) return;
+                if (self.encode) {                 // an ffmpeg child per rendition segment, all at once
+                    const job = plan.jobs[k];
+                    const p = self._segmentPath(row.mainJob, row.chunkOffset, ffpipe.codecOf(job).ext);
+                    fs.mkdirSync(path.dirname(p), { recursive: true });
+                    encs.push(ffpipe.encodeSegment(self.ffmpeg, p, o.per[k], outs[k].w, outs[k].h, outs[k].fmt, fps, job,
+                                                   ladder.parseSettings(job.codecSettings)).then(function (r) {
+                        files[k] = r.file;
+                        written[k] = r.bytes;
+                        encMs[k] = r.encodeMs;
+                    }));
+                    return;
+                }
                 const p = self._segmentPath(row.mainJob, row.chunkOffset);
                 fs.mkdirSync(path.dirname(p), { recursive: true });
-                const fps = plan.framerate ? ladder.rateOf(plan.framerate) : (plan.srcFps || [25, 1]);
                 written[k] = y4m.writeSegment(p, o.per[k], outs[k].w, outs[k].h, outs[k].fmt, fps);
                 files[k] = p;
             });
+            await Promise.all(encs);
         }
         const t4 = Date.now();
         return task.rows.map(function (row, k) {
@@ -243,6 +285,10 @@ class GpuSegmentScheduler extends EventEmitter {
                         readMs: t1 - t0, gpuMs: t2 - t1, qualityMs: t3 - t2, writeMs: t4 - t3,
                         width: outs[k].w, height: outs[k].h, fmt: outs[k].fmt };
             if (quality[k]) r.quality = quality[k];
+            if (encMs[k] !== null) {
+                r.encodeMs = encMs[k];
+                r.codec = plan.jobs[k].codec;
+            }
             if (files[k]) {
                 r.file = files[k];
                 r.fileBytes = written[k];
@@ -298,8 +344,13 @@ class GpuSegmentScheduler extends EventEmitter {
                     fields.quality = JSON.stringify(q);
                 }
                 if (self.outDir && !self.sink) {
-                    const files = mine.map(function (c, i) { return recs[i].file || self._segmentPath(job.id, c.chunkOffset); });
-                    const a = assemble.assembleY4M(files, path.join(self.outDir, "blocks"));
+                    const ext = self.encode ? ffpipe.codecOf(job).ext : "y4m";
+                    const files = mine.map(function (c, i) { return recs[i].file || self._segmentPath(job.id, c.chunkOffset, ext); });
+                    const a = self.encode
+                        ? assemble.assembleFiles([ffpipe.concatSegments(self.ffmpeg, files,
+                                                                        path.join(self.outDir, "job" + job.id, "output." + ext))],
+                                                 path.join(self.outDir, "blocks"))
+                        : assemble.assembleY4M(files, path.join(self.outDir, "blocks"));
                     fields.assembledData = JSON.stringify(a);
                     fields.finished = true;
                 }
@@ -342,7 +393,12 @@ class GpuSegmentScheduler extends EventEmitter {
             Object.keys(sources).forEach(function (sid) {
                 const s = sources[sid];
                 if (!s.path || self.readers[sid]) return;
-                const r = new y4m.Y4MReader(s.path);
+                // a compressed source (decode: "ffmpeg", or a regular file that is not YUV4MPEG2):
+                // an ffmpeg child decodes it to a pipe; pipes / FIFOs / stdin are read as Y4M
+                const viaFfmpeg = s.decode === "ffmpeg" || (s.decode === undefined && !isY4MFile(s.path));
+                if (viaFfmpeg && !self.ffmpeg) throw new Error("source " + sid + ": " + s.path + " needs an ffmpeg binary to decode");
+                const r = viaFfmpeg ? new ffpipe.FfmpegDecoder(self.ffmpeg, s.path, { fmt: s.fmt })
+                                    : new y4m.Y4MReader(s.path);
                 self.readers[sid] = r;
                 s.w = s.w || r.hdr.w;
                 s.h = s.h || r.hdr.h;

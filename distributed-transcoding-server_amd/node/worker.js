@@ -3,7 +3,7 @@
 // renditions + updated JobChunks rows out (the drop-in for a CPU worker that
 // spawns ffmpeg-static per segment, index.js:9).
 //
-//   node worker.js <job.json> [--out DIR | --dump DIR]
+//   node worker.js <job.json> [--out DIR [--encode] | --dump DIR]
 //
 // job.json: {"workerId": 1, "segmentFrames": 600, "gpus": [0, ...] (optional),
 //            "sources": {"<sourceID>": {"path": "src.y4m"} or {"w": 3840, "h": 2160, "fmt": 0,
@@ -15,7 +15,10 @@
 // Jobs.assembledData (1 MiB blocks in DIR/blocks) and finished = true.
 // --dump DIR writes every output frame as DIR/<jobId>_<chunkOffset>_<frame>.raw
 // (packed planes) for offline checks.  Without a path the source is libdts's
-// synthetic one.  Compressed decode / encode (libavcodec) are not part of this build.
+// synthetic one.  Decode / encode stay in ffmpeg child processes (ffpipe.js): a source
+// path that is not .y4m is decoded by one, and --encode (or "encode": true) hands each
+// rendition segment to one with the Jobs row's codec and bitrate; the binary is
+// cfg.ffmpeg, $DTS_FFMPEG, ffmpeg-static or `ffmpeg` on PATH.
 const path = require("path");
 const fs = require("fs");
 
@@ -48,7 +51,8 @@ async function main(argv) {
         });
     } : null;
     const sched = new GpuSegmentScheduler({ addon: addon, gpus: cfg.gpus, workerId: cfg.workerId,
-                                            segmentFrames: cfg.segmentFrames, sink: sink, outDir: outDir });
+                                            segmentFrames: cfg.segmentFrames, sink: sink, outDir: outDir,
+                                            encode: argv.indexOf("--encode") >= 0 || !!cfg.encode, ffmpeg: cfg.ffmpeg });
     const summary = await sched.runJobs(cfg.jobs, cfg.chunks, cfg.sources);
     process.stdout.write(JSON.stringify({ chunks: cfg.chunks, jobs: cfg.jobs, summary: summary }) + "\n");
 }

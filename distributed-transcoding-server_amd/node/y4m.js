@@ -64,13 +64,89 @@ function parseHeader(line) {
     return h;
 }
 
-// one line (up to and without "\n") from fd at `pos` (null: the current position of a
-// stream); returns {line, bytes} or null at the end of the stream
+// A non-blocking descriptor (a child process's pipe, stdin after the parent set
+// O_NONBLOCK) answers EAGAIN while the producer has nothing yet: wait a millisecond and try
+// again (ADVICE r03), up to `EAGAIN_MS` in all, then fail clearly.
+const EAGAIN_MS = 600000;
+const SLEEP = new Int32Array(new SharedArrayBuffer(4));
+function retryAgain(fn) {
+    for (let waited = 0;; ++waited) {
+        try {
+            return fn();
+        } catch (e) {
+            if (e.code !== "EAGAIN" || waited >= EAGAIN_MS) throw e;
+            Atomics.wait(SLEEP, 0, 0, 1);
+        }
+    }
+}
+
+function readSync(fd, buf, off, len, pos) {
+    return retryAgain(function () { return fs.readSync(fd, buf, off, len, pos); });
+}
+
+// Buffered in-order reads of a stream (pipe / FIFO / stdin): header and FRAME lines are
+// parsed from 1 MiB reads instead of one read per byte (ADVICE r03); frame payloads copy
+// what is buffered and read the rest straight into the record.
+class StreamIn {
+    constructor(fd) {
+        this.fd = fd;
+        this.buf = Buffer.alloc(1 << 20);
+        this.start = 0;
+        this.end = 0;
+        this.eof = false;
+    }
+    _fill() {
+        if (this.eof) return 0;
+        if (this.start === this.end) {
+            this.start = this.end = 0;
+        } else if (this.end === this.buf.length) {
+            this.buf.copy(this.buf, 0, this.start, this.end);
+            this.end -= this.start;
+            this.start = 0;
+        }
+        const n = readSync(this.fd, this.buf, this.end, this.buf.length - this.end, null);
+        if (n <= 0) this.eof = true;
+        else this.end += n;
+        return Math.max(n, 0);
+    }
+    // {line, bytes} up to and without "\n", or null at the end of the stream
+    line(limit) {
+        for (;;) {
+            const nl = this.buf.indexOf(0x0a, this.start);
+            if (nl >= 0 && nl < this.end) {
+                const r = { line: this.buf.toString("latin1", this.start, nl), bytes: nl + 1 - this.start };
+                this.start = nl + 1;
+                return r;
+            }
+            if (this.end - this.start > limit) throw new Error("y4m: header line longer than " + limit + " bytes");
+            if (!this._fill()) {
+                if (this.start === this.end) return null;
+                throw new Error("y4m: stream ends inside a header line");
+            }
+        }
+    }
+    // fill dst; returns the bytes read (short at the end of the stream)
+    read(dst) {
+        const have = Math.min(this.end - this.start, dst.length);
+        this.buf.copy(dst, 0, this.start, this.start + have);
+        this.start += have;
+        let off = have;
+        while (off < dst.length && !this.eof) {
+            const n = readSync(this.fd, dst, off, dst.length - off, null);
+            if (n <= 0) this.eof = true;
+            else off += n;
+        }
+        return off;
+    }
+}
+
+// one line (up to and without "\n") of a regular file at `pos`; returns {line, bytes} or
+// null at the end of the file
 function readLine(fd, pos, limit) {
     const one = Buffer.alloc(1), out = [];
     let n = 0;
     for (;;) {
-        const got = fs.readSync(fd, one, 0, 1, pos === null ? null : pos + n);
+        const got = readSync(fd, one, 0, 1, pos + n);
         if (got <= 0) {
             if (n === 0) return null;
             throw new Error("y4m: stream ends inside a header line");
@@ -87,7 +163,7 @@ function readLine(fd, pos, limit) {
 function readFull(fd, buf, pos) {
     let off = 0;
     while (off < buf.length) {
-        const n = fs.readSync(fd, buf, off, buf.length - off, pos === null ? null : pos + off);
+        const n = readSync(fd, buf, off, buf.length - off, pos === null ? null : pos + off);
         if (n <= 0) break;
         off += n;
     }
@@ -121,7 +197,8 @@ class Y4MReader {
         this.ownFd = typeof src === "string" && src !== "-";
         const st = fs.fstatSync(this.fd);
         this.seekable = st.isFile();
-        const hl = readLine(this.fd, this.seekable ? 0 : null, MAX_HEADER);
+        if (!this.seekable) this.sin = new StreamIn(this.fd);
+        const hl = this.seekable ? readLine(this.fd, 0, MAX_HEADER) : this.sin.line(MAX_HEADER);
         if (!hl) throw new Error("y4m: empty stream");
         this.hdr = parseHeader(hl.line);
         this.hdr.headerBytes = hl.bytes;
@@ -157,14 +234,14 @@ class Y4MReader {
         if (this.kept.has(i)) return this.kept.get(i);
         if (i < this.next) throw new Error("y4m: frame " + i + " of a stream was already released");
         while (this.next <= i) {
-            const tl = readLine(this.fd, null, MAX_HEADER);
+            const tl = this.sin.line(MAX_HEADER);
             if (!tl) {
                 this.frames = this.next;
                 return null;
             }
             if (tl.line.slice(0, 5) !== "FRAME") throw new Error("y4m: record " + this.next + " is not a FRAME");
             const rec = Buffer.alloc(this.frameBytes);
-            if (readFull(this.fd, rec, null) !== rec.length) throw new Error("y4m: frame " + this.next + " is truncated");
+            if (this.sin.read(rec) !== rec.length) throw new Error("y4m: frame " + this.next + " is truncated");
             this.kept.set(this.next++, recordToFrame(rec, this.hdr.w, this.hdr.h, this.hdr.bits));
         }
         return this.kept.get(i);
@@ -248,7 +325,11 @@ class Y4MWriter {
 
     _put(buf) {
         let off = 0;
-        while (off < buf.length) off += fs.writeSync(this.fd, buf, off, buf.length - off);
+        const fd = this.fd;
+        while (off < buf.length) {
+            const o = off;
+            off += retryAgain(function () { return fs.writeSync(fd, buf, o, buf.length - o); });
+        }
         this.bytes += buf.length;
     }
 

@@ -384,20 +384,21 @@ function testY4M10BitAndHeaders() {
     fs.writeFileSync(q, Buffer.concat([Buffer.from("YUV4MPEG2 W6 H4 F30:1 C420jpeg " + tags + "\n"),
                                        Buffer.from("FRAME Ixyz\n"), rec, Buffer.from("FRAME\n"), rec]));
     assert.ok(y4m.headerBytes(q) > 512);
-    const fd = fs.openSync(q, "r");
-    const st = new y4m.Y4MReader(fd);
-    st.seekable = false;                     // (a regular file read as a stream: past its header)
-    fs.readSync(fd, Buffer.alloc(st.hdr.headerBytes), 0, st.hdr.headerBytes, null);
-    st.frames = Infinity;
-    st.next = 0;
-    st.kept = new Map();
+    // the same file through a FIFO (a real stream: buffered in-order reads, FRAME parameters)
+    const fifo = path.join(d, "long.fifo");
+    require("child_process").execFileSync("mkfifo", [fifo]);
+    const feeder = require("child_process").spawn("sh", ["-c", "cat \"$0\" > \"$1\"", q, fifo]);
+    const st = new y4m.Y4MReader(fifo);
+    assert.strictEqual(st.seekable, false);
+    assert.strictEqual(st.hdr.headerBytes, y4m.headerBytes(q));
     assert.strictEqual(st.read(1).data[0][0], 9);
     assert.strictEqual(st.read(0).data[2][0], 9);                 // kept until released
     st.release(2);
     assert.throws(function () { st.read(0); }, /released/);
     assert.strictEqual(st.read(2), null);
     assert.strictEqual(st.frames, 2);
-    fs.closeSync(fd);
+    st.close();
+    return new Promise(function (res) { feeder.on("exit", res); if (feeder.exitCode !== null) res(); });
 }
 
 async function testPipeSourceAndPartialJob() {
@@ -451,7 +452,7 @@ function testNoDevicesIsLoud() {
     testQualitySummary();
     await testY4MJobAssembled();
     await testDeinterlaceWithRateChange();
-    testY4M10BitAndHeaders();
+    await testY4M10BitAndHeaders();
     await testPipeSourceAndPartialJob();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });

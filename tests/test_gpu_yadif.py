@@ -120,3 +120,54 @@ def test_graph_yadif_then_ladder(ctx, mode, tff):
         Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_YUV420P, outs, deint=(1, 1)))
     with pytest.raises(Dm.DtsError):
         Dm.Graph(ctx, Dm.make_spec(sw, sh, Dm.FMT_NV12, outs, deint=(0, 1)))
+
+
+def _aligned_seq(frames, w, h, n_extra_out=0):
+    """frames laid out by bench.dev_batch (pitches of 256 B, planes 16-byte aligned): the
+    temporal-walk kernel's domain (k_yadif_t)"""
+    import torch
+    from bench import dev_batch, frame_bytes
+    fb = frame_bytes(w, h, D.FMT_YUV420P)
+    t = torch.zeros((len(frames), fb), dtype=torch.uint8, device="cuda")
+    d, _ = dev_batch(t, w, h, D.FMT_YUV420P)
+    host = np.zeros((len(frames), fb), np.uint8)
+    for i, f in enumerate(frames):
+        for p in range(3):
+            off = d.data[p] - t.data_ptr()
+            rows, cols = f[p].shape
+            host[i, off:off + rows * d.pitch[p]].reshape(rows, d.pitch[p])[:, :cols] = f[p]
+    t.copy_(torch.from_numpy(host))
+    return t, d
+
+
+@pytest.mark.parametrize("w,h,n,first,count", [(720, 480, 5, 0, 5), (130, 74, 4, 0, 4), (1000, 36, 3, 0, 3),
+                                               (1920, 1080, 20, 1, 18), (3840, 2160, 3, 0, 3), (16, 6, 3, 0, 3)])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("tff", [1, 0])
+def test_yadif_temporal_walk_vs_oracle(ctx, w, h, n, first, count, mode, tff):
+    """k_yadif_t (16-byte aligned sequences: every frame tile staged once, a ring of prev /
+    cur / next in LDS): bit-exact vs the oracle in every mode and field order; tiles at every
+    plane edge, widths not multiples of 16, walks longer than one workgroup's (16 frames) and
+    starting inside the sequence (first > 0: the graph path's context frame)."""
+    import torch
+    from bench import dev_batch, frame_bytes, unpack_dev_frame
+    if w >= 1920 and (mode, tff) not in [(0, 1), (1, 0), (2, 0)]:
+        pytest.skip("large frames: a subset of modes")
+    rng = np.random.default_rng(w + h + 31 * mode + tff)
+    frames = [random_frame(w, h, D.FMT_YUV420P, rng) if i % 3 == 0 else D.synth_host(w, h, D.FMT_YUV420P, 0, 13, i)
+              for i in range(n)]
+    seq_t, seq = _aligned_seq(frames, w, h)
+    fields = 2 if mode & 1 else 1
+    out_t = torch.zeros((count * fields, frame_bytes(w, h, D.FMT_YUV420P)), dtype=torch.uint8, device="cuda")
+    od, _ = dev_batch(out_t, w, h, D.FMT_YUV420P)
+    ctx.yadif_device(w, h, mode, tff, seq, n, first, count, od, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = out_t.cpu().numpy()
+    for j in range(count):
+        i = first + j
+        for s in range(fields):
+            want = orc.yadif_frame(frames[max(i - 1, 0)], frames[i], frames[min(i + 1, n - 1)], w, h, mode, tff, s)
+            got = unpack_dev_frame(out[j * fields + s], w, h, D.FMT_YUV420P)
+            for p in range(3):
+                assert np.array_equal(got[p], want[p]), \
+                    f"frame {i} field {s} plane {p}: {int((got[p] != want[p]).sum())} diffs"

@@ -295,3 +295,141 @@ def test_worker_gpu_two_slots_one_device_with_a_failure(tmp_path):
     mse_avg = sum(m_ * a for m_, a in zip(mse, area)) / sum(area)
     assert q["frames"] == 24 and q["psnr"]["avg"] == pytest.approx(10 * np.log10(255 * 255 / mse_avg), rel=1e-9)
     assert q["ssim"]["all"] == pytest.approx(sum(x["ssim_all"] for x in recs) / len(recs), abs=1e-4)
+
+
+def test_ffpipe_cpu():
+    """node/ffpipe.js (decode / encode / concat ffmpeg children over yuv4mpegpipe) with the
+    stub binary tests/node/ffmpeg_stub.js: frames in order from the decoder's pipe, the Jobs
+    row's codec / bitrate / encoderArgs on the encoder's command line, its input the exact Y4M
+    records, a dead encoder an error (not a hang)."""
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "test_ffpipe.js")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().endswith("ok")
+
+
+def _write_y4m_p010(path, frames, w, h, fps=(60, 1)):
+    """p010 host frames (Y << 6, U / V interleaved) as a C420p10 stream (planar 10-bit LE)"""
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    with open(path, "wb") as f:
+        f.write(f"YUV4MPEG2 W{w} H{h} F{fps[0]}:{fps[1]} Ip A1:1 C420p10 XYSCSS=420P10\n".encode())
+        for p in frames:
+            y = np.ascontiguousarray(p[0]).view(np.uint16) >> 6
+            uv = np.ascontiguousarray(p[1]).view(np.uint16).reshape(ch, 2 * cw) >> 6
+            f.write(b"FRAME\n")
+            for plane in (y, uv[:, 0::2], uv[:, 1::2]):
+                f.write(np.ascontiguousarray(plane).astype("<u2").tobytes())
+
+
+@pytest.mark.gpu
+def test_worker_gpu_hdr10_fifo(tmp_path):
+    """An HDR10 job through the Node worker on the GPU: a C420p10 (p010) source streamed
+    through a FIFO, codecSettings {"tonemap": "hable"} -> the ladder's bit-exact p010 scale +
+    k_tonemap, 8-bit segments written as Y4M; every sample within +-1 LSB of
+    orc.hdr_to_sdr and at most 1 % off by one (database.js:73-79: the job row's fields drive
+    the graph)."""
+    import threading
+    sw, sh, n, seg, w, h = 256, 144, 5, 3, 128, 72
+    frames = [D.synth_host(sw, sh, D.FMT_P010LE, 0, 0x5EED, i) for i in range(n)]
+    src = tmp_path / "hdr.y4m"
+    _write_y4m_p010(src, frames, sw, sh)
+    fifo = tmp_path / "hdr.fifo"
+    os.mkfifo(fifo)
+
+    def feed():
+        with open(fifo, "wb") as f:
+            f.write(src.read_bytes())
+    th = threading.Thread(target=feed, daemon=True)
+    th.start()
+    jobs = [{"id": 91, "sourceID": 3, "width": w, "height": h, "framerate": 60, "chunks": 2,
+             "codecSettings": json.dumps({"tonemap": "hable", "format": "yuv420p"})}]
+    chunks = [{"id": 100 + o, "mainJob": 91, "chunkOffset": o, "status": None} for o in range(2)]
+    cfg = {"workerId": 2, "segmentFrames": seg, "gpus": [0], "sources": {"3": {"path": str(fifo)}},
+           "jobs": jobs, "chunks": chunks}
+    (tmp_path / "job.json").write_text(json.dumps(cfg))
+    r = subprocess.run([NODE, os.path.join(ROOT, "distributed-transcoding-server_amd", "node", "worker.js"),
+                        str(tmp_path / "job.json"), "--out", str(tmp_path / "out")], capture_output=True, text=True,
+                       timeout=120)
+    th.join(timeout=10)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    nframes = 0
+    for c in res["chunks"]:
+        assert c["status"] == "done", c
+        rec = json.loads(c["result"])
+        assert rec["gpuMs"] >= 0 and rec["readMs"] >= 0 and rec["writeMs"] >= 0
+        gw, gh, got = _read_y4m(rec["file"])
+        idx = list(range(c["chunkOffset"] * seg, min(n, (c["chunkOffset"] + 1) * seg)))
+        assert (gw, gh, len(got)) == (w, h, len(idx))
+        for i, g in zip(idx, got):
+            mid = orc.scale_frame(frames[i], sw, sh, D.FMT_P010LE, w, h, D.FMT_P010LE, D.SCALE_BICUBIC)
+            want = orc.hdr_to_sdr(mid, w, h, D.FMT_YUV420P, D.TM_HABLE, float("nan"), 2.0, 0.0, 100.0)
+            bad = tot = 0
+            for a, b in zip(g, want):
+                d = np.abs(a.astype(np.int16) - np.asarray(b).astype(np.int16))
+                assert d.max() <= 1, (i, int(d.max()))
+                bad += int((d > 0).sum())
+                tot += d.size
+            assert bad <= 0.01 * tot, (i, bad, tot)
+            nframes += 1
+    assert nframes == n
+    assert json.loads(res["jobs"][0]["assembledData"])["size"] > 0
+
+
+@pytest.mark.gpu
+def test_worker_gpu_ffmpeg_decode_encode(tmp_path):
+    """The ffmpeg process boundary (index.js:9) on both sides of the GPU path, with the stub
+    binary: the source decoded by an ffmpeg child (decode: "ffmpeg"), each rendition segment
+    encoded by one with the Jobs row's codec / bitrate (database.js:76-78; h264 -> .mp4,
+    vp9 -> .webm as index.js:108-118), decode (readMs) and encode (encodeMs) timed apart from
+    gpuMs, the job's segments concatenated by ffmpeg and cut into Jobs.assembledData blocks.
+    The stub's "encoded" segments carry the Y4M records it was fed: bit-exact vs the oracle."""
+    sw, sh, n, seg = 320, 180, 6, 3
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 21, i) for i in range(n)]
+    src = tmp_path / "src.mkv"
+    _write_y4m(src, frames, sw, sh)
+    stub = os.path.join(ROOT, "tests", "node", "ffmpeg_stub.js")
+    jobs = [{"id": 41, "sourceID": 8, "width": 160, "height": 90, "framerate": 60, "chunks": 2, "codec": "h264",
+             "bitrate": 1500000, "codecSettings": json.dumps({"encoderArgs": ["-preset", "veryfast"]})},
+            {"id": 42, "sourceID": 8, "width": 96, "height": 54, "framerate": 60, "chunks": 2, "codec": "vp9",
+             "bitrate": 800000, "codecSettings": json.dumps({"format": "yuv420p", "scale": "lanczos"})}]
+    chunks = [{"id": 200 + 2 * k + o, "mainJob": j["id"], "chunkOffset": o, "status": None}
+              for k, j in enumerate(jobs) for o in range(2)]
+    cfg = {"workerId": 5, "segmentFrames": seg, "gpus": [0], "ffmpeg": stub, "encode": True,
+           "sources": {"8": {"path": str(src), "decode": "ffmpeg"}}, "jobs": jobs, "chunks": chunks}
+    (tmp_path / "job.json").write_text(json.dumps(cfg))
+    env = dict(os.environ, STUB_LOG=str(tmp_path / "argv.log"))
+    r = subprocess.run([NODE, os.path.join(ROOT, "distributed-transcoding-server_amd", "node", "worker.js"),
+                        str(tmp_path / "job.json"), "--out", str(tmp_path / "out")], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout)
+    spec = {41: (160, 90, D.FMT_NV12, D.SCALE_BICUBIC, "libx264", "1500000", ".mp4"),
+            42: (96, 54, D.FMT_YUV420P, D.SCALE_LANCZOS, "libvpx-vp9", "800000", ".webm")}
+    for c in res["chunks"]:
+        assert c["status"] == "done", c
+        rec = json.loads(c["result"])
+        w, h, fmt, m, enc, br, ext = spec[c["mainJob"]]
+        assert rec["file"].endswith(ext) and rec["codec"] in ("h264", "vp9")
+        assert rec["encodeMs"] >= 0 and rec["gpuMs"] >= 0 and rec["readMs"] >= 0
+        body = open(rec["file"], "rb").read()
+        nl = body.index(b"\n")
+        args = json.loads(body[8:nl])
+        assert args[args.index("-c:v") + 1] == enc and args[args.index("-b:v") + 1] == br
+        (tmp_path / "seg.y4m").write_bytes(body[nl + 1:])
+        gw, gh, got = _read_y4m(tmp_path / "seg.y4m")
+        idx = list(range(c["chunkOffset"] * seg, (c["chunkOffset"] + 1) * seg))
+        assert (gw, gh, len(got)) == (w, h, len(idx))
+        for i, g in zip(idx, got):
+            assert planes_equal(g, _planar(orc.scale_frame(frames[i], sw, sh, D.FMT_YUV420P, w, h, fmt, m), fmt)), i
+    for j in res["jobs"]:
+        assert j["finished"] is True
+        a = json.loads(j["assembledData"])
+        segs = [json.loads(c["result"])["file"] for c in sorted(res["chunks"], key=lambda c: c["chunkOffset"])
+                if c["mainJob"] == j["id"]]
+        whole = b"".join(open(f, "rb").read() for f in segs)
+        assert a["size"] == len(whole)
+        assert b"".join((tmp_path / "out" / "blocks" / cid).read_bytes() for cid in a["chunk"]) == whole
+    log = [json.loads(x) for x in (tmp_path / "argv.log").read_text().splitlines()]
+    assert any("-i" in a and str(src) in a for a in log)           # the decoder child
+    assert sum(1 for a in log if "concat" in a) == 2               # one concat per job
