@@ -11,9 +11,12 @@
 //   encode:  Y4MWriter -> ffmpeg -f yuv4mpegpipe -i - -c:v CODEC -b:v BITRATE ... SEGMENT
 //   concat:  ffmpeg -f concat -safe 0 -i LIST -c copy OUTPUT  (a job's encoded segments)
 //
-// Both pipes are the children's stdio; the worker reads / writes them synchronously (y4m.js
-// retries the pipe's EAGAIN), so decode time lands in JobChunks.result.readMs and encode
-// time in writeMs / encodeMs, apart from gpuMs.  The binary: opts.ffmpeg, $DTS_FFMPEG,
+// Both pipes are the children's stdio, made from a FIFO whose two ends are opened here (a
+// Node stream on a child's stdio would read ahead into its own buffer whenever the event loop
+// runs and take bytes from under the synchronous reader): the child's end in blocking mode,
+// the worker's end non-blocking, read / written synchronously (y4m.js retries EAGAIN; a
+// dead encoder is EPIPE, a finished decoder EOF).  Decode time lands in
+// JobChunks.result.readMs and encode time in writeMs / encodeMs, apart from gpuMs.  The binary: opts.ffmpeg, $DTS_FFMPEG,
 // ffmpeg-static if installed, else `ffmpeg` on PATH; none -> null (the worker then reads and
 // writes Y4M files only).  libavcodec is not in this image: tests run a stub executable that
 // speaks yuv4mpegpipe.
@@ -22,6 +25,7 @@
 
 const cp = require("child_process");
 const fs = require("fs");
+const os = require("os");
 const path = require("path");
 const y4m = require("./y4m");
 
@@ -66,10 +70,28 @@ function encodeArgs(job, settings) {
     return a;
 }
 
-function pipeFd(stream) {
-    const fd = stream && stream._handle && stream._handle.fd;
-    if (typeof fd !== "number" || fd < 0) throw new Error("ffpipe: the child's pipe has no file descriptor");
-    return fd;
+// A pipe as {mine, theirs}: `theirs` (blocking) for the child's stdin (toChild) or stdout,
+// `mine` (non-blocking) for this process.  Made from a FIFO opened from both sides, then
+// unlinked; the child's end is closed here once the child has it.
+let fifoSeq = 0;
+function pipePair(toChild) {
+    const p = path.join(os.tmpdir(), "dts-ff-" + process.pid + "-" + (fifoSeq++) + ".fifo");
+    cp.execFileSync("mkfifo", ["-m", "600", p]);
+    const C = fs.constants;
+    try {
+        if (toChild) {                         // we write, the child reads
+            const tmp = fs.openSync(p, C.O_RDONLY | C.O_NONBLOCK);      // a reader, so the next open does not block
+            const mine = fs.openSync(p, C.O_WRONLY | C.O_NONBLOCK);
+            const theirs = fs.openSync(p, C.O_RDONLY);                  // a writer exists: no block
+            fs.closeSync(tmp);
+            return { mine: mine, theirs: theirs };
+        }
+        const mine = fs.openSync(p, C.O_RDONLY | C.O_NONBLOCK);         // we read, the child writes
+        const theirs = fs.openSync(p, C.O_WRONLY);                      // a reader exists: no block
+        return { mine: mine, theirs: theirs };
+    } finally {
+        fs.unlinkSync(p);
+    }
 }
 
 function collect(child) {
@@ -87,7 +109,13 @@ class FfmpegDecoder {
         const pf = opts.fmt === y4m.FMT_P010LE ? "yuv420p10le" : "yuv420p";
         this.args = ["-v", "error", "-nostdin", "-i", input, "-f", "yuv4mpegpipe", "-pix_fmt", pf, "-strict", "-1", "-"];
         this.t0 = Date.now();
-        this.child = cp.spawn(bin, this.args, { stdio: ["ignore", "pipe", "pipe"] });
+        const pp = pipePair(false);
+        try {
+            this.child = cp.spawn(bin, this.args, { stdio: ["ignore", pp.theirs, "pipe"] });
+        } finally {
+            fs.closeSync(pp.theirs);
+        }
+        this.fd = pp.mine;
         this.stderr = collect(this.child);
         const self = this;
         this.exited = new Promise(function (resolve) {
@@ -95,9 +123,10 @@ class FfmpegDecoder {
             self.child.on("error", function (e) { resolve({ code: -1, error: e }); });
         });
         try {
-            this.reader = new y4m.Y4MReader(pipeFd(this.child.stdout));
+            this.reader = new y4m.Y4MReader(this.fd);
         } catch (e) {
             this.kill();
+            fs.closeSync(this.fd);
             throw new Error("ffmpeg decode of " + input + ": " + e.message);
         }
         this.hdr = this.reader.hdr;
@@ -110,6 +139,8 @@ class FfmpegDecoder {
     }
     close() {
         this.reader.close();
+        if (this.fd !== null) fs.closeSync(this.fd);
+        this.fd = null;
         if (this.child.exitCode === null) this.kill();
     }
 }
@@ -123,7 +154,13 @@ class FfmpegEncoder {
         this.args = ["-v", "error", "-nostdin", "-f", "yuv4mpegpipe", "-i", "-"].concat(encodeArgs(job || {}, settings),
                                                                                        ["-y", out]);
         this.t0 = Date.now();
-        this.child = cp.spawn(bin, this.args, { stdio: ["pipe", "ignore", "pipe"] });
+        const pp = pipePair(true);
+        try {
+            this.child = cp.spawn(bin, this.args, { stdio: [pp.theirs, "ignore", "pipe"] });
+        } finally {
+            fs.closeSync(pp.theirs);
+        }
+        this.fd = pp.mine;
         this.stderr = collect(this.child);
         const self = this;
         this.exited = new Promise(function (resolve) {
@@ -131,17 +168,21 @@ class FfmpegEncoder {
             self.child.on("error", function (e) { resolve({ code: -1, error: e }); });
         });
         try {
-            this.writer = new y4m.Y4MWriter(pipeFd(this.child.stdin), w, h, fps, fmt);
+            this.writer = new y4m.Y4MWriter(this.fd, w, h, fps, fmt);
         } catch (e) {
             e.encoder = this;
             throw e;
         }
     }
     write(frame) { this.writer.write(frame); }
+    _closeFd() {
+        if (this.fd !== null) fs.closeSync(this.fd);
+        this.fd = null;
+    }
     close() {
         const self = this;
         this.writer.close();
-        this.child.stdin.destroy();                       // EOF: the encoder flushes and exits
+        this._closeFd();                                  // EOF: the encoder flushes and exits
         return this.exited.then(function (st) {
             if (st.code !== 0)
                 throw new Error("ffmpeg encode of " + self.out + " failed (" + (st.error || st.signal || st.code) + "): " +
@@ -161,6 +202,7 @@ function encodeSegment(bin, out, frames, w, h, fmt, fps, job, settings) {
         enc = enc || e.encoder || null;
         if (!enc) return Promise.reject(new Error("ffmpeg encode of " + out + ": " + e.message));
         enc.child.kill("SIGKILL");
+        enc._closeFd();
         return enc.exited.then(function () {
             throw new Error("ffmpeg encode of " + out + ": " + e.message + " " + enc.stderr());
         });

@@ -435,6 +435,38 @@ async function testPipeSourceAndPartialJob() {
     assert.deepStrictEqual(Object.keys(s.readers), []);          // readers closed
 }
 
+async function testFfmpegBoundary() {
+    // decode and encode through ffmpeg children (tests/node/ffmpeg_stub.js as the binary):
+    // frames bigger than a pipe's buffer, several segments (the decoder's pipe read across
+    // awaits), every rendition segment encoded with its row's codec, the job concatenated
+    const d = tmpdir(), src = path.join(d, "src.mkv"), W = 320, H = 180, N = 7;
+    y4m.writeFile(src, W, H, [60, 1], N, function (i) {
+        return { data: [Buffer.alloc(W * H, i), Buffer.alloc(W * H / 4, 90), Buffer.alloc(W * H / 4, 160)],
+                 pitch: [W, W / 2, W / 2] };
+    });
+    const jobs = [{ id: 41, sourceID: 8, width: 320, height: 180, framerate: 60, chunks: 3, codec: "h264", bitrate: 1500000 },
+                  { id: 42, sourceID: 8, width: 96, height: 54, framerate: 60, chunks: 3, codec: "vp9" }];
+    const chunks = [];
+    jobs.forEach(function (j, k) { [0, 1, 2].forEach(function (o) { chunks.push({ id: 300 + 3 * k + o, mainJob: j.id, chunkOffset: o, status: null }); }); });
+    const s = new GpuSegmentScheduler({ addon: fakeAddon({ devices: 1 }), segmentFrames: 3, outDir: path.join(d, "out"),
+                                        encode: true, ffmpeg: path.join(__dirname, "ffmpeg_stub.js") });
+    await s.runJobs(jobs, chunks, { 8: { path: src, decode: "ffmpeg" } });
+    chunks.forEach(function (c) {
+        assert.strictEqual(c.status, "done", c.result);
+        const r = JSON.parse(c.result);
+        assert.ok(r.encodeMs >= 0 && r.file.endsWith(c.mainJob === 41 ? ".mp4" : ".webm"));
+        const body = fs.readFileSync(r.file), nl = body.indexOf(0x0a);
+        const seg = path.join(d, "seg.y4m");
+        fs.writeFileSync(seg, body.slice(nl + 1));
+        const rd = new y4m.Y4MReader(seg);
+        const got = Array.from({ length: rd.frames }, function (_, i) { return rd.read(i).data[0][0]; });
+        rd.close();
+        const base = 3 * c.chunkOffset;
+        assert.deepStrictEqual(got, [base, base + 1, base + 2].filter(function (i) { return i < N; }), "chunk " + c.chunkOffset);
+    });
+    jobs.forEach(function (j) { assert.strictEqual(j.finished, true); });
+}
+
 function testNoDevicesIsLoud() {
     assert.throws(function () { new GpuSegmentScheduler({ addon: fakeAddon({ devices: 0 }) }); }, /no CPU fallback/);
 }
@@ -454,5 +486,6 @@ function testNoDevicesIsLoud() {
     await testDeinterlaceWithRateChange();
     await testY4M10BitAndHeaders();
     await testPipeSourceAndPartialJob();
+    await testFfmpegBoundary();
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });
