@@ -390,7 +390,9 @@ __device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t
         const int td2 = (absd(byte_at(nm, k), c) + absd(byte_at(np, k), e)) >> 1;
         int diff = max(max(td0 >> 1, td1), td2);
         int pred = (c + e) >> 1;
-        if ((ne >> k) & 1u) {
+        if ((ne >> k) & 1u) {               // (a branch per pixel, uniform in interior tiles: computed
+                                            // unconditionally the sixteen pixels' window sums share
+                                            // values across pixels and need 241 VGPRs)
             // CHECK(j): the 3-byte windows cm[x + j - 1 ..] vs cp[x - j - 1 ..]
             int score = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 1), win3(cp, X - 1), 0u) - 1;
             const int sm1 = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 2), win3(cp, X), 0u);

@@ -1,0 +1,4 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+bash tools/r04_yadif.sh r04a || exit $?
+bash tools/r04_hdr_ab.sh
