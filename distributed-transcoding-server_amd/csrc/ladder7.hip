@@ -50,6 +50,8 @@
 //    granule publishes them to the other waves of the rendition;
 //  * waves beyond the group's units (the workgroup has the widest group's size)
 //    only stage pieces and keep the barrier count.
+#include <type_traits>
+
 #include "dts_internal.h"
 #include "ladder_mfma.h"
 
@@ -713,13 +715,46 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     // first, then the DMA of granule q + NS7 - 1, then (DTS_L7_DEFER) the row blocks that
     // fired at q - 1 -- the ring still holds granules q - R .. q - 1 -- while the A reads
     // land, then H(q) into ring slot q % R.
-    static_assert(8 % R == 0, "ring periods divide the unroll");
+    // UNR: the walk's unroll -- the ring length R (4 granules for the one-V-K-block walks, 8 for
+    // two), or 8 for every walk (DTS_L7_UNROLL8, the round-3 shape: twice the code of the
+    // one-K-block walks, whose copies compete for the CU pair's instruction cache)
+#ifndef DTS_L7_UNROLL8
+#define DTS_L7_UNROLL8 1
+#endif
+    // DTS_L7_ROLLED: one staging batch per loop copy (UNR = PB7) and the ring slot chosen at run
+    // time by a switch -- a quarter / an eighth of the code (A/B)
+#ifndef DTS_L7_ROLLED
+#define DTS_L7_ROLLED 0
+#endif
+    constexpr bool ROLL = DTS_L7_ROLLED;
+    constexpr int UNR = ROLL ? PB7 : (DTS_L7_UNROLL8 ? 8 : (R > 2 * PB7 ? R : 2 * PB7));
+    static_assert(ROLL || (UNR % R == 0 && UNR % PB7 == 0), "ring and batch periods divide the unroll");
+    // the H result of tile t (hi / lo dwords) into ring slot K
+    auto ring_put = [&](auto K, int t, uint32_t hv, uint32_t lv) {
+        constexpr int k = decltype(K)::value;
+        if constexpr (k < R) {
+            rh[k / 4][t][k % 4] = (int)hv;
+            rl[k / 4][t][k % 4] = (int)lv;
+        }
+    };
+    auto ring_put_rt = [&](int rsr, int t, uint32_t hv, uint32_t lv) {
+        switch (rsr) {      // (the empty asm keeps each case a branch, not a select over every slot)
+        case 0: asm volatile(""); ring_put(std::integral_constant<int, 0>{}, t, hv, lv); break;
+        case 1: asm volatile(""); ring_put(std::integral_constant<int, 1>{}, t, hv, lv); break;
+        case 2: asm volatile(""); ring_put(std::integral_constant<int, 2>{}, t, hv, lv); break;
+        case 3: asm volatile(""); ring_put(std::integral_constant<int, 3>{}, t, hv, lv); break;
+        case 4: asm volatile(""); ring_put(std::integral_constant<int, 4>{}, t, hv, lv); break;
+        case 5: asm volatile(""); ring_put(std::integral_constant<int, 5>{}, t, hv, lv); break;
+        case 6: asm volatile(""); ring_put(std::integral_constant<int, 6>{}, t, hv, lv); break;
+        default: asm volatile(""); ring_put(std::integral_constant<int, 7>{}, t, hv, lv); break;
+        }
+    };
     const int ngran = G.ngran;
     int sq = 0;
     L7_STAMP_INIT;
-    for (int q0 = 0; q0 < ngran; q0 += 8) {
+    for (int q0 = 0; q0 < ngran; q0 += UNR) {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+        for (int s = 0; s < UNR; ++s) {
             const int q = q0 + s;
             if (q >= ngran) break;
             if (s % PB7 == 0) {
@@ -861,21 +896,28 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                 }
                 const int rs = s % R;
+#define WRING(t_, hv_, lv_)                                                                   \
+    do {                                                                                      \
+        if constexpr (ROLL) {                                                                 \
+            ring_put_rt(q % R, (t_), (hv_), (lv_));                                           \
+        } else {                                                                              \
+            rh[rs / 4][(t_)][rs % 4] = (int)(hv_);                                            \
+            rl[rs / 4][(t_)][rs % 4] = (int)(lv_);                                            \
+        }                                                                                     \
+    } while (0)
                 if ((HS == 128 || P10) && !RC) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
                         const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(ah[t].x, ah[t].y));
                         const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(ah[t].z, ah[t].w));
-                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                        WRING(t, __builtin_amdgcn_perm(p1, p0, 0x07050301u), __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                     }
                 } else if (!RC) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) {
                         const uint32_t p0 = pack_h6(ah[t].x, al[t].x, ah[t].y, al[t].y);   // rows 4g, 4g+1
                         const uint32_t p1 = pack_h6(ah[t].z, al[t].z, ah[t].w, al[t].w);   // rows 4g+2, 4g+3
-                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                        WRING(t, __builtin_amdgcn_perm(p1, p0, 0x07050301u), __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                     }
                 } else {
                     // range conversion of the 15-bit H output (swscale.c lum/chrRange{To,From}Jpeg_c:
@@ -890,11 +932,11 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                         }
                         const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)y[1], (uint32_t)y[0], 0x05040100u);
                         const uint32_t p1 = __builtin_amdgcn_perm((uint32_t)y[3], (uint32_t)y[2], 0x05040100u);
-                        rh[rs / 4][t][rs % 4] = (int)__builtin_amdgcn_perm(p1, p0, 0x07050301u);
-                        rl[rs / 4][t][rs % 4] = (int)(__builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
+                        WRING(t, __builtin_amdgcn_perm(p1, p0, 0x07050301u), __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ 0x80808080u);
                     }
                 }
             }
+#undef WRING
             L7_STAMP(3);
             if (!DTS_L7_DEFER) vfire(q);
             L7_STAMP(4);

@@ -4,6 +4,9 @@
 #pragma once
 #include "dts_internal.h"
 
+#ifndef DTS_L7_COMPACT_EDGE
+#define DTS_L7_COMPACT_EDGE 0   // 1: partial-row stores as a byte loop (smaller walk code; A/B)
+#endif
 #ifndef DTS_NT_STORES
 #define DTS_NT_STORES 0     // 1: non-temporal output row stores (ladder7 A/B)
 #endif
@@ -64,6 +67,19 @@ __device__ __forceinline__ void put_row6(uint64_t rowp, int at, int room, const 
             *GP6(g_u32, p) = w[0];
 #endif
     } else {
+#if DTS_L7_COMPACT_EDGE
+        // the plane's last columns (right-edge units only): a byte loop, not unrolled -- the
+        // unrolled form put NB predicated stores with their exec-mask sequences into every
+        // row-block store site of every walk variant, code the whole CU pair's instruction
+        // cache carries for a path few waves take
+        asm volatile("" : "+v"(room));
+#pragma unroll 1
+        for (int i = 0; i < NB && i < room; ++i) {
+            const int q = i >> 2;
+            const uint32_t d = q == 0 ? w[0] : q == 1 ? w[1 % (NB / 4)] : q == 2 ? w[2 % (NB / 4)] : w[3 % (NB / 4)];
+            p[i] = (uint8_t)(d >> (8 * (i & 3)));
+        }
+#else
         // the plane's last columns: predicated byte stores.  room goes through an empty asm
         // so the per-byte lane masks are formed here, not hoisted out of the walk (16 SGPR
         // pairs live across every granule)
@@ -71,6 +87,7 @@ __device__ __forceinline__ void put_row6(uint64_t rowp, int at, int room, const 
 #pragma unroll
         for (int i = 0; i < NB; ++i)
             if (i < room) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+#endif
     }
 }
 
