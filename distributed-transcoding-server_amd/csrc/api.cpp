@@ -1061,6 +1061,8 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
+    // diagnostic: a floor on the workgroup's LDS (one group per CU leaves room for other kernels' workgroups)
+    if (const char *e = diag_env("DTS_L7_LDS_MIN")) g->lds7 = std::max(g->lds7, std::min(atoi(e), 160 * 1024));
     g->waves7 = gp.p7.waves;
     g->hsplit7 = gp.p7.hsplit;
     g->v7 = true;
