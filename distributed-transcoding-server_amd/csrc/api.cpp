@@ -221,11 +221,7 @@ struct dts_graph {
     DevLayout lay_mid[DTS_MAX_OUTPUTS];
     uint8_t *hdr_mid[2][DTS_MAX_OUTPUTS] = {};
     hipEvent_t hdr_ev[2] = {nullptr, nullptr};   // k_tonemap done reading intermediate sl
-    hipEvent_t hdr_mid_ev[2] = {nullptr, nullptr};   // the ladder wrote intermediate sl
-    hipEvent_t hdr_go = nullptr, hdr_end = nullptr;
-    hipStream_t hdr_tm = nullptr;         // k_tonemap's stream: the tonemap of chunk i runs beside the
-                                          // ladder of chunk i + 1 (nullptr: both on the caller's stream)
-    int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk
+    int hdr_chunk = 0;                    // frames per ladder -> tonemap chunk (the graph's batch)
     unsigned hdr_next = 0;
     TonemapParams tm{};
     float *dev_tm_lut = nullptr;          // the transfer-curve tables of tm (TonemapParams::lut)
@@ -547,21 +543,6 @@ bool l7_narrow()
 {
     const char *f = diag_env("DTS_L7_NARROW");
     return f ? f[0] == '1' : false;
-}
-
-// HDR graphs: frames per ladder -> tonemap chunk and whether the tonemaps run on a stream of
-// their own (diagnostic DTS_HDR_CHUNK / DTS_HDR_STREAMS; the defaults are the measured best)
-int hdr_chunk_frames(int batch)
-{
-    const char *f = diag_env("DTS_HDR_CHUNK");
-    const int c = f ? std::atoi(f) : batch;
-    return std::min(std::max(c, 1), batch);
-}
-
-bool hdr_two_streams()
-{
-    const char *f = diag_env("DTS_HDR_STREAMS");
-    return f ? f[0] == '2' : false;
 }
 
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
@@ -1061,8 +1042,6 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
     g->ngroups7 = (int)gp.p7.groups.size();
     g->lds7 = gp.p7.lds_bytes;
-    // diagnostic: a floor on the workgroup's LDS (one group per CU leaves room for other kernels' workgroups)
-    if (const char *e = diag_env("DTS_L7_LDS_MIN")) g->lds7 = std::max(g->lds7, std::min(atoi(e), 160 * 1024));
     g->waves7 = gp.p7.waves;
     g->hsplit7 = gp.p7.hsplit;
     g->v7 = true;
@@ -1116,20 +1095,13 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
             // chunk's ladder are no faster -- DESIGN.md §4 k_tonemap)
             e = DTS_OK;
             for (int k = 0; k < s.nout; ++k) g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
-            g->hdr_chunk = hdr_chunk_frames(g->batch);
+            g->hdr_chunk = g->batch;
             for (int sl = 0; sl < 2 && !e; ++sl) {
                 for (int k = 0; k < s.nout && !e; ++k)
                     if (hipMalloc(&g->hdr_mid[sl][k], (size_t)g->hdr_chunk * g->lay_mid[k].fstride) != hipSuccess)
                         e = DTS_E_NOMEM;
-                if (!e && (hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess ||
-                           hipEventCreateWithFlags(&g->hdr_mid_ev[sl], hipEventDisableTiming) != hipSuccess))
-                    e = DTS_E_HIP;
+                if (!e && hipEventCreateWithFlags(&g->hdr_ev[sl], hipEventDisableTiming) != hipSuccess) e = DTS_E_HIP;
             }
-            if (!e && hdr_two_streams() &&
-                (hipStreamCreateWithFlags(&g->hdr_tm, hipStreamNonBlocking) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->hdr_go, hipEventDisableTiming) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->hdr_end, hipEventDisableTiming) != hipSuccess))
-                e = DTS_E_HIP;
             if (!e) {
                 const std::vector<float> luts = tonemap_luts(s.tonemap);
                 const size_t nb = luts.size() * sizeof(float);
@@ -1204,14 +1176,7 @@ void dts_graph_destroy(dts_graph *g)
     if (!g) return;
     hipSetDevice(g->ctx->device);
     free_host_path(g);
-    if (g->hdr_tm) {
-        hipStreamSynchronize(g->hdr_tm);
-        hipStreamDestroy(g->hdr_tm);
-    }
-    if (g->hdr_go) hipEventDestroy(g->hdr_go);
-    if (g->hdr_end) hipEventDestroy(g->hdr_end);
     for (int sl = 0; sl < 2; ++sl) {
-        if (g->hdr_mid_ev[sl]) hipEventDestroy(g->hdr_mid_ev[sl]);
         if (g->hdr_ev[sl]) {
             hipEventSynchronize(g->hdr_ev[sl]);
             hipEventDestroy(g->hdr_ev[sl]);
@@ -1500,20 +1465,15 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
 }
 
 // HDR10 -> SDR: per chunk of hdr_chunk frames, the bit-exact ladder into a p010
-// intermediate (two, alternating), then k_tonemap from it into the caller's output.  With
-// the tonemap stream (hdr_tm) the tonemap of chunk i runs beside the ladder of chunk i + 1
-// -- the memory-bound ladder and the VALU-bound tonemap share the CUs -- and the caller's
-// stream waits for the last tonemap before the call returns; without it both run in order
-// on the caller's stream.
+// intermediate (two, alternating: a chunk's ladder may run while the other buffer's tonemap
+// of the host path's other stream still reads), then k_tonemap from it into the caller's
+// output, both on the caller's stream.  (Round 4 measured the tonemaps on a stream of their
+// own beside the next chunk's ladder, with and without room for them on the ladder's CUs:
+// no gain -- DESIGN.md, k_tonemap.)
 static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst, int nframes, hipStream_t st)
 {
     const dts_graph_spec &s = g->spec;
     dts_ctx *ctx = g->ctx;
-    hipStream_t tm = g->hdr_tm ? g->hdr_tm : st;
-    if (g->hdr_tm) {                                  // the outputs' earlier users on st come first
-        HIPCHK(ctx, hipEventRecord(g->hdr_go, st));
-        HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_go, 0));
-    }
     for (int f0 = 0; f0 < nframes; f0 += g->hdr_chunk) {
         const int n = std::min(g->hdr_chunk, nframes - f0);
         const int sl = (int)(g->hdr_next++ & 1u);
@@ -1527,10 +1487,6 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
         }
         int e = enqueue_ladder(g, sc, mid, mid_fmt, n, st);
         if (e) return e;
-        if (g->hdr_tm) {
-            HIPCHK(ctx, hipEventRecord(g->hdr_mid_ev[sl], st));
-            HIPCHK(ctx, hipStreamWaitEvent(tm, g->hdr_mid_ev[sl], 0));
-        }
         for (int k = 0; k < s.nout; ++k) {
             TonemapParams tp = g->tm;
             tp.src = mid[k];
@@ -1540,13 +1496,9 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
             tp.w = s.out[k].w;
             tp.h = s.out[k].h;
             tp.nframes = n;
-            HIPCHK(ctx, launch_tonemap(tp, tm));
+            HIPCHK(ctx, launch_tonemap(tp, st));
         }
-        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], tm));
-    }
-    if (g->hdr_tm) {
-        HIPCHK(ctx, hipEventRecord(g->hdr_end, tm));
-        HIPCHK(ctx, hipStreamWaitEvent(st, g->hdr_end, 0));
+        HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], st));
     }
     return DTS_OK;
 }

@@ -28,10 +28,6 @@
 #ifndef DTS_TM_ABLATE
 #define DTS_TM_ABLATE 0     // diagnostic bits (wrong output): 1 no ring pass, 2 no chroma 2:1 pass, 4 no pixel math
 #endif
-#ifndef DTS_TM_OCC
-#define DTS_TM_OCC 0        // 5: value-only tables (two adjacent reads per lookup, 8.2 KB of LDS) and <= 96 VGPRs:
-                            // five workgroups per CU instead of four (A/B knob)
-#endif
 #ifndef DTS_TM_UNROLL
 #define DTS_TM_UNROLL 0     // 1: both block iterations of a lane unrolled (8 pixels in flight; A/B knob)
 #endif
@@ -56,28 +52,6 @@ __device__ __forceinline__ float lut(const float2 *t, float xn)
     const float2 e = t[(int)x];
     return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
 }
-
-// value-only table t[0..kTmLutN + 1] (the last entry repeated): the two entries around x
-// (one ds_read2_b32), the slope formed here
-[[maybe_unused]] __device__ __forceinline__ float lut(const float *t, float xn)
-{
-    const float x = __builtin_amdgcn_fmed3f(xn, 0.f, (float)kTmLutN);
-    const int i = (int)x;
-    const float a = t[i], b = t[i + 1];
-    return __builtin_fmaf(__builtin_amdgcn_fractf(x), b - a, a);
-}
-
-// LDS image of the transfer tables: (value, slope) pairs or values only
-template <bool VALUES> struct TmTab;
-template <> struct TmTab<false> {
-    using T = float2;
-    static constexpr int stride = kTmLutN + 1;
-};
-template <> struct TmTab<true> {
-    using T = float;
-    [[maybe_unused]] static constexpr int stride = kTmLutN + 2;
-};
-using TmT = TmTab<DTS_TM_OCC != 0>;
 
 #if DTS_TM_OETF_POW
 // BT.709 OETF on [0, 1] (the host table's curve, api.cpp tonemap_luts)
@@ -119,7 +93,7 @@ __device__ __forceinline__ int q8(float v)
 // The curve and the desaturation switch are template parameters: a branch per pixel
 // would keep the compiler from interleaving a thread's four pixels (LUT reads in flight).
 template <int MODE, bool DESAT>
-__device__ __forceinline__ void pixel(const TonemapParams &P, const TmT::T *tl, float y10, float2 c, float &Y,
+__device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, float y10, float2 c, float &Y,
                                       float2 &C)
 {
     if (DTS_TM_ABLATE & 4) {
@@ -127,7 +101,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const TmT::T *tl, 
         C = c;
         return;
     }
-    const TmT::T *pq = tl, *oetf = tl + TmT::stride;          // pq already scaled by 10000 / npl
+    const float2 *pq = tl, *oetf = tl + kTmLutN + 1;          // pq already scaled by 10000 / npl
     constexpr float N = (float)kTmLutN;
     constexpr float kr2 = 0.2627f, kb2 = 0.0593f, kg2 = 1.f - kr2 - kb2;
     constexpr float kr7 = 0.2126f, kb7 = 0.0722f, kg7 = 1.f - kr7 - kb7;
@@ -193,18 +167,13 @@ constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged:
 // luma loads, 16-byte (Cb, Cr) x 2 LDS stores; edge tiles and the one-pixel ring take
 // the per-pixel path with the clamps.  The top ring row of tile t > 0 is the previous
 // tile's last luma row, carried in LDS rather than recomputed.
-#if DTS_TM_OCC
-#define DTS_TM_ATTR __attribute__((amdgpu_waves_per_eu(DTS_TM_OCC)))
-#else
-#define DTS_TM_ATTR
-#endif
 template <int MODE, bool DESAT>
-__global__ void __launch_bounds__(256) DTS_TM_ATTR k_tonemap(const TonemapParams P)
+__global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
     constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
     constexpr int kRow = 129;                       // ring row: columns x0 - 1 .. x0 + 127
     constexpr int kCin = kTmCH * kTmCW;             // staged chroma samples per tile (660: 3 per thread)
-    __shared__ TmT::T tl[kTabs * TmT::stride];
+    __shared__ float2 tl[kTabs * (kTmLutN + 1)];
     __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
     __shared__ __attribute__((aligned(16))) float2 cc[kTmLH][kTmLP];   // output (Cb, Cr) at full resolution
     const int t = threadIdx.x, f = blockIdx.z;
@@ -215,14 +184,7 @@ __global__ void __launch_bounds__(256) DTS_TM_ATTR k_tonemap(const TonemapParams
     const uint64_t sy0 = P.src.data[0] + sf, sc0 = P.src.data[1] + sf;
     const int lp = P.src.pitch[0], cp = P.src.pitch[1];
     const bool a4 = ((P.src.data[0] + sf) & 3) == 0 && (P.src.pitch[0] & 3) == 0;
-    if (DTS_TM_OCC) {
-        for (int i = t; i < kTabs * TmT::stride; i += 256) {
-            const int c = i / TmT::stride, j = i - c * TmT::stride;
-            ((float *)tl)[i] = P.lut[c * (kTmLutN + 1) + min(j, kTmLutN)].x;
-        }
-    } else {
-        for (int i = t; i < kTabs * (kTmLutN + 1); i += 256) ((float2 *)tl)[i] = P.lut[i];
-    }
+    for (int i = t; i < kTabs * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
     // a thread's staged chroma samples (rows / columns fixed over the tiles) and block positions
     int cr[3], cxo[3];
 #pragma unroll

@@ -50,8 +50,6 @@
 //    granule publishes them to the other waves of the rendition;
 //  * waves beyond the group's units (the workgroup has the widest group's size)
 //    only stage pieces and keep the barrier count.
-#include <type_traits>
-
 #include "dts_internal.h"
 #include "ladder_mfma.h"
 
@@ -721,34 +719,8 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 #ifndef DTS_L7_UNROLL8
 #define DTS_L7_UNROLL8 1
 #endif
-    // DTS_L7_ROLLED: one staging batch per loop copy (UNR = PB7) and the ring slot chosen at run
-    // time by a switch -- a quarter / an eighth of the code (A/B)
-#ifndef DTS_L7_ROLLED
-#define DTS_L7_ROLLED 0
-#endif
-    constexpr bool ROLL = DTS_L7_ROLLED;
-    constexpr int UNR = ROLL ? PB7 : (DTS_L7_UNROLL8 ? 8 : (R > 2 * PB7 ? R : 2 * PB7));
-    static_assert(ROLL || (UNR % R == 0 && UNR % PB7 == 0), "ring and batch periods divide the unroll");
-    // the H result of tile t (hi / lo dwords) into ring slot K
-    auto ring_put = [&](auto K, int t, uint32_t hv, uint32_t lv) {
-        constexpr int k = decltype(K)::value;
-        if constexpr (k < R) {
-            rh[k / 4][t][k % 4] = (int)hv;
-            rl[k / 4][t][k % 4] = (int)lv;
-        }
-    };
-    auto ring_put_rt = [&](int rsr, int t, uint32_t hv, uint32_t lv) {
-        switch (rsr) {      // (the empty asm keeps each case a branch, not a select over every slot)
-        case 0: asm volatile(""); ring_put(std::integral_constant<int, 0>{}, t, hv, lv); break;
-        case 1: asm volatile(""); ring_put(std::integral_constant<int, 1>{}, t, hv, lv); break;
-        case 2: asm volatile(""); ring_put(std::integral_constant<int, 2>{}, t, hv, lv); break;
-        case 3: asm volatile(""); ring_put(std::integral_constant<int, 3>{}, t, hv, lv); break;
-        case 4: asm volatile(""); ring_put(std::integral_constant<int, 4>{}, t, hv, lv); break;
-        case 5: asm volatile(""); ring_put(std::integral_constant<int, 5>{}, t, hv, lv); break;
-        case 6: asm volatile(""); ring_put(std::integral_constant<int, 6>{}, t, hv, lv); break;
-        default: asm volatile(""); ring_put(std::integral_constant<int, 7>{}, t, hv, lv); break;
-        }
-    };
+    constexpr int UNR = DTS_L7_UNROLL8 ? 8 : (R > 2 * PB7 ? R : 2 * PB7);
+    static_assert(UNR % R == 0 && UNR % PB7 == 0, "ring and batch periods divide the unroll");
     const int ngran = G.ngran;
     int sq = 0;
     L7_STAMP_INIT;
@@ -898,12 +870,8 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 const int rs = s % R;
 #define WRING(t_, hv_, lv_)                                                                   \
     do {                                                                                      \
-        if constexpr (ROLL) {                                                                 \
-            ring_put_rt(q % R, (t_), (hv_), (lv_));                                           \
-        } else {                                                                              \
-            rh[rs / 4][(t_)][rs % 4] = (int)(hv_);                                            \
-            rl[rs / 4][(t_)][rs % 4] = (int)(lv_);                                            \
-        }                                                                                     \
+        rh[rs / 4][(t_)][rs % 4] = (int)(hv_);                                                \
+        rl[rs / 4][(t_)][rs % 4] = (int)(lv_);                                                \
     } while (0)
                 if ((HS == 128 || P10) && !RC) {
 #pragma unroll
