@@ -363,13 +363,32 @@ __device__ __forceinline__ uint32_t win3(const uint32_t *a, int i)
     return __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], sel);
 }
 
-__device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn_sad_u8((uint32_t)a, (uint32_t)b, 0u); }
 
 // vf_yadif.c filter_line_c / filter_edges for the 16 pixels x .. x + 15 of one interpolated
 // row.  cm / cp: cur rows mrefs / prefs, bytes x - 16 .. x + 31 (pixel k at byte 16 + k);
 // the rest bytes x .. x + 15: pm / pp prev rows mrefs / prefs, nm / np next, p2 / n2 prev2 /
-// next2 on this row, p2m .. n2p prev2 / next2 two rows away (mode 0 only).  ne: bit k set
-// when pixel k is not an edge pixel (3 <= x + k < w - 3).
+// next2 on this row, p2m .. n2p prev2 / next2 two rows away (FAR: mode 0 / 1 away from the
+// top and bottom rows).  ne: bit k set when pixel k is not an edge pixel (3 <= x + k < w - 3);
+// edge pixels skip the spatial search (filter_edges).  In three parts:
+// - the temporal bounds d -+ diff (everything but the spatial search) for two pixels per
+//   dword, as packed 16-bit lanes (v_pk_* arithmetic: half the instructions of a pixel at a
+//   time; no value leaves [-510, 510]);
+// - the spatial search per pixel, without a branch, so the 3-byte windows are shared between
+//   neighbouring pixels (window i of cm serves pixels i - 1 .. i + 3: 20 windows per row for
+//   16 pixels instead of 80) and the candidate predictions stay sums until one halving; a
+//   scheduling barrier per pixel keeps the live windows to the sliding ten.  Edge pixels'
+//   windows read the staged halo (clamped columns) and are replaced afterwards;
+// - the clamp, packed again.
+typedef short i16x2y __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i16x2y pair16(uint32_t d, int h)   // bytes 2h, 2h + 1 of d, zero-extended
+{
+    return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(0u, d, h ? 0x0c030c02u : 0x0c010c00u));
+}
+__device__ __forceinline__ i16x2y absd16(i16x2y a, i16x2y b)
+{
+    return __builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b);
+}
+
 template <bool FAR>
 __device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t (&cp)[12], const uint32_t (&pm)[4],
                                         const uint32_t (&pp)[4], const uint32_t (&nm)[4], const uint32_t (&np)[4],
@@ -377,50 +396,86 @@ __device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t
                                         const uint32_t (&p2p)[4], const uint32_t (&n2m)[4], const uint32_t (&n2p)[4],
                                         uint32_t ne, uint32_t (&out)[4])
 {
+    i16x2y lo[8], hi[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[q] = 0;
+    for (int i = 0; i < 8; ++i) {
+        const int q = i >> 1, h = i & 1;
+        const i16x2y c = pair16(cm[4 + q], h), e = pair16(cp[4 + q], h);
+        const i16x2y a2 = pair16(p2[q], h), b2 = pair16(n2[q], h);
+        const i16x2y d = (a2 + b2) >> 1;
+        const i16x2y td0 = absd16(a2, b2);
+        const i16x2y td1 = (absd16(pair16(pm[q], h), c) + absd16(pair16(pp[q], h), e)) >> 1;
+        const i16x2y td2 = (absd16(pair16(nm[q], h), c) + absd16(pair16(np[q], h), e)) >> 1;
+        i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0 >> 1, td1), td2);
+        if (FAR) {
+            const i16x2y b = (pair16(p2m[q], h) + pair16(n2m[q], h)) >> 1;
+            const i16x2y f = (pair16(p2p[q], h) + pair16(n2p[q], h)) >> 1;
+            const i16x2y de = d - e, dc = d - c, bc = b - c, fe = f - e;
+            const i16x2y mx = __builtin_elementwise_max(__builtin_elementwise_max(de, dc), __builtin_elementwise_min(bc, fe));
+            const i16x2y mn = __builtin_elementwise_min(__builtin_elementwise_min(de, dc), __builtin_elementwise_max(bc, fe));
+            diff = __builtin_elementwise_max(__builtin_elementwise_max(diff, mn), -mx);
+        }
+        lo[i] = d - diff;
+        hi[i] = d + diff;
+    }
+    // the 3-byte windows of cm / cp starting at byte 13 + i (i = 0 .. 19), made as the walk
+    // reaches them and passed through an empty asm: what depends on a window cannot be
+    // scheduled before it, so the sliding ten are all that is live
+    uint32_t wm[20], wp[20];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        wm[i] = win3(cm, 13 + i);
+        wp[i] = win3(cp, 13 + i);
+        asm volatile("" : "+v"(wm[i]), "+v"(wp[i]));
+    }
+    auto b8 = [](uint32_t w, int i) { return (int)((w >> (8 * i)) & 255u); };
+    uint32_t pr[8];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int X = 16 + k;
-        const int c = byte_at(cm, X), e = byte_at(cp, X);
-        const int a2 = byte_at(p2, k), b2 = byte_at(n2, k);
-        const int d = (a2 + b2) >> 1;
-        const int td0 = absd(a2, b2);
-        const int td1 = (absd(byte_at(pm, k), c) + absd(byte_at(pp, k), e)) >> 1;
-        const int td2 = (absd(byte_at(nm, k), c) + absd(byte_at(np, k), e)) >> 1;
-        int diff = max(max(td0 >> 1, td1), td2);
-        int pred = (c + e) >> 1;
-        if ((ne >> k) & 1u) {               // (a branch per pixel, uniform in interior tiles: computed
-                                            // unconditionally the sixteen pixels' window sums share
-                                            // values across pixels and need 241 VGPRs)
-            // CHECK(j): the 3-byte windows cm[x + j - 1 ..] vs cp[x - j - 1 ..]
-            int score = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 1), win3(cp, X - 1), 0u) - 1;
-            const int sm1 = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 2), win3(cp, X), 0u);
-            const int sm2 = (int)__builtin_amdgcn_sad_u8(win3(cm, X - 3), win3(cp, X + 1), 0u);
-            const int s1 = (int)__builtin_amdgcn_sad_u8(win3(cm, X), win3(cp, X - 2), 0u);
-            const int s2 = (int)__builtin_amdgcn_sad_u8(win3(cm, X + 1), win3(cp, X - 3), 0u);
-            const bool b1 = sm1 < score;
-            score = b1 ? sm1 : score;
-            pred = b1 ? (byte_at(cm, X - 1) + byte_at(cp, X + 1)) >> 1 : pred;
-            const bool bb2 = b1 && sm2 < score;
-            score = bb2 ? sm2 : score;
-            pred = bb2 ? (byte_at(cm, X - 2) + byte_at(cp, X + 2)) >> 1 : pred;
-            const bool b3 = s1 < score;
-            score = b3 ? s1 : score;
-            pred = b3 ? (byte_at(cm, X + 1) + byte_at(cp, X - 1)) >> 1 : pred;
-            const bool b4 = b3 && s2 < score;
-            pred = b4 ? (byte_at(cm, X + 2) + byte_at(cp, X - 2)) >> 1 : pred;
-        }
-        if (FAR) {
-            const int b = (byte_at(p2m, k) + byte_at(n2m, k)) >> 1;
-            const int f = (byte_at(p2p, k) + byte_at(n2p, k)) >> 1;
-            const int mx = max(max(d - e, d - c), min(b - c, f - e));
-            const int mn = min(min(d - e, d - c), max(b - c, f - e));
-            diff = max(max(diff, mn), -mx);
-        }
-        // diff >= 0, so the reference's two-sided clamp is a median
-        pred = min(max(pred, d - diff), d + diff);
-        out[k >> 2] |= (uint32_t)pred << (8 * (k & 3));
+        // pixel X = 16 + k: windows starting at X - 3 .. X + 1 = indices k .. k + 4
+        wm[k + 4] = win3(cm, 17 + k);
+        wp[k + 4] = win3(cp, 17 + k);
+        asm volatile("" : "+v"(wm[k + 4]), "+v"(wp[k + 4]));
+        const uint32_t m3 = wm[k], m2 = wm[k + 1], m1 = wm[k + 2], m0 = wm[k + 3], m_1 = wm[k + 4];
+        const uint32_t p3 = wp[k], p2_ = wp[k + 1], p1 = wp[k + 2], p0 = wp[k + 3], p_1 = wp[k + 4];
+        // CHECK(j): cm window at X + j - 1 against cp window at X - j - 1
+        int score = (int)__builtin_amdgcn_sad_u8(m1, p1, 0u) - 1;
+        const int sm1 = (int)__builtin_amdgcn_sad_u8(m2, p0, 0u);
+        const int sm2 = (int)__builtin_amdgcn_sad_u8(m3, p_1, 0u);
+        const int s1 = (int)__builtin_amdgcn_sad_u8(m0, p2_, 0u);
+        const int s2 = (int)__builtin_amdgcn_sad_u8(m_1, p3, 0u);
+        // 2 x the candidate predictions, bytes of the same windows: window X - 1 holds X - 1 .. X + 1
+        int ps = b8(m1, 1) + b8(p1, 1);                   // cm[X] + cp[X]
+        const bool b1 = sm1 < score;
+        score = b1 ? sm1 : score;
+        ps = b1 ? b8(m1, 0) + b8(p0, 1) : ps;             // cm[X - 1] + cp[X + 1]
+        const bool bb2 = b1 & (sm2 < score);
+        score = bb2 ? sm2 : score;
+        ps = bb2 ? b8(m2, 0) + b8(p0, 2) : ps;            // cm[X - 2] + cp[X + 2]
+        const bool b3 = s1 < score;
+        score = b3 ? s1 : score;
+        ps = b3 ? b8(m0, 1) + b8(p1, 0) : ps;             // cm[X + 1] + cp[X - 1]
+        const bool b4 = b3 & (s2 < score);
+        ps = b4 ? b8(m0, 2) + b8(p2_, 0) : ps;            // cm[X + 2] + cp[X - 2]
+        const uint32_t pv = (uint32_t)ps >> 1;
+        pr[k >> 1] = (k & 1) ? pr[k >> 1] | (pv << 16) : pv;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ne != 0xffffu) {                                  // filter_edges: no spatial search
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!((ne >> k) & 1u)) {
+                const uint32_t pv = (uint32_t)(byte_at(cm, 16 + k) + byte_at(cp, 16 + k)) >> 1;
+                pr[k >> 1] = (k & 1) ? (pr[k >> 1] & 0xffffu) | (pv << 16) : (pr[k >> 1] & 0xffff0000u) | pv;
+            }
+    }
+    // the reference's two-sided clamp (diff >= 0: a median), then two 16-bit pairs per dword of bytes
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const i16x2y r0 = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q]), lo[2 * q]), hi[2 * q]);
+        const i16x2y r1 = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q + 1]), lo[2 * q + 1]),
+                                                    hi[2 * q + 1]);
+        out[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, r1), __builtin_bit_cast(uint32_t, r0), 0x06040200u);
     }
 }
 
@@ -472,7 +527,6 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
     const uint64_t sbase = P.seq.data[p];
     const int wr16 = (w + 15) & ~15;
     // one frame tile (sequence frame clamped to [0, nseq)) into LDS slot s: this wave's pieces
-    int ops = 0;
     auto stage = [&](int pos, int s) {
         const int f = min(max(P.first + pos, 0), P.nseq - 1);
         const uint64_t fb = sbase + (uint64_t)f * (uint64_t)P.seq.fstride;
@@ -486,7 +540,6 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
                                                  (__attribute__((address_space(3))) void *)(yl + s * kYtSlot + 1024 * k),
                                                  16, 0, 0);
             }
-            ++ops;
         }
     };
     // every output row of this tile is whole and every 16-byte segment inside the plane: the
@@ -503,12 +556,12 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
     const uint64_t obase0 = P.dst.data[p] + (uint64_t)x;
     for (int j = j0; j < j1; ++j) {
         const int s = j - j0;
-        if (s) __syncthreads();                // every wave is done with frame j - 2's slot
-        const int dma0 = ops;
-        if (j + 2 <= j1) stage(j + 2, (s + 3) & 3);
-        // frame j + 1's pieces: issued before the previous step's stores and these pieces
-        vm_wait_yt(nst + (ops - dma0));
+        // frame j + 1's pieces (issued a step ago, before that step's stores) have landed in
+        // every wave; past the barrier every wave is also done with step j - 1, so frame
+        // j - 2's slot takes frame j + 2 -- one barrier per step
+        vm_wait_yt(nst);
         __syncthreads();
+        if (j + 2 <= j1) stage(j + 2, (s + 3) & 3);
         const uint8_t *sl_p = yl + ((s + 0) & 3) * kYtSlot, *sl_c = yl + ((s + 1) & 3) * kYtSlot,
                       *sl_n = yl + ((s + 2) & 3) * kYtSlot;
         nst = 0;
