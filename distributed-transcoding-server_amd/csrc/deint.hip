@@ -337,6 +337,9 @@ constexpr int kYtThreads = 512;
 #define DTS_YADIF_WALK 16
 #endif
 constexpr int kYtWalk = DTS_YADIF_WALK;         // input frames per workgroup
+#ifndef DTS_YT_ABLATE
+#define DTS_YT_ABLATE 0                         // diagnostic bits (wrong output): 1 no arithmetic
+#endif
 
 namespace {
 
@@ -602,7 +605,10 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
 #pragma unroll
                 for (int k = 0; k < 16; ++k) ne |= (x + k >= 3 && x + k < w - 3) ? 1u << k : 0u;
                 uint32_t res[4];
-                if (far) {
+                if (DTS_YT_ABLATE & 1) {               // diagnostic: no arithmetic (wrong output)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) res[q] = cm[4 + q] ^ cp[4 + q] ^ pm[q] ^ np[q] ^ p2[q] ^ n2[q];
+                } else if (far) {
                     const int rm2 = 2 * rm - y, rp2 = 2 * rp - y;   // 2 mrefs / 2 prefs
                     unpack4(lds16(row(pv2, rm2)), p2m);
                     unpack4(lds16(row(pv2, rp2)), p2p);

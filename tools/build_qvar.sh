@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../distributed-transcoding-server_amd"
 make -s lib/libdts.so
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-value -Wno-unused-result"
-OBJS="build/filters.o build/plan5.o build/plan6.o build/ladder4.o build/ladder5.o build/ladder7.o build/hdr.o build/deint.o build/qfuse.o"
+OBJS="build/filters.o build/plan5.o build/plan6.o build/ladder4.o build/ladder5.o build/ladder7.o build/hdr.o build/deint.o"
 for a in "$@"; do
   n=${a%%=*}; d=${a#*=}
   if [ "${d:0:1}" = "@" ]; then
