@@ -9,4 +9,4 @@ make -s lib/libdts.so
     -c csrc/ladder7.hip -o build/ladder7_stamp.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libdts_stamp7.so build/api_stamp7.o build/filters.o \
     build/plan5.o build/plan6.o build/kernels.o build/ladder4.o build/ladder5.o build/ladder7_stamp.o \
-    build/hdr.o build/deint.o build/qfuse.o -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdts.so
+    build/hdr.o build/deint.o -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdts.so

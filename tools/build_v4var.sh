@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/../distributed-transcoding-server_amd"
 make -s lib/libdts.so
-OBJS="build/api.o build/filters.o build/plan5.o build/plan6.o build/kernels.o build/ladder5.o build/ladder7.o build/hdr.o build/deint.o build/qfuse.o"
+OBJS="build/api.o build/filters.o build/plan5.o build/plan6.o build/kernels.o build/ladder5.o build/ladder7.o build/hdr.o build/deint.o"
 for a in "$@"; do
   n=${a%%=*}; d=${a#*=}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $d -c csrc/ladder4.hip -o build/ladder4_$n.o \
