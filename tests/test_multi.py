@@ -1,6 +1,6 @@
 """N > 1 path on CPU: bench.py's per-rank segment sharding and its only
 collectives (record all-gather + wall-time max-reduce), run with the gloo
-backend at world size 2 (the GPU box runs the same code over RCCL)."""
+backend at world sizes 2 and 4 (the GPU box runs the same code over RCCL)."""
 import os
 import socket
 import sys
@@ -32,17 +32,17 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_gather_records_gloo_world2():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_records_gloo(world):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for rank in range(world):
         total, wall, recs, base = out[rank]
-        assert total == 32 + 64
-        assert wall == pytest.approx(1.5)                 # max over ranks
-        assert recs == [(32, 1000), (64, 1001)]
-    assert out[0][3] != out[1][3]                          # disjoint segments per rank
+        assert total == sum(32 * (r + 1) for r in range(world))
+        assert wall == pytest.approx(world - 0.5)         # max over ranks
+        assert recs == [(32 * (r + 1), 1000 + r) for r in range(world)]
+    assert len({out[r][3] for r in range(world)}) == world  # disjoint segments per rank
 
 
 def _qworker(rank, world, port, out):
@@ -66,11 +66,11 @@ def _segment_records(rank, nseg=3, nrung=3):
     return sse, ssim
 
 
-def test_gather_quality_gloo_world2():
-    """cfg5's quality-stat all-gather (RCCL on the GPU box) at world size 2 on gloo:
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_quality_gloo(world):
+    """cfg5's quality-stat all-gather (RCCL on the GPU box) at world sizes 2 and 4 on gloo:
     every rank ends with every rank's segment records in rank (= segment) order, equal
     to what a single rank holding all the segments would have."""
-    world = 2
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_qworker, args=(world, _free_port(), out), nprocs=world, join=True)
