@@ -1090,9 +1090,9 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
             g->hdr = true;
             g->tm = tonemap_params(s.tonemap);
             // chunks of `batch` frames: the ladder writes a chunk's p010 intermediates, k_tonemap
-            // converts them on the same stream (measured in round 3: smaller chunks, which keep the
-            // intermediates in the Infinity Cache, or the tonemap on a second stream beside the next
-            // chunk's ladder are no faster -- DESIGN.md §4 k_tonemap)
+            // converts them on the same stream (measured in rounds 3 and 4: smaller chunks, which keep
+            // the intermediates in the Infinity Cache, and the tonemap on a second stream beside the
+            // next chunk's ladder are slower -- DESIGN.md §4 k_tonemap)
             e = DTS_OK;
             for (int k = 0; k < s.nout; ++k) g->lay_mid[k].init(s.out[k].w, s.out[k].h, DTS_FMT_P010LE);
             g->hdr_chunk = g->batch;
