@@ -641,9 +641,22 @@ hipError_t launch_yadif_t(const YadifParams &p, int count, hipStream_t s)
     const int txl = (p.w + kYtW - 1) / kYtW, txc = (cw + kYtW - 1) / kYtW;
     const int tiles_l = txl * ((p.h + kYtH - 1) / kYtH), tiles_c = txc * ((ch + kYtH - 1) / kYtH);
     const int ntiles = tiles_l + 2 * tiles_c;
-    const dim3 grid((unsigned)(8 * ((ntiles + 7) / 8)), (unsigned)((count + kYtWalk - 1) / kYtWalk));
-    hipLaunchKernelGGL(k_yadif_t, grid, dim3(kYtThreads), 4 * kYtSlot, s, p, tiles_l, tiles_c, txl, txc, count);
-    return hipGetLastError();
+    // grid.y is one walk of kYtWalk frames; a longer sequence goes out in launches of at most
+    // 65535 walks (the y-dimension limit), each starting kMax frames further into the sequence
+    // and writing kMax * fields output frames further on
+    constexpr int kMax = 65535 * kYtWalk;
+    const int fields = (p.mode & 1) ? 2 : 1;
+    for (int done = 0; done < count; done += kMax) {
+        const int n = count - done < kMax ? count - done : kMax;
+        YadifParams q = p;
+        q.first += done;
+        for (int pl = 0; pl < 3; ++pl) q.dst.data[pl] += (uint64_t)done * fields * (uint64_t)p.dst.fstride;
+        const dim3 grid((unsigned)(8 * ((ntiles + 7) / 8)), (unsigned)((n + kYtWalk - 1) / kYtWalk));
+        hipLaunchKernelGGL(k_yadif_t, grid, dim3(kYtThreads), 4 * kYtSlot, s, q, tiles_l, tiles_c, txl, txc, n);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_yadif(const YadifParams &p, int nout, hipStream_t s)
