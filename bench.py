@@ -215,19 +215,20 @@ def unpack_dev_frame(raw, w, h, fmt):
     return planes
 
 
-def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_first=None, rung_qraws=None):
-    """Frame 0 of the last batch against the CPU oracle: bit-exact for the
-    integer paths, +-1 LSB for the HDR float path, 1e-4 for SSIM."""
+def verify_frame(wl, src_index, outs, j=0, qref_host=None, qraw=None, ring_first=None, ring_len=None,
+                 rung_qraws=None):
+    """Frame j of the last batch (source frame src_index) against the CPU oracle: bit-exact
+    for the integer paths, +-1 LSB for the HDR float path, 1e-4 for SSIM."""
     import numpy as np
     sw, sh, sfmt = wl["src"]
     host = D.synth_host(sw, sh, sfmt, 0, 0x5EED, src_index)
     prev = nxt = None
-    if wl.get("yadif") is not None:        # neighbours inside the ring (clamped at its first frame)
+    if wl.get("yadif") is not None:        # neighbours inside the ring (clamped at its ends)
         prev = D.synth_host(sw, sh, sfmt, 0, 0x5EED, max(src_index - 1, ring_first))
-        nxt = D.synth_host(sw, sh, sfmt, 0, 0x5EED, src_index + 1)
+        nxt = D.synth_host(sw, sh, sfmt, 0, 0x5EED, min(src_index + 1, ring_first + ring_len - 1))
     want, wq = oracle_outputs(wl, host, qref_host, prev, nxt)
     for k, (w, h, fmt, m) in enumerate(wl["outs"]):
-        got = unpack_dev_frame(outs[k][0].cpu().numpy(), w, h, fmt)
+        got = unpack_dev_frame(outs[k][j].cpu().numpy(), w, h, fmt)
         for a, b in zip(got, want[k]):
             if a is None:
                 continue
@@ -237,13 +238,13 @@ def verify_first_frame(wl, src_index, outs, qref_host=None, qraw=None, ring_firs
     if rung_qraws is not None:             # cfg5: each rendition's record vs the oracle's (lanczos reference)
         for k, (w, h, fmt, _m) in enumerate(wl["outs"]):
             oq = wq[k]
-            r = D.QRaw.from_buffer_copy(rung_qraws[k][0].cpu().numpy().tobytes())
+            r = D.QRaw.from_buffer_copy(rung_qraws[k][j].cpu().numpy().tobytes())
             gq = D.qstat_finalize(w, h, [r])[0]
             if gq["sse"] != oq["sse"] or abs(gq["ssim_all"] - oq["ssim_all"]) > 1e-4:
                 return False
     if wq is not None and qraw is not None and not wl.get("rung_quality"):
         w, h = wl["outs"][0][:2]
-        r = D.QRaw.from_buffer_copy(qraw[0].cpu().numpy().tobytes())
+        r = D.QRaw.from_buffer_copy(qraw[j].cpu().numpy().tobytes())
         gq = D.qstat_finalize(w, h, [r])[0]
         if gq["sse"] != wq["sse"] or abs(gq["ssim_all"] - wq["ssim_all"]) > 1e-4:
             return False
@@ -569,13 +570,18 @@ def main():
 
     verified = None
     if rank == 0 and not args.no_verify:
+        # the first and the last frame of the last batch (the last one sits in the launch's
+        # highest frame quad: k_ladder7 maps frame 8 fq + b % 8)
         last = args.warmup + args.steps - 1
-        qhost = None
-        if wl["quality"]:                  # the reference of the batch's frame 0
-            w, h, fmt, _m = wl["outs"][0]
-            qhost = D.synth_host(w, h, fmt, 0, 0x0EF, first + (last * B) % R)
-        verified = verify_first_frame(wl, first + (last * B) % R, outs, qhost, qraw, ring_first=first,
-                                      rung_qraws=qraws if rungq else None)
+        verified = True
+        for j in sorted({0, B - 1}):
+            si = first + (last * B) % R + j
+            qhost = None
+            if wl["quality"]:              # the reference of that frame
+                w, h, fmt, _m = wl["outs"][0]
+                qhost = D.synth_host(w, h, fmt, 0, 0x0EF, si)
+            verified = verified and verify_frame(wl, si, outs, j, qhost, qraw, ring_first=first, ring_len=R,
+                                                 rung_qraws=qraws if rungq else None)
     if rank == 0:
         fps = frames_total / wall_max
         algo = algo_bytes

@@ -7,16 +7,20 @@
 // host -- entropy decode and encode -- and takes the pixel filtergraph itself, so the
 // child processes talk rawvideo to it over pipes (`-f yuv4mpegpipe`):
 //
-//   decode:  ffmpeg -i SOURCE -f yuv4mpegpipe -pix_fmt yuv420p|yuv420p10le -   -> Y4MReader
-//   encode:  Y4MWriter -> ffmpeg -f yuv4mpegpipe -i - -c:v CODEC -b:v BITRATE ... SEGMENT
+//   decode:  ffmpeg -i SOURCE -f yuv4mpegpipe -pix_fmt yuv420p|yuv420p10le -   -> Y4MStream
+//   encode:  Y4MSink -> ffmpeg -f yuv4mpegpipe -i - -c:v CODEC -b:v BITRATE ... SEGMENT
 //   concat:  ffmpeg -f concat -safe 0 -i LIST -c copy OUTPUT  (a job's encoded segments)
 //
-// Both pipes are the children's stdio, made from a FIFO whose two ends are opened here (a
-// Node stream on a child's stdio would read ahead into its own buffer whenever the event loop
-// runs and take bytes from under the synchronous reader): the child's end in blocking mode,
-// the worker's end non-blocking, read / written synchronously (y4m.js retries EAGAIN; a
-// dead encoder is EPIPE, a finished decoder EOF).  Decode time lands in
-// JobChunks.result.readMs and encode time in writeMs / encodeMs, apart from gpuMs.  The binary: opts.ffmpeg, $DTS_FFMPEG,
+// Both pipes are the children's stdio as Node streams, polled by libuv on the event loop:
+// the decoder's stdout is read in paused mode (y4m.Y4MStream pulls only the frames the
+// segments ask for, so the child waits on a full pipe), the encoders' stdin is written
+// with 'drain' backpressure (y4m.Y4MSink), and stderr is always drained (an ffmpeg that
+// logs a lot never blocks on it).  No call here blocks the event loop: one Node process
+// drives every GPU slot of the node (SURVEY.md §8b "Threading"), and an encode waiting on a
+// slow libx264 must not hold back the other slots.  Every rendition of a segment gets its
+// own encoder child, all started before the first frame is written and fed concurrently
+// (encodeRenditions).  Decode time lands in JobChunks.result.readMs and encode time in
+// writeMs / encodeMs, apart from gpuMs.  The binary: opts.ffmpeg, $DTS_FFMPEG,
 // ffmpeg-static if installed, else `ffmpeg` on PATH; none -> null (the worker then reads and
 // writes Y4M files only).  libavcodec is not in this image: tests run a stub executable that
 // speaks yuv4mpegpipe.
@@ -25,7 +29,6 @@
 
 const cp = require("child_process");
 const fs = require("fs");
-const os = require("os");
 const path = require("path");
 const y4m = require("./y4m");
 
@@ -70,66 +73,48 @@ function encodeArgs(job, settings) {
     return a;
 }
 
-// A pipe as {mine, theirs}: `theirs` (blocking) for the child's stdin (toChild) or stdout,
-// `mine` (non-blocking) for this process.  Made from a FIFO opened from both sides, then
-// unlinked; the child's end is closed here once the child has it.
-let fifoSeq = 0;
-function pipePair(toChild) {
-    const p = path.join(os.tmpdir(), "dts-ff-" + process.pid + "-" + (fifoSeq++) + ".fifo");
-    cp.execFileSync("mkfifo", ["-m", "600", p]);
-    const C = fs.constants;
-    try {
-        if (toChild) {                         // we write, the child reads
-            const tmp = fs.openSync(p, C.O_RDONLY | C.O_NONBLOCK);      // a reader, so the next open does not block
-            const mine = fs.openSync(p, C.O_WRONLY | C.O_NONBLOCK);
-            const theirs = fs.openSync(p, C.O_RDONLY);                  // a writer exists: no block
-            fs.closeSync(tmp);
-            return { mine: mine, theirs: theirs };
-        }
-        const mine = fs.openSync(p, C.O_RDONLY | C.O_NONBLOCK);         // we read, the child writes
-        const theirs = fs.openSync(p, C.O_WRONLY);                      // a reader exists: no block
-        return { mine: mine, theirs: theirs };
-    } finally {
-        fs.unlinkSync(p);
-    }
-}
-
 function collect(child) {
     const err = [];
-    if (child.stderr) child.stderr.on("data", function (d) { if (err.length < 64) err.push(d); });
+    let kept = 0;
+    // drained whatever the child writes (a full stderr pipe would block it); the first 64 KB kept
+    if (child.stderr) child.stderr.on("data", function (d) { if (kept < 65536) { err.push(d); kept += d.length; } });
     return function () { return Buffer.concat(err).toString("utf8").trim(); };
 }
 
-// A decoder child: its stdout is a Y4M stream read by a Y4MReader (stream mode: frames in
-// order, kept until released).  fmt: the libdts source format wanted (8-bit -> yuv420p,
-// p010 -> yuv420p10le, which y4m.js turns into p010 host frames).
+function exitOf(child) {
+    return new Promise(function (resolve) {
+        child.on("exit", function (code, sig) { resolve({ code: code, signal: sig }); });
+        child.on("error", function (e) { resolve({ code: -1, error: e }); });
+    });
+}
+
+// A decoder child: its stdout is a Y4M stream read in order (y4m.Y4MStream: frames kept
+// until released).  fmt: the libdts source format wanted (8-bit -> yuv420p, p010 ->
+// yuv420p10le, which y4m.js turns into p010 host frames).  FfmpegDecoder.open resolves once
+// the stream's header has arrived.
 class FfmpegDecoder {
+    static async open(bin, input, opts) {
+        const d = new FfmpegDecoder(bin, input, opts);
+        try {
+            d.reader = await y4m.Y4MStream.open(d.child.stdout);
+        } catch (e) {
+            d.kill();
+            const st = await d.exited;
+            throw new Error("ffmpeg decode of " + input + ": " + e.message + " (" + (st.error || st.signal || st.code) + ") " +
+                            d.stderr());
+        }
+        d.hdr = d.reader.hdr;
+        return d;
+    }
     constructor(bin, input, opts) {
         opts = opts || {};
         const pf = opts.fmt === y4m.FMT_P010LE ? "yuv420p10le" : "yuv420p";
         this.args = ["-v", "error", "-nostdin", "-i", input, "-f", "yuv4mpegpipe", "-pix_fmt", pf, "-strict", "-1", "-"];
         this.t0 = Date.now();
-        const pp = pipePair(false);
-        try {
-            this.child = cp.spawn(bin, this.args, { stdio: ["ignore", pp.theirs, "pipe"] });
-        } finally {
-            fs.closeSync(pp.theirs);
-        }
-        this.fd = pp.mine;
+        this.child = cp.spawn(bin, this.args, { stdio: ["ignore", "pipe", "pipe"] });
         this.stderr = collect(this.child);
-        const self = this;
-        this.exited = new Promise(function (resolve) {
-            self.child.on("exit", function (code, sig) { resolve({ code: code, signal: sig }); });
-            self.child.on("error", function (e) { resolve({ code: -1, error: e }); });
-        });
-        try {
-            this.reader = new y4m.Y4MReader(this.fd);
-        } catch (e) {
-            this.kill();
-            fs.closeSync(this.fd);
-            throw new Error("ffmpeg decode of " + input + ": " + e.message);
-        }
-        this.hdr = this.reader.hdr;
+        this.exited = exitOf(this.child);
+        this.reader = null;
     }
     get frames() { return this.reader.frames; }
     read(i) { return this.reader.read(i); }
@@ -138,90 +123,97 @@ class FfmpegDecoder {
         try { this.child.kill("SIGKILL"); } catch (e) { /* gone */ }
     }
     close() {
-        this.reader.close();
-        if (this.fd !== null) fs.closeSync(this.fd);
-        this.fd = null;
+        if (this.reader) this.reader.close();
         if (this.child.exitCode === null) this.kill();
     }
 }
 
 // An encoder child: Y4M records written to its stdin become SEGMENT (codec, bitrate and
-// options of the Jobs row).  close() ends the stream and resolves once the child exits, with
-// the encode time and the file size.
+// options of the Jobs row).  write(frame) resolves when the child's pipe takes more;
+// close() ends the stream and resolves once the child exits, with the encode time and the
+// file size.
 class FfmpegEncoder {
     constructor(bin, out, w, h, fps, fmt, job, settings) {
         this.out = out;
         this.args = ["-v", "error", "-nostdin", "-f", "yuv4mpegpipe", "-i", "-"].concat(encodeArgs(job || {}, settings),
                                                                                        ["-y", out]);
         this.t0 = Date.now();
-        const pp = pipePair(true);
-        try {
-            this.child = cp.spawn(bin, this.args, { stdio: [pp.theirs, "ignore", "pipe"] });
-        } finally {
-            fs.closeSync(pp.theirs);
-        }
-        this.fd = pp.mine;
+        this.child = cp.spawn(bin, this.args, { stdio: ["pipe", "ignore", "pipe"] });
         this.stderr = collect(this.child);
-        const self = this;
-        this.exited = new Promise(function (resolve) {
-            self.child.on("exit", function (code, sig) { resolve({ code: code, signal: sig }); });
-            self.child.on("error", function (e) { resolve({ code: -1, error: e }); });
-        });
+        this.exited = exitOf(this.child);
+        this.sink = new y4m.Y4MSink(this.child.stdin, w, h, fps, fmt);
+    }
+    write(frame) { return this.sink.write(frame); }
+    kill() {
+        try { this.child.kill("SIGKILL"); } catch (e) { /* gone */ }
+    }
+    async close() {
+        let werr = null;
         try {
-            this.writer = new y4m.Y4MWriter(this.fd, w, h, fps, fmt);
+            await this.sink.end();                        // EOF: the encoder flushes and exits
         } catch (e) {
-            e.encoder = this;
-            throw e;
+            werr = e;                                     // EPIPE: the exit status says why
         }
-    }
-    write(frame) { this.writer.write(frame); }
-    _closeFd() {
-        if (this.fd !== null) fs.closeSync(this.fd);
-        this.fd = null;
-    }
-    close() {
-        const self = this;
-        this.writer.close();
-        this._closeFd();                                  // EOF: the encoder flushes and exits
-        return this.exited.then(function (st) {
-            if (st.code !== 0)
-                throw new Error("ffmpeg encode of " + self.out + " failed (" + (st.error || st.signal || st.code) + "): " +
-                                self.stderr());
-            return { file: self.out, bytes: fs.statSync(self.out).size, encodeMs: Date.now() - self.t0 };
-        });
+        const st = await this.exited;
+        if (st.code !== 0 || werr)
+            throw new Error("ffmpeg encode of " + this.out + " failed (" + (st.error || st.signal || st.code) + ")" +
+                            (werr ? " " + werr.message : "") + ": " + this.stderr());
+        return { file: this.out, bytes: fs.statSync(this.out).size, encodeMs: Date.now() - this.t0 };
     }
 }
 
-// a rendition segment through an encoder child; resolves to {file, bytes, encodeMs}
-function encodeSegment(bin, out, frames, w, h, fmt, fps, job, settings) {
-    let enc = null;
+// one rendition segment through an encoder child; resolves to {file, bytes, encodeMs}
+async function encodeSegment(bin, out, frames, w, h, fmt, fps, job, settings) {
+    return (await encodeRenditions(bin, [{ out: out, frames: frames, w: w, h: h, fmt: fmt, fps: fps, job: job,
+                                           settings: settings }]))[0];
+}
+
+// Every rendition segment of a launch through its own encoder child: all children are started
+// first, then each is fed by its own loop (the loops interleave on the event loop, each
+// paced by its child's pipe).  items: [{out, frames, w, h, fmt, fps, job, settings}];
+// resolves to [{file, bytes, encodeMs}] in item order, or rejects with the first failure
+// once every child has ended (the others are killed).
+async function encodeRenditions(bin, items) {
+    const encs = [];
     try {
-        enc = new FfmpegEncoder(bin, out, w, h, fps, fmt, job, settings);
-        frames.forEach(function (f) { enc.write(f); });
-    } catch (e) {                              // e.g. EPIPE: the child is gone
-        enc = enc || e.encoder || null;
-        if (!enc) return Promise.reject(new Error("ffmpeg encode of " + out + ": " + e.message));
-        enc.child.kill("SIGKILL");
-        enc._closeFd();
-        return enc.exited.then(function () {
-            throw new Error("ffmpeg encode of " + out + ": " + e.message + " " + enc.stderr());
-        });
+        items.forEach(function (it) { encs.push(new FfmpegEncoder(bin, it.out, it.w, it.h, it.fps, it.fmt, it.job, it.settings)); });
+    } catch (e) {
+        encs.forEach(function (en) { en.kill(); });
+        throw new Error("ffmpeg encode: " + e.message);
     }
-    return enc.close();
+    const runs = encs.map(async function (en, k) {
+        try {
+            const fr = items[k].frames;
+            for (let i = 0; i < fr.length; ++i) await en.write(fr[i]);
+        } catch (e) { /* a dead child: close() reports it with its exit status */ }
+        return en.close();
+    });
+    const res = await Promise.all(runs.map(function (p) {
+        return p.then(function (r) { return { ok: r }; }, function (e) { return { err: e }; });
+    }));
+    const bad = res.find(function (r) { return r.err; });
+    if (bad) {
+        encs.forEach(function (en) { en.kill(); });
+        throw bad.err;
+    }
+    return res.map(function (r) { return r.ok; });
 }
 
 // a job's encoded segments (chunkOffset order) -> one file, stream-copied by ffmpeg's
-// concat demuxer (the container is rewritten; the bitstreams are not re-encoded)
-function concatSegments(bin, files, out) {
+// concat demuxer (the container is rewritten; the bitstreams are not re-encoded); resolves
+// to the output path
+async function concatSegments(bin, files, out) {
     const list = out + ".txt";
     fs.writeFileSync(list, files.map(function (f) { return "file '" + path.resolve(f).replace(/'/g, "'\\''") + "'\n"; }).join(""));
-    const r = cp.spawnSync(bin, ["-v", "error", "-nostdin", "-f", "concat", "-safe", "0", "-i", list, "-c", "copy", "-y", out],
+    const child = cp.spawn(bin, ["-v", "error", "-nostdin", "-f", "concat", "-safe", "0", "-i", list, "-c", "copy", "-y", out],
                            { stdio: ["ignore", "ignore", "pipe"] });
+    const err = collect(child);
+    const st = await exitOf(child);
     fs.unlinkSync(list);
-    if (r.status !== 0) throw new Error("ffmpeg concat of " + out + " failed: " + String(r.stderr || r.error || r.status));
+    if (st.code !== 0) throw new Error("ffmpeg concat of " + out + " failed (" + (st.error || st.signal || st.code) + "): " + err());
     return out;
 }
 
 module.exports = { CODECS: CODECS, ffmpegBinary: ffmpegBinary, codecOf: codecOf, encodeArgs: encodeArgs,
                    FfmpegDecoder: FfmpegDecoder, FfmpegEncoder: FfmpegEncoder, encodeSegment: encodeSegment,
-                   concatSegments: concatSegments };
+                   encodeRenditions: encodeRenditions, concatSegments: concatSegments };

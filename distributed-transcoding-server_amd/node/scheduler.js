@@ -36,7 +36,9 @@
 //     field `quality`, from the summed records: vf_psnr / vf_ssim end of stream).
 //
 // The addon's run() executes on the libuv thread pool: set UV_THREADPOOL_SIZE
-// >= the GPU count before the first async call (worker.js does).
+// >= the GPU count before the first async call (worker.js does).  Source reads, encoder
+// feeds and segment writes are asynchronous too (y4m.js / ffpipe.js): while one slot's
+// segment is decoding or encoding, the event loop completes and starts the other slots'.
 // Node 12: no `??` / `?.`.
 
 const crypto = require("crypto");
@@ -83,22 +85,25 @@ function synthSource(addon, seed) {
     };
 }
 
-// Y4M source (a file read at random, or a pipe read in order: y4m.js Y4MReader).  Each
-// index is read once per request (vf_fps may repeat a frame); a stream reader keeps the
-// frames it has read until the scheduler releases them (release(sourceID, below)).
+// Y4M source (a file read at random: y4m.Y4MReader.readAsync, or a pipe read in order:
+// y4m.Y4MStream / an ffmpeg decoder child).  Each index is read once per request (vf_fps may
+// repeat a frame); a stream reader keeps the frames it has read until the scheduler
+// releases them (release(sourceID, below)).  Reads resolve asynchronously: the event loop
+// keeps serving the other GPU slots while a segment's frames arrive.
 function y4mSource(readers) {
-    const src = function (plan, frameIdx) {
+    const src = async function (plan, frameIdx) {
         const r = readers[plan.sourceID];
         if (!r) throw new Error("source " + plan.sourceID + " has no Y4M path");
         const got = new Map();
-        frameIdx.forEach(function (i) {
-            if (got.has(i) || i >= r.frames) return;
-            const f = r.read(i);
+        for (let k = 0; k < frameIdx.length; ++k) {
+            const i = frameIdx[k];
+            if (got.has(i) || i >= r.frames) continue;
+            const f = r.readAsync ? await r.readAsync(i) : await r.read(i);
             if (f) {
                 f.index = i;
                 got.set(i, f);
             }
-        });
+        }
         return frameIdx.filter(function (i) { return got.has(i); }).map(function (i) { return got.get(i); });
     };
     src.release = function (sourceID, below) {
@@ -252,27 +257,34 @@ class GpuSegmentScheduler extends EventEmitter {
             await this.sink(plan, task.rows, o.per);
         } else if (this.outDir) {
             const fps = plan.framerate ? ladder.rateOf(plan.framerate) : (plan.srcFps || [25, 1]);
-            const encs = [];
+            const ks = [], items = [];
             task.rows.forEach(function (row, k) {
                 if (!row) return;
-                if (self.encode) {                 // an ffmpeg child per rendition segment, all at once
-                    const job = plan.jobs[k];
-                    const p = self._segmentPath(row.mainJob, row.chunkOffset, ffpipe.codecOf(job).ext);
-                    fs.mkdirSync(path.dirname(p), { recursive: true });
-                    encs.push(ffpipe.encodeSegment(self.ffmpeg, p, o.per[k], outs[k].w, outs[k].h, outs[k].fmt, fps, job,
-                                                   ladder.parseSettings(job.codecSettings)).then(function (r) {
-                        files[k] = r.file;
-                        written[k] = r.bytes;
-                        encMs[k] = r.encodeMs;
-                    }));
-                    return;
-                }
-                const p = self._segmentPath(row.mainJob, row.chunkOffset);
+                const job = plan.jobs[k];
+                const p = self._segmentPath(row.mainJob, row.chunkOffset, self.encode ? ffpipe.codecOf(job).ext : "y4m");
                 fs.mkdirSync(path.dirname(p), { recursive: true });
-                written[k] = y4m.writeSegment(p, o.per[k], outs[k].w, outs[k].h, outs[k].fmt, fps);
-                files[k] = p;
+                ks.push(k);
+                items.push({ out: p, frames: o.per[k], w: outs[k].w, h: outs[k].h, fmt: outs[k].fmt, fps: fps, job: job,
+                             settings: ladder.parseSettings(job.codecSettings) });
             });
-            await Promise.all(encs);
+            if (this.encode) {
+                // an ffmpeg child per rendition segment, all started before the first frame and
+                // fed concurrently (ffpipe.encodeRenditions); the event loop stays free meanwhile
+                const rs = await ffpipe.encodeRenditions(this.ffmpeg, items);
+                rs.forEach(function (r, i) {
+                    files[ks[i]] = r.file;
+                    written[ks[i]] = r.bytes;
+                    encMs[ks[i]] = r.encodeMs;
+                });
+            } else {
+                const ns = await Promise.all(items.map(function (it) {
+                    return y4m.writeSegment(it.out, it.frames, it.w, it.h, it.fmt, it.fps);
+                }));
+                ns.forEach(function (n, i) {
+                    files[ks[i]] = items[i].out;
+                    written[ks[i]] = n;
+                });
+            }
         }
         const t4 = Date.now();
         return task.rows.map(function (row, k) {
@@ -322,11 +334,12 @@ class GpuSegmentScheduler extends EventEmitter {
     // every chunk of a job done -> the job's quality (every segment's summed record,
     // combined as vf_psnr / vf_ssim average a whole stream) and, with outDir, its
     // segments assembled into 1 MiB blocks of one Y4M stream
-    _assembleJobs(jobs, chunks) {
+    async _assembleJobs(jobs, chunks) {
         const self = this;
-        jobs.forEach(function (job) {
+        for (let ji = 0; ji < jobs.length; ++ji) {
+            const job = jobs[ji];
             const mine = self._completeJob(job, chunks);
-            if (!mine) return;
+            if (!mine) continue;
             try {
                 const fields = {};
                 const recs = mine.map(function (c) {
@@ -347,21 +360,21 @@ class GpuSegmentScheduler extends EventEmitter {
                     const ext = self.encode ? ffpipe.codecOf(job).ext : "y4m";
                     const files = mine.map(function (c, i) { return recs[i].file || self._segmentPath(job.id, c.chunkOffset, ext); });
                     const a = self.encode
-                        ? assemble.assembleFiles([ffpipe.concatSegments(self.ffmpeg, files,
-                                                                        path.join(self.outDir, "job" + job.id, "output." + ext))],
+                        ? assemble.assembleFiles([await ffpipe.concatSegments(self.ffmpeg, files,
+                                                                              path.join(self.outDir, "job" + job.id, "output." + ext))],
                                                  path.join(self.outDir, "blocks"))
                         : assemble.assembleY4M(files, path.join(self.outDir, "blocks"));
                     fields.assembledData = JSON.stringify(a);
                     fields.finished = true;
                 }
-                if (!Object.keys(fields).length) return;
+                if (!Object.keys(fields).length) continue;
                 Object.keys(fields).forEach(function (k) { job[k] = fields[k]; });
                 self.onJobUpdate(job, fields);
                 self.emit("jobUpdate", job, fields);
             } catch (e) {
                 self.emit("updateError", e, job, null);
             }
-        });
+        }
     }
 
     // a stream source keeps frames until no pending segment can ask for them again
@@ -386,27 +399,34 @@ class GpuSegmentScheduler extends EventEmitter {
     // jobs: Jobs rows of one or more ladders; chunks: their JobChunks rows;
     // sources: {sourceID: {w, h, fmt, fps: [num, den]}}.  Resolves to a summary
     // once every chunk is "done" or "failed".
-    runJobs(jobs, chunks, sources) {
-        const self = this;
-        if (this.outDir && !this.sink) {          // Y4M sources: stream geometry / rate from the file header
-            const self = this;
-            Object.keys(sources).forEach(function (sid) {
-                const s = sources[sid];
-                if (!s.path || self.readers[sid]) return;
-                // a compressed source (decode: "ffmpeg", or a regular file that is not YUV4MPEG2):
-                // an ffmpeg child decodes it to a pipe; pipes / FIFOs / stdin are read as Y4M
-                const viaFfmpeg = s.decode === "ffmpeg" || (s.decode === undefined && !isY4MFile(s.path));
-                if (viaFfmpeg && !self.ffmpeg) throw new Error("source " + sid + ": " + s.path + " needs an ffmpeg binary to decode");
-                const r = viaFfmpeg ? new ffpipe.FfmpegDecoder(self.ffmpeg, s.path, { fmt: s.fmt })
-                                    : new y4m.Y4MReader(s.path);
-                self.readers[sid] = r;
-                s.w = s.w || r.hdr.w;
-                s.h = s.h || r.hdr.h;
-                s.fmt = s.fmt === undefined ? r.hdr.fmt : s.fmt;
-                s.fps = s.fps || r.hdr.fps;
-            });
-            if (Object.keys(this.readers).length && !this._userSource) this.source = y4mSource(this.readers);
+    async runJobs(jobs, chunks, sources) {
+        if (this.outDir && !this.sink) await this._openSources(sources);
+        return this._schedule(jobs, chunks, sources);
+    }
+
+    // Y4M / compressed sources: stream geometry and rate from the stream header.  A compressed
+    // source (decode: "ffmpeg", or a regular file that is not YUV4MPEG2) is decoded by an ffmpeg
+    // child into a pipe; pipes / FIFOs / stdin are read as Y4M streams, regular Y4M files at
+    // random.  Opening waits for the header without blocking the event loop.
+    async _openSources(sources) {
+        const sids = Object.keys(sources);
+        for (let i = 0; i < sids.length; ++i) {
+            const sid = sids[i], s = sources[sid];
+            if (!s.path || this.readers[sid]) continue;
+            const viaFfmpeg = s.decode === "ffmpeg" || (s.decode === undefined && !isY4MFile(s.path));
+            if (viaFfmpeg && !this.ffmpeg) throw new Error("source " + sid + ": " + s.path + " needs an ffmpeg binary to decode");
+            const r = viaFfmpeg ? await ffpipe.FfmpegDecoder.open(this.ffmpeg, s.path, { fmt: s.fmt }) : await y4m.open(s.path);
+            this.readers[sid] = r;
+            s.w = s.w || r.hdr.w;
+            s.h = s.h || r.hdr.h;
+            s.fmt = s.fmt === undefined ? r.hdr.fmt : s.fmt;
+            s.fps = s.fps || r.hdr.fps;
         }
+        if (Object.keys(this.readers).length && !this._userSource) this.source = y4mSource(this.readers);
+    }
+
+    _schedule(jobs, chunks, sources) {
+        const self = this;
         const plans = ladder.planLadders(jobs, sources);
         const queue = [];
         plans.forEach(function (plan, pi) {
@@ -440,9 +460,12 @@ class GpuSegmentScheduler extends EventEmitter {
         const inflight = [];
         return new Promise(function (resolve) {
             function finish() {
-                self._assembleJobs(jobs, chunks);
-                self._closeReaders();
-                resolve(self._summary(total));
+                self._assembleJobs(jobs, chunks).catch(function (e) {
+                    self.emit("updateError", e, null, null);
+                }).then(function () {
+                    self._closeReaders();
+                    resolve(self._summary(total));
+                });
             }
             if (!total) return finish();
             function pull(slot) {

@@ -11,11 +11,19 @@
 // yuv4mpegpipe -` into a pipe is a source, `... | ffmpeg -f yuv4mpegpipe -i - -c:v
 // libx264 out.mp4` a sink.
 //
-// Sources are read either at random (a regular file: frame i at a fixed offset) or in
-// order (a pipe / FIFO / stdin: frames are read forward as segments ask for them and
-// kept until the scheduler releases them).  10-bit sources become p010 host frames (the layout libdts
-// takes: value << 6 in 16-bit words, U / V interleaved); p010 renditions are written
-// back as C420p10.
+// Sources are read either at random (a regular file: frame i at a fixed offset; Y4MReader)
+// or in order (a pipe / FIFO / stdin / a decoder child's stdout: Y4MStream, frames read
+// forward as segments ask for them and kept until the scheduler releases them).  10-bit
+// sources become p010 host frames (the layout libdts takes: value << 6 in 16-bit words,
+// U / V interleaved); p010 renditions are written back as C420p10.
+//
+// Nothing here blocks the event loop on a pipe: a stream is read through a paused Node
+// Readable (libuv polls the descriptor; the reader pulls only as many bytes as the frames
+// asked for, so the producer is held back by the pipe itself), and sinks (Y4MSink: an
+// encoder child's stdin, a segment file) are Writables awaited on 'drain'.  One Node
+// process drives every GPU slot of a node (SURVEY.md §8b "Threading"), so a decode or an
+// encode must never stall the other slots.  Y4MReader / Y4MWriter keep synchronous calls
+// for regular files only (fixtures, tests, random access).
 //
 // Node 12: no `??` / `?.`.
 
@@ -64,77 +72,87 @@ function parseHeader(line) {
     return h;
 }
 
-// A non-blocking descriptor (a child process's pipe, stdin after the parent set
-// O_NONBLOCK) answers EAGAIN while the producer has nothing yet: wait a millisecond and try
-// again (ADVICE r03), up to `EAGAIN_MS` in all, then fail clearly.
-const EAGAIN_MS = 600000;
-const SLEEP = new Int32Array(new SharedArrayBuffer(4));
-function retryAgain(fn) {
-    for (let waited = 0;; ++waited) {
-        try {
-            return fn();
-        } catch (e) {
-            if (e.code !== "EAGAIN" || waited >= EAGAIN_MS) throw e;
-            Atomics.wait(SLEEP, 0, 0, 1);
+const readP = require("util").promisify(fs.read);
+
+// Bytes of a Readable in paused mode: chunks are pulled with read() only when the parser
+// needs more, and a pull with nothing buffered waits for 'readable' / 'end' / 'error' --
+// a Promise, never a loop on the event loop's thread.
+class ByteQueue {
+    constructor(rs) {
+        this.rs = rs;
+        this.bufs = [];
+        this.have = 0;
+        this.ended = false;
+        this.err = null;
+        this.wake = null;
+        const self = this;
+        rs.on("readable", function () { self._wake(); });
+        rs.on("end", function () { self.ended = true; self._wake(); });
+        rs.on("close", function () { self.ended = true; self._wake(); });
+        rs.on("error", function (e) { self.err = self.err || e; self._wake(); });
+    }
+    _wake() {
+        const w = this.wake;
+        this.wake = null;
+        if (w) w();
+    }
+    // one more chunk into the queue; false at the end of the stream
+    async _more() {
+        for (;;) {
+            if (this.err) throw this.err;
+            const c = this.rs.read();
+            if (c !== null) {
+                this.bufs.push(c);
+                this.have += c.length;
+                return true;
+            }
+            if (this.ended) return false;
+            const self = this;
+            await new Promise(function (res) { self.wake = res; });
         }
     }
-}
-
-function readSync(fd, buf, off, len, pos) {
-    return retryAgain(function () { return fs.readSync(fd, buf, off, len, pos); });
-}
-
-// Buffered in-order reads of a stream (pipe / FIFO / stdin): header and FRAME lines are
-// parsed from 1 MiB reads instead of one read per byte (ADVICE r03); frame payloads copy
-// what is buffered and read the rest straight into the record.
-class StreamIn {
-    constructor(fd) {
-        this.fd = fd;
-        this.buf = Buffer.alloc(1 << 20);
-        this.start = 0;
-        this.end = 0;
-        this.eof = false;
-    }
-    _fill() {
-        if (this.eof) return 0;
-        if (this.start === this.end) {
-            this.start = this.end = 0;
-        } else if (this.end === this.buf.length) {
-            this.buf.copy(this.buf, 0, this.start, this.end);
-            this.end -= this.start;
-            this.start = 0;
+    _consume(n) {
+        this.have -= n;
+        while (n > 0) {
+            const b = this.bufs[0];
+            if (b.length <= n) {
+                this.bufs.shift();
+                n -= b.length;
+            } else {
+                this.bufs[0] = b.subarray(n);
+                n = 0;
+            }
         }
-        const n = readSync(this.fd, this.buf, this.end, this.buf.length - this.end, null);
-        if (n <= 0) this.eof = true;
-        else this.end += n;
-        return Math.max(n, 0);
     }
     // {line, bytes} up to and without "\n", or null at the end of the stream
-    line(limit) {
+    async line(limit) {
+        let scanned = 0;
         for (;;) {
-            const nl = this.buf.indexOf(0x0a, this.start);
-            if (nl >= 0 && nl < this.end) {
-                const r = { line: this.buf.toString("latin1", this.start, nl), bytes: nl + 1 - this.start };
-                this.start = nl + 1;
+            if (this.bufs.length > 1) this.bufs = [Buffer.concat(this.bufs, this.have)];
+            const b = this.bufs[0];
+            const nl = b ? b.indexOf(0x0a, scanned) : -1;
+            if (nl >= 0) {
+                const r = { line: b.toString("latin1", 0, nl), bytes: nl + 1 };
+                this._consume(nl + 1);
                 return r;
             }
-            if (this.end - this.start > limit) throw new Error("y4m: header line longer than " + limit + " bytes");
-            if (!this._fill()) {
-                if (this.start === this.end) return null;
+            scanned = this.have;
+            if (this.have > limit) throw new Error("y4m: header line longer than " + limit + " bytes");
+            if (!(await this._more())) {
+                if (!this.have) return null;
                 throw new Error("y4m: stream ends inside a header line");
             }
         }
     }
-    // fill dst; returns the bytes read (short at the end of the stream)
-    read(dst) {
-        const have = Math.min(this.end - this.start, dst.length);
-        this.buf.copy(dst, 0, this.start, this.start + have);
-        this.start += have;
-        let off = have;
-        while (off < dst.length && !this.eof) {
-            const n = readSync(this.fd, dst, off, dst.length - off, null);
-            if (n <= 0) this.eof = true;
-            else off += n;
+    // fill dst; resolves to the bytes read (short at the end of the stream)
+    async read(dst) {
+        let off = 0;
+        while (off < dst.length) {
+            if (!this.have && !(await this._more())) break;
+            const b = this.bufs[0], n = Math.min(b.length, dst.length - off);
+            b.copy(dst, off, 0, n);
+            this._consume(n);
+            off += n;
         }
         return off;
     }
@@ -146,7 +164,7 @@ function readLine(fd, pos, limit) {
     const one = Buffer.alloc(1), out = [];
     let n = 0;
     for (;;) {
-        const got = readSync(fd, one, 0, 1, pos + n);
+        const got = fs.readSync(fd, one, 0, 1, pos + n);
         if (got <= 0) {
             if (n === 0) return null;
             throw new Error("y4m: stream ends inside a header line");
@@ -159,11 +177,11 @@ function readLine(fd, pos, limit) {
     return { line: Buffer.from(out).toString("latin1"), bytes: n };
 }
 
-// fill buf from fd (a stream may return short reads); returns the bytes read
+// fill buf from a regular file at pos; returns the bytes read
 function readFull(fd, buf, pos) {
     let off = 0;
     while (off < buf.length) {
-        const n = readSync(fd, buf, off, buf.length - off, pos === null ? null : pos + off);
+        const n = fs.readSync(fd, buf, off, buf.length - off, pos + off);
         if (n <= 0) break;
         off += n;
     }
@@ -189,75 +207,145 @@ function recordToFrame(rec, w, h, bits) {
     return { data: [y, uv, null], pitch: [2 * w, 4 * cw, 0] };
 }
 
+// Random access to a Y4M regular file: frame i at a fixed offset.  read(i) is synchronous
+// (fixtures, tests); readAsync(i) is what the worker uses (the reads run on the libuv pool).
 class Y4MReader {
-    // src: a path ("-" = stdin) or an open file descriptor
+    // src: the path of a regular file (pipes, FIFOs and stdin: y4m.open -> Y4MStream)
     constructor(src) {
-        this.path = typeof src === "string" ? src : null;
-        this.fd = typeof src === "number" ? src : (src === "-" ? 0 : fs.openSync(src, "r"));
-        this.ownFd = typeof src === "string" && src !== "-";
+        this.path = src;
+        if (!fs.statSync(src).isFile())             // (opening a FIFO would wait for its writer)
+            throw new Error("y4m: " + src + " is not a regular file (read pipes through y4m.open)");
+        this.fd = fs.openSync(src, "r");
         const st = fs.fstatSync(this.fd);
-        this.seekable = st.isFile();
-        if (!this.seekable) this.sin = new StreamIn(this.fd);
-        const hl = this.seekable ? readLine(this.fd, 0, MAX_HEADER) : this.sin.line(MAX_HEADER);
+        this.seekable = true;
+        const hl = readLine(this.fd, 0, MAX_HEADER);
         if (!hl) throw new Error("y4m: empty stream");
         this.hdr = parseHeader(hl.line);
         this.hdr.headerBytes = hl.bytes;
         this.bps = this.hdr.bits > 8 ? 2 : 1;
         this.frameBytes = frameBytes(this.hdr.w, this.hdr.h, this.bps);
-        if (this.seekable) {
-            this.stride = 6 + this.frameBytes;             // "FRAME\n" + planes (no frame parameters)
-            this.frames = Math.floor((st.size - hl.bytes) / this.stride);
-        } else {
-            this.frames = Infinity;                        // known at the end of the stream
-            this.next = 0;                                 // index of the next record in the stream
-            this.kept = new Map();                         // frames read, not yet released
-        }
+        this.stride = 6 + this.frameBytes;                 // "FRAME\n" + planes (no frame parameters)
+        this.frames = Math.floor((st.size - hl.bytes) / this.stride);
     }
 
-    // frame i as a host frame for the addon, or null past the end of the stream.  A
-    // stream keeps every frame it has read until release() drops it (segments are
-    // requested roughly in order, so at most a few segments are held; a frame may be
-    // asked for twice: vf_fps repeats, yadif context frames, two ladders of one source).
+    // frame i as a host frame for the addon, or null past the end of the file
     read(i) {
         if (i < 0) throw new Error("y4m: frame " + i);
-        if (this.seekable) {
-            if (i >= this.frames) return null;
-            const off = this.hdr.headerBytes + i * this.stride;
-            const tag = Buffer.alloc(6);
-            readFull(this.fd, tag, off);
-            if (tag.toString("latin1") !== "FRAME\n")
-                throw new Error("y4m: frame " + i + ": FRAME parameters need a stream (pipe) reader");
-            const rec = Buffer.alloc(this.frameBytes);
-            if (readFull(this.fd, rec, off + 6) !== rec.length) throw new Error("y4m: frame " + i + " is truncated");
-            return recordToFrame(rec, this.hdr.w, this.hdr.h, this.hdr.bits);
+        if (i >= this.frames) return null;
+        const off = this.hdr.headerBytes + i * this.stride;
+        const rec = Buffer.alloc(this.stride);
+        if (readFull(this.fd, rec, off) !== rec.length) throw new Error("y4m: frame " + i + " is truncated");
+        return this._frame(i, rec);
+    }
+
+    async readAsync(i) {
+        if (i < 0) throw new Error("y4m: frame " + i);
+        if (i >= this.frames) return null;
+        const off = this.hdr.headerBytes + i * this.stride;
+        const rec = Buffer.alloc(this.stride);
+        let got = 0;
+        while (got < rec.length) {
+            const r = await readP(this.fd, rec, got, rec.length - got, off + got);
+            if (r.bytesRead <= 0) break;
+            got += r.bytesRead;
         }
+        if (got !== rec.length) throw new Error("y4m: frame " + i + " is truncated");
+        return this._frame(i, rec);
+    }
+
+    _frame(i, rec) {
+        if (rec.toString("latin1", 0, 6) !== "FRAME\n")
+            throw new Error("y4m: frame " + i + ": FRAME parameters need a stream (pipe) reader");
+        return recordToFrame(rec.subarray(6), this.hdr.w, this.hdr.h, this.hdr.bits);
+    }
+
+    release() {}
+
+    close() {
+        if (this.fd !== null) fs.closeSync(this.fd);
+        this.fd = null;
+    }
+}
+
+// In-order reads of a Y4M byte stream (a Readable: a decoder child's stdout, a FIFO, stdin).
+// open() resolves once the header is parsed; read(i) resolves to frame i (or null past the
+// end).  Calls are served one after another in call order (two GPU slots may ask at once);
+// every frame read is kept until release() drops it (segments are requested roughly in
+// order, so at most a few segments are held; a frame may be asked for twice: vf_fps
+// repeats, yadif context frames, two ladders of one source).
+class Y4MStream {
+    static async open(rs) {
+        const q = new ByteQueue(rs);
+        const hl = await q.line(MAX_HEADER);
+        if (!hl) throw new Error("y4m: empty stream");
+        return new Y4MStream(rs, q, hl);
+    }
+    constructor(rs, q, hl) {
+        this.rs = rs;
+        this.q = q;
+        this.seekable = false;
+        this.hdr = parseHeader(hl.line);
+        this.hdr.headerBytes = hl.bytes;
+        this.bps = this.hdr.bits > 8 ? 2 : 1;
+        this.frameBytes = frameBytes(this.hdr.w, this.hdr.h, this.bps);
+        this.frames = Infinity;                            // known at the end of the stream
+        this.next = 0;                                     // index of the next record in the stream
+        this.kept = new Map();                             // frames read, not yet released
+        this.chain = Promise.resolve();
+    }
+
+    read(i) {
+        const self = this;
+        const p = this.chain.then(function () { return self._read(i); });
+        this.chain = p.catch(function () {});
+        return p;
+    }
+
+    async _read(i) {
+        if (i < 0) throw new Error("y4m: frame " + i);
         if (this.kept.has(i)) return this.kept.get(i);
         if (i < this.next) throw new Error("y4m: frame " + i + " of a stream was already released");
         while (this.next <= i) {
-            const tl = this.sin.line(MAX_HEADER);
+            if (this.next >= this.frames) return null;
+            const tl = await this.q.line(MAX_HEADER);
             if (!tl) {
                 this.frames = this.next;
                 return null;
             }
             if (tl.line.slice(0, 5) !== "FRAME") throw new Error("y4m: record " + this.next + " is not a FRAME");
             const rec = Buffer.alloc(this.frameBytes);
-            if (this.sin.read(rec) !== rec.length) throw new Error("y4m: frame " + this.next + " is truncated");
+            if ((await this.q.read(rec)) !== rec.length) throw new Error("y4m: frame " + this.next + " is truncated");
             this.kept.set(this.next++, recordToFrame(rec, this.hdr.w, this.hdr.h, this.hdr.bits));
         }
         return this.kept.get(i);
     }
 
-    // a stream forgets the frames below `below` (no pending segment asks for them again)
+    // forget the frames below `below` (no pending segment asks for them again)
     release(below) {
-        if (!this.kept) return;
         const self = this;
         Array.from(this.kept.keys()).forEach(function (k) { if (k < below) self.kept.delete(k); });
     }
 
     close() {
-        if (this.fd !== null && this.ownFd) fs.closeSync(this.fd);
-        this.fd = null;
-        if (this.kept) this.kept.clear();
+        this.kept.clear();
+        if (this.rs && this.rs !== process.stdin) this.rs.destroy();
+        this.rs = null;
+    }
+}
+
+// A source by path: a regular file -> Y4MReader (random access); "-" -> stdin, any other
+// path (a FIFO, a device) -> opened on the libuv pool (a FIFO's open waits for its writer
+// there, not on the event loop) and polled as a pipe -> Y4MStream.
+async function open(src) {
+    if (src === "-") return Y4MStream.open(process.stdin);
+    if (fs.statSync(src).isFile()) return new Y4MReader(src);
+    const fd = await require("util").promisify(fs.open)(src, "r");
+    const sock = new (require("net").Socket)({ fd: fd, readable: true, writable: false });
+    try {
+        return await Y4MStream.open(sock);
+    } catch (e) {
+        sock.destroy();
+        throw e;
     }
 }
 
@@ -308,13 +396,11 @@ function frameRecord(f, w, h, fmt) {
     return out;
 }
 
-// A streaming sink: the header, then one record per frame written as it comes (a
-// segment of any size never sits in memory as one Buffer; ADVICE r02)
+// A synchronous writer of a regular file (fixtures, tests): the header, then one record
+// per frame as it comes (a segment of any size never sits in memory as one Buffer)
 class Y4MWriter {
-    // dst: a path or an open file descriptor (e.g. a pipe into an encoder)
-    constructor(dst, w, h, fps, fmt) {
-        this.fd = typeof dst === "number" ? dst : fs.openSync(dst, "w");
-        this.ownFd = typeof dst !== "number";
+    constructor(path, w, h, fps, fmt) {
+        this.fd = fs.openSync(path, "w");
         this.w = w;
         this.h = h;
         this.fmt = fmt;
@@ -325,11 +411,7 @@ class Y4MWriter {
 
     _put(buf) {
         let off = 0;
-        const fd = this.fd;
-        while (off < buf.length) {
-            const o = off;
-            off += retryAgain(function () { return fs.writeSync(fd, buf, o, buf.length - o); });
-        }
+        while (off < buf.length) off += fs.writeSync(this.fd, buf, off, buf.length - off);
         this.bytes += buf.length;
     }
 
@@ -339,21 +421,81 @@ class Y4MWriter {
     }
 
     close() {
-        if (this.fd !== null && this.ownFd) fs.closeSync(this.fd);
+        if (this.fd !== null) fs.closeSync(this.fd);
         this.fd = null;
         return this.bytes;
     }
 }
 
-// write a whole rendition segment, frame by frame; returns the bytes written
-function writeSegment(path, frames, w, h, fmt, fps) {
-    const wr = new Y4MWriter(path, w, h, fps, fmt);
-    try {
-        frames.forEach(function (f) { wr.write(f); });
-    } finally {
-        wr.close();
+// The worker's sink: Y4M records into a Writable (an encoder child's stdin, a file stream).
+// write(frame) resolves once the Writable takes more (its 'drain'), so at most one record
+// per sink waits in memory and a slow consumer holds back only its own writer; a failed
+// Writable (EPIPE: the encoder died) rejects the pending and every later write.
+class Y4MSink {
+    constructor(ws, w, h, fps, fmt) {
+        this.ws = ws;
+        this.w = w;
+        this.h = h;
+        this.fmt = fmt;
+        this.bytes = 0;
+        this.frames = 0;
+        this.err = null;
+        this.waiters = [];
+        const self = this;
+        ws.on("error", function (e) {
+            self.err = self.err || e;
+            self._wake();
+        });
+        ws.on("drain", function () { self._wake(); });
+        this.pending = this._put(header(w, h, fps, fmt));
     }
-    return wr.bytes;
+    _wake() {
+        const ws = this.waiters;
+        this.waiters = [];
+        ws.forEach(function (f) { f(); });
+    }
+    async _put(buf) {
+        if (this.err) throw this.err;
+        this.bytes += buf.length;
+        if (this.ws.write(buf)) return;
+        const self = this;
+        await new Promise(function (res) { self.waiters.push(res); });
+        if (this.err) throw this.err;
+    }
+    async write(frame) {
+        await this.pending;
+        this.pending = this._put(frameRecord(frame, this.w, this.h, this.fmt));
+        ++this.frames;
+        return this.pending;
+    }
+    // resolves with the bytes written once the Writable has flushed them ('finish')
+    async end() {
+        await this.pending;
+        if (this.err) throw this.err;
+        const self = this;
+        await new Promise(function (res, rej) {
+            if (self.err) return rej(self.err);
+            self.waiters.push(function () { if (self.err) rej(self.err); });
+            self.ws.end(function () { res(); });
+        });
+        return this.bytes;
+    }
+}
+
+// a rendition segment as a Y4M file, written through a file stream (the libuv pool); resolves
+// to the bytes written
+async function writeSegment(path, frames, w, h, fmt, fps) {
+    const ws = fs.createWriteStream(path);
+    const sink = new Y4MSink(ws, w, h, fps, fmt);
+    try {
+        for (let i = 0; i < frames.length; ++i) await sink.write(frames[i]);
+        const n = await sink.end();
+        await new Promise(function (res) { if (ws.closed || ws.destroyed) res(); else ws.once("close", res); });
+        return n;
+    } catch (e) {
+        ws.destroy();
+        throw e;
+    }
 }
 
 // a complete 8-bit Y4M file from frames made by gen(i) (tests, fixtures)
@@ -376,7 +518,8 @@ function headerBytes(path) {
     }
 }
 
-module.exports = { Y4MReader: Y4MReader, Y4MWriter: Y4MWriter, parseHeader: parseHeader, frameBytes: frameBytes,
+module.exports = { Y4MReader: Y4MReader, Y4MStream: Y4MStream, Y4MWriter: Y4MWriter, Y4MSink: Y4MSink, open: open,
+                   parseHeader: parseHeader, frameBytes: frameBytes,
                    header: header, frameRecord: frameRecord, writeSegment: writeSegment, writeFile: writeFile,
                    headerBytes: headerBytes, recordToFrame: recordToFrame,
                    FMT_YUV420P: FMT_YUV420P, FMT_NV12: FMT_NV12, FMT_P010LE: FMT_P010LE };

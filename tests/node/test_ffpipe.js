@@ -30,11 +30,11 @@ y4m.writeFile(src, w, h, [30, 1], n, gen);
     assert.deepStrictEqual(ffpipe.encodeArgs({ codec: "h264", bitrate: 3000000 }, { encoderArgs: ["-preset", "fast"] }),
                            ["-c:v", "libx264", "-b:v", "3000000", "-preset", "fast"]);
     // decode: frames in order from the child's pipe
-    const dec = new ffpipe.FfmpegDecoder(stub, src, { fmt: 0 });
+    const dec = await ffpipe.FfmpegDecoder.open(stub, src, { fmt: 0 });
     assert.strictEqual(dec.hdr.w, w);
     const frames = [];
     for (let i = 0; ; ++i) {
-        const f = dec.read(i);
+        const f = await dec.read(i);
         if (!f) break;
         assert.strictEqual(f.data[0][0], i);
         assert.strictEqual(f.data[0][3], 7 * i);
@@ -64,7 +64,7 @@ y4m.writeFile(src, w, h, [30, 1], n, gen);
         assert.ok(body.slice(nl + 1).equals(expect), "segment " + s + " carries the Y4M records");
         segs.push(out);
     }
-    const all = ffpipe.concatSegments(stub, segs, path.join(dir, "output.mp4"));
+    const all = await ffpipe.concatSegments(stub, segs, path.join(dir, "output.mp4"));
     assert.ok(fs.readFileSync(all).equals(Buffer.concat(segs.map(function (f) { return fs.readFileSync(f); }))));
     // a failing encoder is an error, not a hang
     await ffpipe.encodeSegment("/bin/false", path.join(dir, "x.mp4"), frames.slice(0, 1), w, h, 0, [30, 1],

@@ -352,7 +352,7 @@ async function testDeinterlaceWithRateChange() {
     }, /frame-rate modes/);
 }
 
-function testY4M10BitAndHeaders() {
+async function testY4M10BitAndHeaders() {
     // C420p10 <-> p010 host frames; a long header line; FRAME parameters on a stream
     const d = tmpdir(), p = path.join(d, "p10.y4m");
     const w = 6, h = 4, cw = 3, ch = 2;
@@ -388,16 +388,17 @@ function testY4M10BitAndHeaders() {
     const fifo = path.join(d, "long.fifo");
     require("child_process").execFileSync("mkfifo", [fifo]);
     const feeder = require("child_process").spawn("sh", ["-c", "cat \"$0\" > \"$1\"", q, fifo]);
-    const st = new y4m.Y4MReader(fifo);
+    const st = await y4m.open(fifo);
     assert.strictEqual(st.seekable, false);
     assert.strictEqual(st.hdr.headerBytes, y4m.headerBytes(q));
-    assert.strictEqual(st.read(1).data[0][0], 9);
-    assert.strictEqual(st.read(0).data[2][0], 9);                 // kept until released
+    assert.strictEqual((await st.read(1)).data[0][0], 9);
+    assert.strictEqual((await st.read(0)).data[2][0], 9);         // kept until released
     st.release(2);
-    assert.throws(function () { st.read(0); }, /released/);
-    assert.strictEqual(st.read(2), null);
+    await assert.rejects(st.read(0), /released/);
+    assert.strictEqual(await st.read(2), null);
     assert.strictEqual(st.frames, 2);
     st.close();
+    assert.throws(function () { new y4m.Y4MReader(fifo); }, /not a regular file/);
     return new Promise(function (res) { feeder.on("exit", res); if (feeder.exitCode !== null) res(); });
 }
 
@@ -467,25 +468,83 @@ async function testFfmpegBoundary() {
     jobs.forEach(function (j) { assert.strictEqual(j.finished, true); });
 }
 
+async function testSlowEncodersKeepTheLoopFree() {
+    // SURVEY §8b "Threading": one Node process drives every GPU slot, so a slow encoder must
+    // not stall the event loop.  Two slots, three renditions per segment, a stub encoder that
+    // takes 40 ms per frame: each segment's three encoders consume in overlapping windows, the
+    // other slot's GPU runs start while an encode is in progress, an event-loop lag probe
+    // stays under 50 ms, and the whole run takes <= 0.6x the encoders' summed time.
+    const d = tmpdir(), times = path.join(d, "times.jsonl");
+    process.env.STUB_ENC_MS_PER_FRAME = "40";
+    process.env.STUB_TIMES = times;
+    // GPU 1's runs take longer, so the two slots' segments drift apart
+    const addon = fakeAddon({ devices: 2, delay: 5 });
+    const runs = [];
+    addon.run = (function (run) {
+        return function (g, src, dst, q) {
+            runs.push({ t: Date.now(), dev: g.ctx.dev });
+            const p = run(g, src, dst, q);
+            return g.ctx.dev ? p.then(function (r) {
+                return new Promise(function (res) { setTimeout(function () { res(r); }, 60); });
+            }) : p;
+        };
+    })(addon.run);
+    const js = jobSet(6);
+    js.jobs.forEach(function (j) { j.codec = "h264"; });
+    let last = Date.now(), lag = 0;
+    const lags = [];
+    const probe = setInterval(function () {
+        const now = Date.now();
+        lag = Math.max(lag, now - last - 5);
+        if (now - last - 5 > 20) lags.push([now - t0, now - last - 5]);
+        last = now;
+    }, 5);
+    const t0 = Date.now();
+    const s = new GpuSegmentScheduler({ addon: addon, workerId: 1, segmentFrames: 6, outDir: d, encode: true,
+                                        ffmpeg: path.join(__dirname, "ffmpeg_stub.js") });
+    await s.runJobs(js.jobs, js.chunks, js.sources);
+    const wall = Date.now() - t0;
+    clearInterval(probe);
+    delete process.env.STUB_ENC_MS_PER_FRAME;
+    delete process.env.STUB_TIMES;
+    const win = fs.readFileSync(times, "utf8").trim().split("\n").map(JSON.parse);
+    assert.strictEqual(win.length, 18);
+    const slotOf = {};
+    js.chunks.forEach(function (c) {
+        assert.strictEqual(c.status, "done", c.result);
+        const r = JSON.parse(c.result);
+        slotOf[r.file] = r.gpu;
+    });
+    for (let off = 0; off < 6; ++off) {                  // the renditions of a segment encode together
+        const w = win.filter(function (x) { return path.basename(x.out).split(".")[0] === String(off); });
+        assert.strictEqual(w.length, 3);
+        const start = Math.max.apply(null, w.map(function (x) { return x.t0; }));
+        const end = Math.min.apply(null, w.map(function (x) { return x.t1; }));
+        assert.ok(start < end, "segment " + off + " encoders ran one after another: " + JSON.stringify(w));
+    }
+    // the other slot starts a GPU run while an encode is in progress
+    const during = win.some(function (x) {
+        return runs.some(function (r) { return r.dev !== slotOf[x.out] && r.t > x.t0 && r.t < x.t1; });
+    });
+    assert.ok(during, "no GPU run started during any encode");
+    assert.ok(lag < 50, "event loop lag " + lag + " ms " + JSON.stringify(lags) + " wall " + wall);
+    const seq = win.reduce(function (a, x) { return a + (x.t1 - x.t0); }, 0);
+    assert.ok(wall <= 0.6 * seq, "wall " + wall + " ms vs sequential " + seq + " ms");
+}
+
 function testNoDevicesIsLoud() {
     assert.throws(function () { new GpuSegmentScheduler({ addon: fakeAddon({ devices: 0 }) }); }, /no CPU fallback/);
 }
 
 (async function () {
-    testLadderPlanning();
-    testNoDevicesIsLoud();
-    await testAllDoneAndBalanced();
-    await testRetryOnAnotherGpu();
-    await testGiveUpAfterRetries();
-    await testFpsMapAndResume();
-    await testThrowingUpdateDoesNotHang();
-    testY4MRoundTrip();
-    testAssembleBlocks();
-    testQualitySummary();
-    await testY4MJobAssembled();
-    await testDeinterlaceWithRateChange();
-    await testY4M10BitAndHeaders();
-    await testPipeSourceAndPartialJob();
-    await testFfmpegBoundary();
+    const tests = [testLadderPlanning, testNoDevicesIsLoud, testAllDoneAndBalanced, testRetryOnAnotherGpu,
+                   testGiveUpAfterRetries, testFpsMapAndResume, testThrowingUpdateDoesNotHang, testY4MRoundTrip,
+                   testAssembleBlocks, testQualitySummary, testY4MJobAssembled, testDeinterlaceWithRateChange,
+                   testY4M10BitAndHeaders, testPipeSourceAndPartialJob, testFfmpegBoundary,
+                   testSlowEncodersKeepTheLoopFree];
+    for (let i = 0; i < tests.length; ++i) {
+        if (process.env.TEST_VERBOSE) process.stderr.write(tests[i].name + "\n");
+        await tests[i]();
+    }
     process.stdout.write("node scheduler tests ok\n");
 })().catch(function (e) { process.stderr.write((e && e.stack || e) + "\n"); process.exit(1); });

@@ -3,7 +3,8 @@
 Each test drives dts_graph_run_device the way bench.py's step() does -- the same graph
 specs, device-resident batches laid out by bench.dev_batch, the same reference plumbing
 -- and checks every frame against the CPU oracle:
-- cfg2: the 4K -> 1080p/720p/480p nv12 ladder, two launches of three frames;
+- cfg2: the 4K -> 1080p/720p/480p nv12 ladder, two launches of three frames, and one
+  launch of 20 frames (frame quads 0-2 of k_ladder7's frame map on every XCD slot);
 - cfg3: 4K p010 HDR10 -> 1080p SDR on the device path with more frames than one
   ladder -> tonemap chunk (max_batch 4, 9 frames: three chunks, both p010
   intermediates reused), vf_tonemap defaults;
@@ -92,6 +93,39 @@ def test_cfg2_device_path_two_launches(ctx):
                 got = _frame(outs[k][0], f, w, h, fmt)
                 want = orc.scale_frame(src, sw, sh, D.FMT_YUV420P, w, h, fmt, m)
                 assert planes_equal(got, want), f"step {step} frame {f} out {k}: {first_diff(got, want)}"
+    g.close()
+
+
+def test_cfg2_device_path_full_frame_quads(ctx):
+    """The headline launch shape at 4K: one launch of 20 frames, so k_ladder7's frame map
+    (frame 8 fq + b % 8, ladder7.hip k_ladder7) reaches fq = 2 on all 8 XCD slots, the last
+    quad partly filled; every frame of every rendition against the oracle."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from bench import unpack_dev_frame
+    st = torch.cuda.current_stream().cuda_stream
+    sw, sh, n, first = 3840, 2160, 20, 1000
+    _s, sd = _ring(sw, sh, D.FMT_YUV420P, n)
+    ctx.synth_device(sw, sh, D.FMT_YUV420P, 0, 0x5EED, first, sd, n, st)
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, LADDER, max_batch=n))
+    assert g.info.ladder_v5 == 3, "cfg2 runs on k_ladder7"
+    outs = [_ring(w, h, fmt, n) for (w, h, fmt, _m) in LADDER]
+    g.run_device(sd, n, [d for (_t, d) in outs], stream=st)
+    torch.cuda.synchronize()
+    host = [t.cpu().numpy() for (t, _d) in outs]
+
+    def check(f):
+        src = D.synth_host(sw, sh, D.FMT_YUV420P, 0, 0x5EED, first + f)
+        bad = []
+        for k, (w, h, fmt, m) in enumerate(LADDER):
+            got = unpack_dev_frame(host[k][f], w, h, fmt)
+            want = orc.scale_frame(src, sw, sh, D.FMT_YUV420P, w, h, fmt, m)
+            if not planes_equal(got, want):
+                bad.append(f"frame {f} out {k}: {first_diff(got, want)}")
+        return bad
+    with ThreadPoolExecutor(8) as ex:
+        bad = [b for r in ex.map(check, range(n)) for b in r]
+    assert not bad, bad[:4]
     g.close()
 
 
