@@ -1645,10 +1645,16 @@ static int run_device(dts_graph *g, QScratch &qs, const dts_dev_frames *src, int
         return DTS_OK;
     }
     const DevPlanes dsrc = to_dev(*src, s.src_fmt);
-    if (!(g->ref && qraw_dev))                   // no reference renditions to make: one call
+    // diagnostic DTS_Q_SUB=n (round-5 A/B, DESIGN.md §4 k_quality): with rendition quality, the
+    // ladder and its quality passes per sub-batch of n frames, so the renditions may still sit in
+    // the Infinity Cache when k_quality reads them back
+    const char *qsub_env = diag_env("DTS_Q_SUB");
+    const int qsub = qsub_env && qraw_dev && qref ? std::max(0, std::atoi(qsub_env)) : 0;
+    if (!(g->ref && qraw_dev) && !qsub)          // no reference renditions to make: one call
         return ladder_quality(g, qs, dsrc, ddst, dfmt, 0, nframes, nframes, qref, qraw_dev, st);
-    for (int c0 = 0; c0 < nframes; c0 += B) {    // reference renditions: one batch of scratch at a time
-        const int m = std::min(B, nframes - c0);
+    const int step = g->ref && qraw_dev ? (qsub ? std::min(qsub, B) : B) : qsub;
+    for (int c0 = 0; c0 < nframes; c0 += step) { // reference renditions: one batch of scratch at a time
+        const int m = std::min(step, nframes - c0);
         DevPlanes sc = dsrc, dd[DTS_MAX_OUTPUTS];
         for (int pl = 0; pl < 3; ++pl) sc.data[pl] += (uint64_t)((int64_t)c0 * src->frame_stride);
         dst_at(c0, dd);
