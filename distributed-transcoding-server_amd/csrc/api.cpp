@@ -1496,7 +1496,8 @@ static int enqueue_hdr(dts_graph *g, const DevPlanes &src, const DevPlanes *dst,
             tp.w = s.out[k].w;
             tp.h = s.out[k].h;
             tp.nframes = n;
-            HIPCHK(ctx, launch_tonemap(tp, st));
+            // the column walk (k_tonemap_w); diagnostic DTS_TM_TILED=1: the round-4 tiled kernel
+            HIPCHK(ctx, diag_env("DTS_TM_TILED") ? launch_tonemap(tp, st) : launch_tonemap_w(tp, st));
         }
         HIPCHK(ctx, hipEventRecord(g->hdr_ev[sl], st));
     }

@@ -409,7 +409,8 @@ struct TonemapParams {
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
     const float2 *lut;              // device [2][kTmLutN + 1] (value, slope): PQ EOTF x 10000 / npl, BT.709 OETF
 };
-hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);
+hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);     // tiled (k_tonemap)
+hipError_t launch_tonemap_w(const TonemapParams &p, hipStream_t s);   // column walk (k_tonemap_w)
 
 // ---------------------------------------------------------------------------
 // vf_yadif (deint.hip)

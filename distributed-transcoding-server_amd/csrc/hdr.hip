@@ -367,6 +367,171 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_tonemap_w (round 5, the default): the same conversion as a column walk.  A wave owns 63
+// chroma columns of one vertical chunk of the picture (lane 0 overlaps the strip to its left)
+// and walks it top to bottom, one chroma row (a 2 x 2 luma block per lane) per step:
+//  * the chroma a step interpolates (rows s - 1, s, s + 1 of columns cx and cx + 1) comes from
+//    registers: rows s - 1 and s carried, row s + 1 loaded a step ahead with the block's luma;
+//  * the 2:1 chroma filter of output row s - 1 reads full-resolution rows 2s - 3 .. 2s (three
+//    carried in registers, the fourth this step's top row) at columns 2cx - 1 .. 2cx + 1, the
+//    left one from lane - 1 (DPP wave_shr: every value is shifted once, when it is made);
+//  * no LDS but the two transfer tables, no barrier after they are loaded, no ring: the
+//    one-pixel ring of the tiled kernel (14 % more conversions) becomes lane 0's block (1/64)
+//    and one extra block row per chunk edge.
+// The arithmetic per pixel is pixel<> and the chroma / 2:1 expressions of k_tonemap above,
+// term for term, so both kernels give the same bytes.
+constexpr int kTwCols = 63;                      // output chroma columns per wave
+constexpr int kTwRows = 68;                      // chroma rows per chunk (1080p: 8 chunks)
+constexpr int kTwWaves = 8;                      // waves per workgroup (one table load)
+
+__device__ __forceinline__ float shr1(float x)   // lane l gets lane l - 1's value (lane 0: 0)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float2 cdec(uint32_t v)   // one p010 (Cb, Cr) pair, centred
+{
+    return make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f), (float)((int)(v >> 22) - 512) * (1.f / 896.f));
+}
+
+template <int MODE, bool DESAT>
+__global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams P, int nstrips, int nchunks)
+{
+    constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
+    __shared__ float2 tl[kTabs * (kTmLutN + 1)];
+    for (int i = threadIdx.x; i < kTabs * (kTmLutN + 1); i += 64 * kTwWaves) tl[i] = P.lut[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int item = blockIdx.x * kTwWaves + (threadIdx.x >> 6);
+    if (item >= nstrips * nchunks) return;
+    const int strip = item % nstrips, chunk = item / nstrips, f = blockIdx.z;
+    const int cw = P.w >> 1, ch = P.h >> 1;
+    const int r0 = chunk * kTwRows, r1 = min(r0 + kTwRows, ch);
+    const int cx = strip * kTwCols + lane - 1;                // lane 0: the left neighbour's last column
+    const bool out_col = lane > 0 && cx < cw;
+    // the block's two luma columns 2 cx, 2 cx + 1, clamped into the picture as pixc clamps them:
+    // lane 0 of the first strip (cx = -1) converts column 0 twice (chroma column 0, fx 0); lanes
+    // past the picture (last strip) read its last block and store nothing
+    const int cxc = min(max(cx, 0), cw - 1);
+    const int xL = 2 * cxc;
+    const float fx = cx < 0 ? 0.f : 0.5f;                    // the right column's weight of chroma column cx + 1
+    const int jA = cxc, jB = min(cxc + 1, cw - 1);
+    const bool lsplit = cx >= 0;                             // two luma samples (else column 0 twice)
+    const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
+    const uint64_t sy0 = P.src.data[0] + sf, sc0 = P.src.data[1] + sf;
+    const int64_t lp = P.src.pitch[0], cp = P.src.pitch[1];
+    const uint64_t lcol = 2 * (uint64_t)xL;                  // byte of xL in a luma row (xR follows it)
+    auto crow = [&](int r, uint32_t &a, uint32_t &b) {     // chroma row r (clamped), columns jA, jB
+        const uint64_t rb = sc0 + (uint64_t)min(max(r, 0), ch - 1) * cp;
+        a = gld<uint32_t>(rb + 4 * (uint64_t)jA);
+        b = gld<uint32_t>(rb + 4 * (uint64_t)jB);
+    };
+    auto lrow = [&](int y) -> uint32_t { return gld<uint32_t>(sy0 + (uint64_t)y * lp + lcol); };
+    const int s0 = r0 > 0 ? r0 - 1 : 0, s1 = r1 < ch ? r1 : ch - 1;
+    // carried chroma input rows (s - 1, s) and the next row / luma, loaded a step ahead
+    uint32_t mA, mB, aA, aB, pA, pB, l0, l1;
+    crow(s0 - 1, mA, mB);
+    crow(s0, aA, aB);
+    crow(s0 + 1, pA, pB);
+    l0 = lrow(2 * s0);
+    l1 = lrow(2 * s0 + 1);
+    // carried output chroma of full-resolution rows 2s - 3 (b2), 2s - 2 (t1), 2s - 1 (b1), each
+    // already as the 2:1 filter's horizontal sum 1/4 (2cx - 1) + 1/2 (2cx) + 1/4 (2cx + 1)
+    float2 b2, t1, b1;
+    constexpr float wy[4] = {0.125f, 0.375f, 0.375f, 0.125f};
+    auto hsum = [&](float2 l, float2 m, float2 r) {
+        return make_float2(0.25f * l.x + 0.5f * m.x + 0.25f * r.x, 0.25f * l.y + 0.5f * m.y + 0.25f * r.y);
+    };
+    auto emit = [&](int by, float2 a, float2 b, float2 c, float2 d) {
+        if (!out_col || by < r0 || by >= r1) return;
+        const float2 h[4] = {a, b, c, d};
+        float sb = 0.f, sr = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sb += wy[k] * h[k].x;
+            sr += wy[k] * h[k].y;
+        }
+        const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
+        if (P.dst_fmt == DTS_FMT_NV12) {
+            gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * cx, (uint16_t)(u | (v << 8)));
+        } else {
+            gst<uint8_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + cx, (uint8_t)u);
+            gst<uint8_t>(P.dst.data[2] + df + (uint64_t)by * P.dst.pitch[2] + cx, (uint8_t)v);
+        }
+    };
+    for (int s = s0; s <= s1; ++s) {
+        const float2 m0 = cdec(mA), m1 = cdec(mB), a0 = cdec(aA), a1 = cdec(aB), p0 = cdec(pA), p1 = cdec(pB);
+        const uint32_t q0 = l0, q1 = l1;
+        // the next step's loads fly during this step's conversion
+        mA = aA;
+        mB = aB;
+        aA = pA;
+        aB = pB;
+        if (s < s1) {
+            crow(s + 2, pA, pB);
+            l0 = lrow(2 * s + 2);
+            l1 = lrow(2 * s + 3);
+        }
+        const float2 ah = make_float2(a0.x + fx * (a1.x - a0.x), a0.y + fx * (a1.y - a0.y));
+        const float2 mh = make_float2(m0.x + fx * (m1.x - m0.x), m0.y + fx * (m1.y - m0.y));
+        const float2 ph = make_float2(p0.x + fx * (p1.x - p0.x), p0.y + fx * (p1.y - p0.y));
+        const float2 c[4] = {make_float2(0.75f * a0.x + 0.25f * m0.x, 0.75f * a0.y + 0.25f * m0.y),
+                             make_float2(0.75f * ah.x + 0.25f * mh.x, 0.75f * ah.y + 0.25f * mh.y),
+                             make_float2(0.75f * a0.x + 0.25f * p0.x, 0.75f * a0.y + 0.25f * p0.y),
+                             make_float2(0.75f * ah.x + 0.25f * ph.x, 0.75f * ah.y + 0.25f * ph.y)};
+        const float y0 = (float)__builtin_amdgcn_ubfe(q0, 6, 10), y2 = (float)__builtin_amdgcn_ubfe(q1, 6, 10);
+        const float y10[4] = {y0, lsplit ? (float)(q0 >> 22) : y0, y2, lsplit ? (float)(q1 >> 22) : y2};
+        float Yv[4];
+        float2 C[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pixel<MODE, DESAT>(P, tl, y10[q], c[q], Yv[q], C[q]);
+        if (out_col && s >= r0 && s < r1) {
+            const uint64_t yd = P.dst.data[0] + df + (uint64_t)(2 * s) * P.dst.pitch[0] + 2 * cx;
+            gst<uint16_t>(yd, (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)));
+            gst<uint16_t>(yd + P.dst.pitch[0], (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8)));
+        }
+        // this step's rows as horizontal sums, column 2cx - 1 from lane - 1 (all lanes active here)
+        const float2 ht = hsum(make_float2(shr1(C[1].x), shr1(C[1].y)), C[0], C[1]);
+        const float2 hb = hsum(make_float2(shr1(C[3].x), shr1(C[3].y)), C[2], C[3]);
+        if (s == 0) {                                         // row -1 clamps to row 0
+            b2 = ht;
+        } else if (s > s0) {
+            emit(s - 1, b2, t1, b1, ht);
+            b2 = b1;
+        }
+        t1 = ht;
+        b1 = hb;
+    }
+    if (r1 == ch)                                             // row h clamps to row h - 1
+        emit(ch - 1, b2, t1, b1, b1);
+}
+
+hipError_t launch_tonemap_w(const TonemapParams &p, hipStream_t s)
+{
+    const int cw = p.w / 2, ch = p.h / 2;
+    const int nstrips = (cw + kTwCols - 1) / kTwCols, nchunks = (ch + kTwRows - 1) / kTwRows;
+    const dim3 grid((unsigned)((nstrips * nchunks + kTwWaves - 1) / kTwWaves), 1, (unsigned)p.nframes);
+    const bool ds = p.desat > 0.f;
+#define DTS_TM_CASE(m)                                                                                               \
+    case m:                                                                                                          \
+        if (ds) hipLaunchKernelGGL((k_tonemap_w<m, true>), grid, dim3(64 * kTwWaves), 0, s, p, nstrips, nchunks);   \
+        else hipLaunchKernelGGL((k_tonemap_w<m, false>), grid, dim3(64 * kTwWaves), 0, s, p, nstrips, nchunks);     \
+        break;
+    switch (p.mode) {
+    DTS_TM_CASE(DTS_TM_NONE)
+    DTS_TM_CASE(DTS_TM_LINEAR)
+    DTS_TM_CASE(DTS_TM_GAMMA)
+    DTS_TM_CASE(DTS_TM_CLIP)
+    DTS_TM_CASE(DTS_TM_REINHARD)
+    DTS_TM_CASE(DTS_TM_HABLE)
+    DTS_TM_CASE(DTS_TM_MOBIUS)
+    default: return hipErrorInvalidValue;
+    }
+#undef DTS_TM_CASE
+    return hipGetLastError();
+}
+
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s)
 {
     const int rows = kTmCRows * kTmTiles;
