@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -215,6 +217,7 @@ struct dts_graph {
     const dts_frame *p_dst = nullptr;
     dts_qstat *p_q = nullptr;
     int p_chunk_first[2] = {-1, -1}, p_chunk_n[2] = {0, 0};
+    bool p_zout[2] = {false, false};      // the slot's outputs went straight into pinned caller frames
     // HDR10 -> SDR: per output a p010 intermediate of `batch` frames, double-buffered
     // (an event per buffer orders reuse across the host path's two streams)
     bool hdr = false;
@@ -1854,6 +1857,58 @@ static void free_host_path(dts_graph *g)
     g->host_ready = false;
 }
 
+// Pinned host memory the library knows about: dts_host_alloc allocations and
+// dts_host_register'ed ranges.  The host path DMAs straight from / into frames whose
+// planes lie inside one of them (no pack / unpack through the pinned rings).
+extern "C++" {
+namespace {
+struct PinnedSet {
+    std::mutex m;
+    std::map<uintptr_t, std::pair<size_t, bool>> r;   // base -> (bytes, registered rather than allocated)
+};
+PinnedSet &pinned_set()
+{
+    static PinnedSet *p = new PinnedSet;             // (never destroyed: frees may come at exit)
+    return *p;
+}
+bool pinned_range(const void *ptr, size_t n)
+{
+    if (!ptr) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    PinnedSet &ps = pinned_set();
+    std::lock_guard<std::mutex> lk(ps.m);
+    auto it = ps.r.upper_bound(a);
+    if (it == ps.r.begin()) return false;
+    --it;
+    return a >= it->first && a + n <= it->first + it->second.first;
+}
+// every plane of frame f (layout lay: rows x row bytes) lies in pinned memory
+bool frame_pinned(const dts_frame &f, const DevLayout &lay)
+{
+    for (int p = 0; p < 3; ++p) {
+        if (!lay.rows[p]) continue;
+        if (!f.data[p] || f.pitch[p] < lay.rowb[p]) return false;
+        if (!pinned_range(f.data[p], (size_t)((lay.rows[p] - 1) * f.pitch[p] + lay.rowb[p]))) return false;
+    }
+    return true;
+}
+// one frame between a caller frame in pinned memory and frame `i` of a device batch (DMA, 2-D per plane)
+hipError_t copy_frame_direct(uint8_t *dev, const DevLayout &lay, const dts_frame &f, bool h2d, hipStream_t st)
+{
+    for (int p = 0; p < 3; ++p) {
+        if (!lay.rows[p]) continue;
+        const hipError_t e =
+            h2d ? hipMemcpy2DAsync(dev + lay.off[p], (size_t)lay.pitch[p], f.data[p], (size_t)f.pitch[p], (size_t)lay.rowb[p],
+                                   (size_t)lay.rows[p], hipMemcpyHostToDevice, st)
+                : hipMemcpy2DAsync(f.data[p], (size_t)f.pitch[p], dev + lay.off[p], (size_t)lay.pitch[p], (size_t)lay.rowb[p],
+                                   (size_t)lay.rows[p], hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+} // namespace
+} // extern "C++"
+
 static int alloc_host_path(dts_graph *g);
 
 // Every buffer of both slots, or none (a failed allocation frees what was made,
@@ -1967,7 +2022,7 @@ static int finish_slot(dts_graph *g, int sl)
     HIPCHK(ctx, hipEventSynchronize(g->done[sl]));
     const int f0 = g->p_chunk_first[sl], n = g->p_chunk_n[sl];
     const uint8_t *hp0 = g->pin_out[sl];         // per output: a region of `batch` packed frames
-    parallel_for(n * s.nout, [&](int i) {
+    if (!g->p_zout[sl]) parallel_for(n * s.nout, [&](int i) {
         const int f = i / s.nout, k = i % s.nout;
         const uint8_t *hp = hp0;
         for (int kk = 0; kk < k; ++kk) hp += (int64_t)g->batch * g->lay_out[kk].fstride;
@@ -2020,12 +2075,27 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             hipStream_t st = ctx->stream[sl];
             uint8_t *hp = g->pin_in[sl];
             const int cf = s.deint ? 2 : 0;              // deint: src[f0 .. f0 + n + 1] (context frames)
-            parallel_for(n + cf, [&](int f) {
-                pack_frame(hp + (int64_t)f * g->lay_src.fstride, src[f0 + f], g->lay_src);
-            });
-            HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n + cf, true, st));
+            // frames in pinned memory (dts_host_alloc / dts_host_register) go to the device by DMA
+            // straight from the caller's planes; others are packed into the pinned ring first
+            bool zin = true;
+            for (int f = 0; f < n + cf && zin; ++f) zin = frame_pinned(src[f0 + f], g->lay_src);
+            for (int f = 0; f < n && zin && s.quality; ++f) zin = frame_pinned(qref[f0 + f], g->lay_q);
+            if (zin) {
+                for (int f = 0; f < n + cf; ++f)
+                    HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_src[sl]) + (int64_t)f * g->lay_src.fstride,
+                                                  g->lay_src, src[f0 + f], true, st));
+            } else {
+                parallel_for(n + cf, [&](int f) {
+                    pack_frame(hp + (int64_t)f * g->lay_src.fstride, src[f0 + f], g->lay_src);
+                });
+                HIPCHK(ctx, copy_frames(g->dev_src[sl], g->lay_src, hp, n + cf, true, st));
+            }
             uint8_t *qhp = hp + (int64_t)(B + cf) * g->lay_src.fstride;
-            if (s.quality) {
+            if (s.quality && zin) {
+                for (int f = 0; f < n; ++f)
+                    HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_q[sl]) + (int64_t)f * g->lay_q.fstride, g->lay_q,
+                                                  qref[f0 + f], true, st));
+            } else if (s.quality) {
                 parallel_for(n, [&](int f) {
                     pack_frame(qhp + (int64_t)f * g->lay_q.fstride, qref[f0 + f], g->lay_q);
                 });
@@ -2038,11 +2108,22 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             e = run_device(g, g->hqs[sl], &dsrc, n, ddst, s.quality ? &dq : nullptr,
                            (s.quality || g->ref) ? g->dev_qraw[sl] : nullptr, st);
             if (e) return e;
-            uint8_t *op = g->pin_out[sl];
-            for (int k = 0; k < s.nout; ++k) {
-                HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
-                op += (int64_t)B * g->lay_out[k].fstride;
+            bool zout = true;
+            for (int f = 0; f < n && zout; ++f)
+                for (int k = 0; k < s.nout && zout; ++k) zout = frame_pinned(dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
+            if (zout) {                          // straight into the caller's pinned frames
+                for (int f = 0; f < n; ++f)
+                    for (int k = 0; k < s.nout; ++k)
+                        HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_out[sl][k]) + (int64_t)f * g->lay_out[k].fstride,
+                                                      g->lay_out[k], dst[(int64_t)(f0 + f) * s.nout + k], false, st));
+            } else {
+                uint8_t *op = g->pin_out[sl];
+                for (int k = 0; k < s.nout; ++k) {
+                    HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
+                    op += (int64_t)B * g->lay_out[k].fstride;
+                }
             }
+            g->p_zout[sl] = zout;
             if (s.quality || g->ref)
                 HIPCHK(ctx, hipMemcpyAsync(g->pin_qraw[sl], g->dev_qraw[sl],
                                            (size_t)n * (g->ref ? s.nout : 1) * sizeof(dts_qraw),
@@ -2066,6 +2147,69 @@ int dts_graph_wait(dts_graph *g)
     int e0 = finish_slot(g, 0), e1 = finish_slot(g, 1);
     g->pending = false;
     return e0 ? e0 : e1;
+}
+
+int dts_host_alloc(size_t bytes, void **out)
+{
+    if (!out || !bytes) return DTS_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return DTS_E_NODEV;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) return DTS_E_NOMEM;
+    try {
+        PinnedSet &ps = pinned_set();
+        std::lock_guard<std::mutex> lk(ps.m);
+        ps.r[reinterpret_cast<uintptr_t>(p)] = {bytes, false};
+    } catch (...) {
+        hipHostFree(p);
+        return DTS_E_NOMEM;
+    }
+    *out = p;
+    return DTS_OK;
+}
+
+void dts_host_free(void *p)
+{
+    if (!p) return;
+    PinnedSet &ps = pinned_set();
+    {
+        std::lock_guard<std::mutex> lk(ps.m);
+        auto it = ps.r.find(reinterpret_cast<uintptr_t>(p));
+        if (it == ps.r.end() || it->second.second) return;   // not ours (or a registered range)
+        ps.r.erase(it);
+    }
+    hipHostFree(p);
+}
+
+int dts_host_register(void *p, size_t bytes)
+{
+    if (!p || !bytes) return DTS_E_INVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return DTS_E_NODEV;
+    if (hipHostRegister(p, bytes, hipHostRegisterPortable) != hipSuccess) return DTS_E_HIP;
+    try {
+        PinnedSet &ps = pinned_set();
+        std::lock_guard<std::mutex> lk(ps.m);
+        ps.r[reinterpret_cast<uintptr_t>(p)] = {bytes, true};
+    } catch (...) {
+        hipHostUnregister(p);
+        return DTS_E_NOMEM;
+    }
+    return DTS_OK;
+}
+
+int dts_host_unregister(void *p)
+{
+    if (!p) return DTS_E_INVAL;
+    PinnedSet &ps = pinned_set();
+    {
+        std::lock_guard<std::mutex> lk(ps.m);
+        auto it = ps.r.find(reinterpret_cast<uintptr_t>(p));
+        if (it == ps.r.end() || !it->second.second) return DTS_E_INVAL;
+        ps.r.erase(it);
+    }
+    return hipHostUnregister(p) == hipSuccess ? DTS_OK : DTS_E_HIP;
 }
 
 int dts_sws_filter(int src_n, int dst_n, int one, int align, int method, const double param[2], int pos,

@@ -301,7 +301,8 @@ struct Unit6 {                      // one wave's share of a frame
     int32_t x0[4];                  // first source column of each column tile's H K blocks (multiple of 4,
                                     // except a right-edge tile ending at the plane's last column)
     int32_t fs;                     // V fragment slots in LDS: most row blocks firing within kL6Stages granules
-    int32_t pad_;
+    int32_t vdedup;                 // 1: the rendition's V fragments are stored once per distinct fragment and
+                                    // fire entry j carries its index in bits 10..15 (granule in bits 0..9)
 };
 
 
@@ -331,7 +332,7 @@ struct Unit7 {                      // one wave of a group
     int32_t rc_sh;                  // range conversion of the 15-bit H output (0: none):
     int32_t rc_cap, rc_mul, rc_add; //   y = (min(y, cap) * mul + add) >> sh, as swscale.c's lum/chr
                                     //   RangeToJpeg_c / RangeFromJpeg_c (int16 store)
-    int32_t pad_;
+    int32_t vdedup;                 // as Unit6
 };
 
 struct Group7 {                     // one workgroup's strip of one frame

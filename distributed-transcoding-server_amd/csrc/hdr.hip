@@ -381,9 +381,18 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 //    and one extra block row per chunk edge.
 // The arithmetic per pixel is pixel<> and the chroma / 2:1 expressions of k_tonemap above,
 // term for term, so both kernels give the same bytes.
+// chunk height and workgroup size (round-5 A/B on cfg3, tools/r05_tmab.sh: chunks of 34 / 68 / 135
+// rows 79.5 k / 79.5 k / 78.7 k fps, 4-wave workgroups 79.1 k, column cx + 1 through DPP instead of
+// a second load 78.4 k)
+#ifndef DTS_TW_ROWS
+#define DTS_TW_ROWS 68
+#endif
+#ifndef DTS_TW_WAVES
+#define DTS_TW_WAVES 8
+#endif
 constexpr int kTwCols = 63;                      // output chroma columns per wave
-constexpr int kTwRows = 68;                      // chroma rows per chunk (1080p: 8 chunks)
-constexpr int kTwWaves = 8;                      // waves per workgroup (one table load)
+constexpr int kTwRows = DTS_TW_ROWS;             // chroma rows per chunk (1080p: 8 chunks)
+constexpr int kTwWaves = DTS_TW_WAVES;           // waves per workgroup (one table load)
 
 __device__ __forceinline__ float shr1(float x)   // lane l gets lane l - 1's value (lane 0: 0)
 {

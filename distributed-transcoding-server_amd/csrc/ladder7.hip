@@ -621,12 +621,14 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         const uint32_t hi = lane + 64 < nrb ? (uint32_t)fp[lane + 64] : 0xffffu;
         vtab = lo | (hi << 16);
     }
-    auto firev = [&](int i) -> int {
-        if (i >= nrb) return 0x7fffffff;
+    // a fire entry: the granule (bits 0..9) and, for renditions stored per distinct V fragment
+    // (Unit7::vdedup), the row block's fragment index (bits 10..15)
+    auto fentry = [&](int i) -> int {
         if (i >= 128) return (int)fire[i];
         const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)vtab, i & 63);
         return (int)((i & 64 ? x >> 16 : x) & 0xffffu);
     };
+    auto firev = [&](int i) -> int { return i >= nrb ? 0x7fffffff : (fentry(i) & 1023); };
     int j = 0, jf = 0;
     int fg = firev(0), fg1 = firev(1);
     int fgf = U.lead ? fg : 0x7fffffff, fgf1 = U.lead ? fg1 : 0x7fffffff;
@@ -645,7 +647,8 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
     auto frags = [&](int upto) {
         while (fgf <= upto) {
             uint8_t *dst = fb + (uint32_t)fsi * (uint32_t)(VKB * 2048);
-            const uint64_t src = fr + (uint64_t)(U.vfrag + (uint32_t)(jf * VKB)) * 2048u;
+            const uint32_t fj = U.vdedup ? (uint32_t)fentry(jf) >> 10 : (uint32_t)jf;
+            const uint64_t src = fr + (uint64_t)(U.vfrag + fj * (uint32_t)VKB) * 2048u;
             if (!(DTS_L7_ABLATE & 256)) {
                 Z.ops += 2 * VKB;
 #pragma unroll

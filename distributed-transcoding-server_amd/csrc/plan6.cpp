@@ -293,6 +293,38 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
             while (z < nrb && p.r.fire[z] < p.r.fire[a] + fs_window) ++z;
             fs = std::max(fs, z - a);
         }
+        // Distinct V fragments (round 5): row blocks whose fragments are byte-identical (the
+        // filter repeats with the output phase: 4 / 10 / 18 distinct of 68 / 45 / 30 row blocks
+        // for the 4K cfg2 luma renditions) share one copy, and the row block's fire entry carries
+        // its index in bits 10..15.  A group's lead waves then DMA from a table of ~0.2 MB
+        // instead of 1.1 MB, which stays in L2.  More than 64 distinct: stored per row block.
+        int vdedup = 0;
+        {
+            const size_t fw = (size_t)p.r.vkb * 512;
+            auto at = [&](int jb) { return out.frag.data() + (size_t)(p.vfrag + (uint32_t)(jb * p.r.vkb)) * 512; };
+            std::vector<int> uniq, vid((size_t)nrb);
+            for (int jb = 0; jb < nrb; ++jb) {
+                int found = -1;
+                for (int u = 0; u < (int)uniq.size() && found < 0; ++u)
+                    if (!std::memcmp(at(jb), at(uniq[(size_t)u]), fw * 4)) found = u;
+                if (found < 0) {
+                    found = (int)uniq.size();
+                    uniq.push_back(jb);
+                }
+                vid[(size_t)jb] = found;
+            }
+            bool ok = uniq.size() <= 64;
+            for (int jb = 0; jb < nrb && ok; ++jb) ok = p.r.fire[jb] < 1024;
+            if (ok) {
+                for (int u = 0; u < (int)uniq.size(); ++u)     // compact: slot u <= its first row block
+                    if (uniq[(size_t)u] != u) std::memmove(at(u), at(uniq[(size_t)u]), fw * 4);
+                for (int jb = 0; jb < nrb; ++jb) out.fire[(size_t)p.fire + jb] |= vid[(size_t)jb] << 10;
+                vdedup = 1;
+            }
+            if (diag_env("DTS_PLAN_DEBUG"))
+                std::fprintf(stderr, "plan6 kind %d rung %d nrb %d vkb %d distinct V fragments %zu fs %d dedup %d\n",
+                             p.kind, p.rung, nrb, p.r.vkb, uniq.size(), fs, vdedup);
+        }
         for (int u = 0; u * p.ct < ntp; ++u) {
             Unit6 w{};
             w.variant = var;
@@ -311,6 +343,7 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
             w.fire = p.fire;
             for (int c = 0; c < 4; ++c) w.x0[c] = c < p.ct ? p.r.x0[(size_t)u * p.ct + c] : 0;
             w.fs = fs;
+            w.vdedup = vdedup;
             // MFMAs per unit: H ngran x tiles x HKB x 2, V row blocks x tiles x VKB x 4
             const int tiles = p.ct * np;
             const int64_t cost = (int64_t)ngran * tiles * p.r.hkb * 2 + (int64_t)nrb * tiles * p.r.vkb * 4;
@@ -495,6 +528,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
                 for (int c = 0; c < 4; ++c)
                     v.xo[c] = (c < ct && 16 * c < w.ncols) ? w.x0[c] - g.X0 : w.x0[0] - g.X0;
                 v.fs = w.fs;
+                v.vdedup = w.vdedup;
                 // swscale.c (FFmpeg 4.4) range converters (oracle/swscale_ref.c restates them)
                 static const int32_t rc[2][2][4] = {
                     {{14, 30189, 19077, -39057361}, {14, 32767, 14071, 33561947}},   // luma: To, From

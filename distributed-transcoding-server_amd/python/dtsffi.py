@@ -32,7 +32,7 @@ TM_NONE, TM_LINEAR, TM_GAMMA, TM_CLIP, TM_REINHARD, TM_HABLE, TM_MOBIUS = range(
 TM_MODES = {"none": TM_NONE, "linear": TM_LINEAR, "gamma": TM_GAMMA, "clip": TM_CLIP, "reinhard": TM_REINHARD,
             "hable": TM_HABLE, "mobius": TM_MOBIUS}
 MAX_OUTPUTS = 4
-ABI_VERSION = 6              # include/dts.h DTS_ABI_VERSION this binding lays its structs out for
+ABI_VERSION = 7              # include/dts.h DTS_ABI_VERSION this binding lays its structs out for
 
 E_INVAL, E_NOMEM, E_RANGE, E_UNSUPPORTED, E_BUSY, E_NODEV, E_HIP = -22, -12, -34, -95, -16, -19, -1000
 
@@ -97,7 +97,8 @@ EXPORTS = ["dts_version", "dts_strerror", "dts_device_count", "dts_ctx_create", 
            "dts_graph_submit", "dts_graph_wait", "dts_graph_run_device", "dts_quality_run_device",
            "dts_qstat_finalize", "dts_synth_host", "dts_synth_device", "dts_frame_layout",
            "dts_sws_filter", "dts_fps_map", "dts_graph_plan", "dts_yadif_run_device", "dts_quality_run_host",
-           "dts_qraw_sum_device", "dts_qstat_stream", "dts_abi_version", "dts_abi_struct_size"]
+           "dts_qraw_sum_device", "dts_qstat_stream", "dts_abi_version", "dts_abi_struct_size",
+           "dts_host_alloc", "dts_host_free", "dts_host_register", "dts_host_unregister"]
 
 # DTS_STRUCT_* ids of dts_abi_struct_size and the ctypes layout of each (filled below)
 STRUCT_IDS = {}
@@ -147,6 +148,11 @@ def lib():
     L.dts_fps_map.restype = i64
     L.dts_yadif_run_device.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(DevFrames), i32, i32, i32,
                                        ctypes.POINTER(DevFrames), vp]
+    L.dts_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.dts_host_free.argtypes = [vp]
+    L.dts_host_free.restype = None
+    L.dts_host_register.argtypes = [vp, ctypes.c_size_t]
+    L.dts_host_unregister.argtypes = [vp]
     L.dts_abi_version.argtypes = []
     L.dts_abi_struct_size.argtypes = [i32]
     L.dts_abi_struct_size.restype = i64
@@ -206,6 +212,42 @@ def alloc_frame(w, h, fmt, pad=0):
             buf = np.zeros((s[0], s[1] + pad), np.uint8)
             planes.append(buf[:, :s[1]])
     return planes
+
+
+class PinnedBuffer:
+    """dts_host_alloc memory as a uint8 numpy array (`.array`); freed with dts_host_free when
+    the object goes away.  Frames carved from it take the host path's direct DMA (ABI 7)."""
+
+    def __init__(self, nbytes):
+        p = ctypes.c_void_p()
+        check(lib().dts_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().dts_host_free(self.ptr)
+            self.ptr = None
+
+
+def alloc_frames_pinned(w, h, fmt, n):
+    """n frames of (w, h, fmt) in one pinned buffer: ([planes per frame], the PinnedBuffer,
+    which must outlive the frames)."""
+    shapes = plane_shapes(w, h, fmt)
+    fb = sum(s[0] * s[1] for s in shapes if s is not None)
+    buf = PinnedBuffer(max(1, fb * n))
+    frames = []
+    for i in range(n):
+        off, planes = i * fb, []
+        for s in shapes:
+            if s is None:
+                planes.append(None)
+                continue
+            planes.append(buf.array[off:off + s[0] * s[1]].reshape(s[0], s[1]))
+            off += s[0] * s[1]
+        frames.append(planes)
+    return frames, buf
 
 
 def frame_struct(planes):
@@ -381,15 +423,21 @@ class Graph:
         except Exception:
             pass
 
-    def run_host(self, frames, qref=None):
+    def run_host(self, frames, qref=None, pinned_out=False):
         """frames: list of source frames (plane lists; with deint, n + 2 of them: one
         context frame each side).  Returns (outputs, qstats): outputs[f][k] is output
-        k of frame f as a plane list."""
+        k of frame f as a plane list.  pinned_out: the outputs are allocated with
+        dts_host_alloc (the library DMAs straight into them; ABI 7)."""
         s = self.spec
         ns = len(frames)
         n = ns - 2 if s.deint else ns
         src = (Frame * ns)(*[frame_struct(f) for f in frames])
-        outs = [[alloc_frame(s.out[k].w, s.out[k].h, s.out[k].fmt) for k in range(s.nout)] for _ in range(n)]
+        if pinned_out:
+            per = [alloc_frames_pinned(s.out[k].w, s.out[k].h, s.out[k].fmt, n) for k in range(s.nout)]
+            self._pinned_keep = [b for (_f, b) in per]
+            outs = [[per[k][0][f] for k in range(s.nout)] for f in range(n)]
+        else:
+            outs = [[alloc_frame(s.out[k].w, s.out[k].h, s.out[k].fmt) for k in range(s.nout)] for _ in range(n)]
         dst = (Frame * (n * s.nout))(*[frame_struct(outs[f][k]) for f in range(n) for k in range(s.nout)])
         rq = any(s.out[k].quality for k in range(s.nout))
         if rq:                      # rendition quality: q[f * nout + k]

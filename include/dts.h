@@ -45,10 +45,12 @@
 extern "C" {
 #endif
 
-/* ABI 6: dts_output_spec gained quality / qref_method (rendition quality).  A binding
+/* ABI 7: dts_host_alloc / dts_host_free / dts_host_register / dts_host_unregister (pinned
+ * host frames the host path DMAs straight from and into).
+ * ABI 6: dts_output_spec gained quality / qref_method (rendition quality).  A binding
  * compiled against this header checks dts_abi_version() == DTS_ABI_VERSION and
  * dts_abi_struct_size() of every struct it lays out before any other call. */
-#define DTS_ABI_VERSION 6
+#define DTS_ABI_VERSION 7
 #define DTS_MAX_OUTPUTS 4
 
 /* error codes (AVERROR-style negative ints) */
@@ -258,6 +260,20 @@ int dts_graph_plan(const dts_graph_spec *spec, dts_graph_info *info);
 int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes,
                      const dts_frame *dst, const dts_frame *qref, dts_qstat *q);
 int dts_graph_wait(dts_graph *g);
+
+/* Pinned host memory for the host path (ABI 7).  A chunk of dts_graph_submit whose source
+ * (and qref) frames all lie in pinned memory the library knows is copied to the device by
+ * DMA straight from the caller's planes, and a chunk whose output frames all do is copied
+ * straight into them: no pass through the library's pinned rings (the host threads'
+ * pack / unpack copies, which bound the pageable path).  Frames anywhere else take the
+ * ring as before.  dts_host_alloc: page-locked memory usable by every device
+ * (hipHostMalloc portable), released by dts_host_free.  dts_host_register: page-lock a
+ * caller range (hipHostRegister portable) until dts_host_unregister.  Replaces the
+ * pageable frame buffers an ffmpeg worker's decoder / encoder hand around. */
+int dts_host_alloc(size_t bytes, void **out);
+void dts_host_free(void *p);
+int dts_host_register(void *p, size_t bytes);
+int dts_host_unregister(void *p);
 
 /* Device-resident path: enqueue one batch on `stream` (a hipStream_t, NULL =
  * the ctx's stream).  dst[k] is the batch of output k.  When the graph has

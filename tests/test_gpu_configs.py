@@ -85,3 +85,45 @@ def test_cfg2_ladder_4k_host_path_two_frames(ctx):
             want = orc.scale_frame(frames[f], sw, sh, 0, w, h, fmt, m)
             assert planes_equal(got[f][k], want), f"frame {f} out {k}: {first_diff(got[f][k], want)}"
     g.close()
+
+
+@pytest.mark.parametrize("pin_src,pin_out", [(True, True), (True, False), (False, True)])
+def test_host_path_pinned_frames(ctx, pin_src, pin_out):
+    """ABI 7: frames in dts_host_alloc memory go to / come from the device by DMA straight
+    from / into the caller's planes (no pass through the pinned rings); every combination
+    of pinned and pageable sources / outputs over several chunks is bit-exact."""
+    sw, sh, n, batch = 384, 216, 7, 3
+    outs_spec = [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC), (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS)]
+    frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 77, f) for f in range(n)]
+    keep = None
+    if pin_src:
+        pf, keep = D.alloc_frames_pinned(sw, sh, D.FMT_YUV420P, n)
+        for a, b in zip(pf, frames):
+            for pa, pb in zip(a, b):
+                if pa is not None:
+                    pa[...] = pb
+        frames = pf
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, outs_spec, max_batch=batch))
+    for _rep in range(2):
+        outs, _ = g.run_host(frames, pinned_out=pin_out)
+        for f in range(n):
+            for k, (w, h, fmt, m) in enumerate(outs_spec):
+                want = orc.scale_frame(frames[f], sw, sh, D.FMT_YUV420P, w, h, fmt, m)
+                assert planes_equal(outs[f][k], want), f"frame {f} out {k}: {first_diff(outs[f][k], want)}"
+    g.close()
+    del keep
+
+
+def test_host_register_roundtrip(ctx):
+    """dts_host_register / dts_host_unregister a caller range; frees of unknown pointers are
+    ignored and a double unregister is an error."""
+    import ctypes
+    buf = np.zeros(1 << 20, np.uint8)
+    L = D.lib()
+    assert L.dts_host_register(ctypes.c_void_p(buf.ctypes.data), buf.nbytes) == 0
+    assert L.dts_host_unregister(ctypes.c_void_p(buf.ctypes.data)) == 0
+    assert L.dts_host_unregister(ctypes.c_void_p(buf.ctypes.data)) == D.E_INVAL
+    L.dts_host_free(ctypes.c_void_p(buf.ctypes.data))          # not the library's: ignored
+    p = D.PinnedBuffer(4096)
+    p.array[:] = 7
+    assert int(p.array.sum()) == 7 * 4096

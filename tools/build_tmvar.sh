@@ -8,7 +8,7 @@ OBJS="build/api.o build/filters.o build/plan5.o build/plan6.o build/kernels.o bu
 for a in "$@"; do
   n=${a%%=*}; d=${a#*=}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize $d -c csrc/hdr.hip -o build/hdr_$n.o \
-      -Rpass-analysis=kernel-resource-usage 2>&1 | grep -A3 -E "k_tonemapILi5ELb1" | grep -E "VGPRs:|LDS Size" | head -2 | sed "s/^.*remark: */$n: /"
+      -Rpass-analysis=kernel-resource-usage 2>&1 | grep -A3 -E "k_tonemap_wILi5ELb1" | grep -E "VGPRs:|LDS Size" | head -2 | sed "s/^.*remark: */$n: /"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libdts_$n.so $OBJS build/hdr_$n.o \
       -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libdts.so
 done
