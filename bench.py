@@ -339,7 +339,24 @@ def run_e2e(args, wl, ctx, sptr):
     nsrc = args.e2e_frames                   # distinct host source frames, cycled
     srcs = [D.synth_host(sw, sh, sfmt, 0, 0x5EED, i) for i in range(nsrc)]
     per = args.e2e_submit                    # frames per submit (several chunks: both slots busy)
-    outs = [[D.alloc_frame(w, h, fmt) for (w, h, fmt, _m) in wl["outs"]] for _ in range(per)]
+    keep = []
+    if args.e2e_pinned:
+        # ABI 7: frames in dts_host_alloc memory -- the library DMAs straight from / into them
+        pf, buf = D.alloc_frames_pinned(sw, sh, sfmt, nsrc)
+        keep.append(buf)
+        for a, b in zip(pf, srcs):
+            for pa, pb in zip(a, b):
+                if pa is not None:
+                    pa[...] = pb
+        srcs = pf
+        per_out = []
+        for (w, h, fmt, _m) in wl["outs"]:
+            fr, buf = D.alloc_frames_pinned(w, h, fmt, per)
+            keep.append(buf)
+            per_out.append(fr)
+        outs = [[per_out[k][f] for k in range(len(wl["outs"]))] for f in range(per)]
+    else:
+        outs = [[D.alloc_frame(w, h, fmt) for (w, h, fmt, _m) in wl["outs"]] for _ in range(per)]
     nout = len(wl["outs"])
     dst = (D.Frame * (per * nout))(*[D.frame_struct(outs[f][k]) for f in range(per) for k in range(nout)])
     src_arr = [(D.Frame * per)(*[D.frame_struct(srcs[(i * per + f) % nsrc]) for f in range(per)])
@@ -365,13 +382,18 @@ def run_e2e(args, wl, ctx, sptr):
                 if a is not None and not np.array_equal(a, b):
                     ok = False
     g.close()
+    src_b = g.info.src_frame_bytes
+    out_b = sum(g.info.out_frame_bytes[k] for k in range(nout))
     return {"metric": f"frames/s end to end (host memory -> GPU -> host memory), {args.workload}",
             "value": round(fps, 1), "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": f"{nsrc} synthetic host frames, cycled",
             "config": {"workload": wl["desc"], "frames_per_submit": per, "chunk_frames": chunk,
+                       "host_frames": "pinned (dts_host_alloc: direct DMA)" if args.e2e_pinned
+                       else "pageable (packed through the library's pinned rings)",
                        "host_threads": os.environ.get("DTS_HOST_THREADS", "hardware threads (<= 16)")},
             "pcie_bytes_per_frame": io, "host_io_GBps": round(fps * io / 1e9, 2),
+            "h2d_GBps": round(fps * src_b / 1e9, 2), "d2h_GBps": round(fps * out_b / 1e9, 2),
             "verified_vs_oracle": ok if not args.no_verify else None}
 
 
@@ -388,9 +410,13 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="time the host-memory path (dts_graph_submit / wait) instead of device-resident batches")
-    ap.add_argument("--e2e-batch", type=int, default=32, help="--e2e: frames per device chunk (max_batch)")
-    ap.add_argument("--e2e-submit", type=int, default=128, help="--e2e: frames per submit")
-    ap.add_argument("--e2e-frames", type=int, default=128, help="--e2e: distinct host source frames")
+    # (round 5, tools/r05_e2e.sh: submits of 512 frames in chunks of 64 3,174-3,270 fps against 2,918-3,032 for
+    # 128 / 32, pageable or pinned alike)
+    ap.add_argument("--e2e-batch", type=int, default=64, help="--e2e: frames per device chunk (max_batch)")
+    ap.add_argument("--e2e-submit", type=int, default=512, help="--e2e: frames per submit")
+    ap.add_argument("--e2e-frames", type=int, default=256, help="--e2e: distinct host source frames")
+    ap.add_argument("--e2e-pinned", action="store_true",
+                    help="--e2e: host frames in dts_host_alloc memory (direct DMA, no ring copies)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS),
                     help="cfg2 = the BASELINE metric's workload (default line); cfg3 / cfg4 = extra lines")
     args = ap.parse_args()

@@ -655,6 +655,37 @@ static napi_value js_synth_frame(napi_env env, napi_callback_info info)
     return u;
 }
 
+/* ---- hostAlloc(bytes) -> Buffer in pinned memory (dts_host_alloc, ABI 7) ----------
+ * Frames whose planes are views of such a Buffer (pitches = the device layout's, i.e.
+ * row bytes rounded up to 16) cross PCIe by one DMA per plane in run(), without the
+ * library's ring copies.  The memory is released (dts_host_free) when the Buffer is
+ * garbage collected; keep it alive until run() settles. */
+static void host_free_cb(napi_env env, void *data, void *hint)
+{
+    (void)env;
+    (void)hint;
+    dts_host_free(data);
+}
+
+static napi_value js_host_alloc(napi_env env, napi_callback_info info)
+{
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    double nb = 0;
+    if (argc < 1 || napi_get_value_double(env, argv[0], &nb) != napi_ok || !(nb >= 1) || nb > 1e12)
+        return throw_dts(env, DTS_E_INVAL, "hostAlloc(bytes)");
+    void *p = NULL;
+    const int e = dts_host_alloc((size_t)nb, &p);
+    if (e) return throw_dts(env, e, "dts_host_alloc");
+    napi_value buf;
+    if (napi_create_external_buffer(env, (size_t)nb, p, host_free_cb, NULL, &buf) != napi_ok) {
+        dts_host_free(p);
+        return throw_dts(env, DTS_E_NOMEM, "hostAlloc: external buffer");
+    }
+    return buf;
+}
+
 /* ---- frameLayout(w, h, fmt) -> {pitch, rows, bytes} --------------------- */
 static napi_value js_frame_layout(napi_env env, napi_callback_info info)
 {
@@ -763,6 +794,7 @@ static napi_value init(napi_env env, napi_value exports)
         {"synthFrame", NULL, js_synth_frame, NULL, NULL, NULL, napi_default, NULL},
         {"frameLayout", NULL, js_frame_layout, NULL, NULL, NULL, napi_default, NULL},
         {"fpsMap", NULL, js_fps_map, NULL, NULL, NULL, napi_default, NULL},
+        {"hostAlloc", NULL, js_host_alloc, NULL, NULL, NULL, napi_default, NULL},
         {"quality", NULL, js_quality, NULL, NULL, NULL, napi_default, NULL},
         {"qstatStream", NULL, js_qstat_stream, NULL, NULL, NULL, napi_default, NULL},
     };

@@ -211,13 +211,16 @@ struct dts_graph {
     uint8_t *pin_in[2] = {nullptr, nullptr}, *pin_out[2] = {nullptr, nullptr};
     dts_qraw *pin_qraw[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
+    hipEvent_t kdone[2] = {nullptr, nullptr};  // the slot's kernels are done (its D2H may start)
+    hipStream_t d2h = nullptr;            // the host path's device -> host copies (both slots), so a
+                                          // chunk's D2H runs beside the next chunk's H2D
     int64_t pin_in_bytes = 0, pin_out_bytes = 0;
     // pending host submit
     bool pending = false;
     const dts_frame *p_dst = nullptr;
     dts_qstat *p_q = nullptr;
     int p_chunk_first[2] = {-1, -1}, p_chunk_n[2] = {0, 0};
-    bool p_zout[2] = {false, false};      // the slot's outputs went straight into pinned caller frames
+    uint32_t p_zout[2] = {0, 0};          // bit k: the slot's output k went straight into pinned caller frames
     // HDR10 -> SDR: per output a p010 intermediate of `batch` frames, double-buffered
     // (an event per buffer orders reuse across the host path's two streams)
     bool hdr = false;
@@ -1847,6 +1850,8 @@ static void free_host_path(dts_graph *g)
         if (g->pin_out[sl]) hipHostFree(g->pin_out[sl]);
         if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
         if (g->done[sl]) hipEventDestroy(g->done[sl]);
+        if (g->kdone[sl]) hipEventDestroy(g->kdone[sl]);
+        g->kdone[sl] = nullptr;
         g->dev_src[sl] = g->dev_q[sl] = nullptr;
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) g->dev_out[sl][k] = nullptr;
         g->dev_qraw[sl] = g->pin_qraw[sl] = nullptr;
@@ -1854,6 +1859,8 @@ static void free_host_path(dts_graph *g)
         g->done[sl] = nullptr;
         g->p_chunk_first[sl] = -1;
     }
+    if (g->d2h) hipStreamDestroy(g->d2h);
+    g->d2h = nullptr;
     g->host_ready = false;
 }
 
@@ -1882,26 +1889,28 @@ bool pinned_range(const void *ptr, size_t n)
     --it;
     return a >= it->first && a + n <= it->first + it->second.first;
 }
-// every plane of frame f (layout lay: rows x row bytes) lies in pinned memory
-bool frame_pinned(const dts_frame &f, const DevLayout &lay)
+// frame f can move by plain DMA: every plane (layout lay: rows x row bytes) lies in pinned
+// memory with the device layout's pitch, so each plane crosses as one contiguous copy.  (Pitched
+// 2-D copies between host and device measured ~2 GB/s on the box -- 150 fps for cfg2 -- so frames
+// with other pitches take the pinned ring.)
+bool frame_direct(const dts_frame &f, const DevLayout &lay)
 {
     for (int p = 0; p < 3; ++p) {
         if (!lay.rows[p]) continue;
-        if (!f.data[p] || f.pitch[p] < lay.rowb[p]) return false;
+        if (!f.data[p] || f.pitch[p] != lay.pitch[p]) return false;
         if (!pinned_range(f.data[p], (size_t)((lay.rows[p] - 1) * f.pitch[p] + lay.rowb[p]))) return false;
     }
     return true;
 }
-// one frame between a caller frame in pinned memory and frame `i` of a device batch (DMA, 2-D per plane)
+// one frame between a caller frame in pinned memory and a frame of a device batch: one
+// contiguous DMA per plane (frame_direct)
 hipError_t copy_frame_direct(uint8_t *dev, const DevLayout &lay, const dts_frame &f, bool h2d, hipStream_t st)
 {
     for (int p = 0; p < 3; ++p) {
         if (!lay.rows[p]) continue;
-        const hipError_t e =
-            h2d ? hipMemcpy2DAsync(dev + lay.off[p], (size_t)lay.pitch[p], f.data[p], (size_t)f.pitch[p], (size_t)lay.rowb[p],
-                                   (size_t)lay.rows[p], hipMemcpyHostToDevice, st)
-                : hipMemcpy2DAsync(f.data[p], (size_t)f.pitch[p], dev + lay.off[p], (size_t)lay.pitch[p], (size_t)lay.rowb[p],
-                                   (size_t)lay.rows[p], hipMemcpyDeviceToHost, st);
+        const size_t nb = (size_t)((lay.rows[p] - 1) * lay.pitch[p] + lay.rowb[p]);
+        const hipError_t e = h2d ? hipMemcpyAsync(dev + lay.off[p], f.data[p], nb, hipMemcpyHostToDevice, st)
+                                 : hipMemcpyAsync(f.data[p], dev + lay.off[p], nb, hipMemcpyDeviceToHost, st);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1953,7 +1962,9 @@ static int alloc_host_path(dts_graph *g)
         HIPCHK(ctx, hipHostMalloc(&g->pin_in[sl], (size_t)g->pin_in_bytes, hipHostMallocDefault));
         HIPCHK(ctx, hipHostMalloc(&g->pin_out[sl], (size_t)g->pin_out_bytes, hipHostMallocDefault));
         HIPCHK(ctx, hipEventCreateWithFlags(&g->done[sl], hipEventDisableTiming));
+        HIPCHK(ctx, hipEventCreateWithFlags(&g->kdone[sl], hipEventDisableTiming));
     }
+    HIPCHK(ctx, hipStreamCreateWithFlags(&g->d2h, hipStreamNonBlocking));
     return DTS_OK;
 }
 
@@ -2022,8 +2033,9 @@ static int finish_slot(dts_graph *g, int sl)
     HIPCHK(ctx, hipEventSynchronize(g->done[sl]));
     const int f0 = g->p_chunk_first[sl], n = g->p_chunk_n[sl];
     const uint8_t *hp0 = g->pin_out[sl];         // per output: a region of `batch` packed frames
-    if (!g->p_zout[sl]) parallel_for(n * s.nout, [&](int i) {
+    if (g->p_zout[sl] != (1u << s.nout) - 1) parallel_for(n * s.nout, [&](int i) {
         const int f = i / s.nout, k = i % s.nout;
+        if ((g->p_zout[sl] >> k) & 1) return;                      // (went straight into the caller's frame)
         const uint8_t *hp = hp0;
         for (int kk = 0; kk < k; ++kk) hp += (int64_t)g->batch * g->lay_out[kk].fstride;
         unpack_frame(hp + (int64_t)f * g->lay_out[k].fstride, g->p_dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
@@ -2078,8 +2090,8 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             // frames in pinned memory (dts_host_alloc / dts_host_register) go to the device by DMA
             // straight from the caller's planes; others are packed into the pinned ring first
             bool zin = true;
-            for (int f = 0; f < n + cf && zin; ++f) zin = frame_pinned(src[f0 + f], g->lay_src);
-            for (int f = 0; f < n && zin && s.quality; ++f) zin = frame_pinned(qref[f0 + f], g->lay_q);
+            for (int f = 0; f < n + cf && zin; ++f) zin = frame_direct(src[f0 + f], g->lay_src);
+            for (int f = 0; f < n && zin && s.quality; ++f) zin = frame_direct(qref[f0 + f], g->lay_q);
             if (zin) {
                 for (int f = 0; f < n + cf; ++f)
                     HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_src[sl]) + (int64_t)f * g->lay_src.fstride,
@@ -2108,20 +2120,27 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             e = run_device(g, g->hqs[sl], &dsrc, n, ddst, s.quality ? &dq : nullptr,
                            (s.quality || g->ref) ? g->dev_qraw[sl] : nullptr, st);
             if (e) return e;
-            bool zout = true;
-            for (int f = 0; f < n && zout; ++f)
-                for (int k = 0; k < s.nout && zout; ++k) zout = frame_pinned(dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
-            if (zout) {                          // straight into the caller's pinned frames
-                for (int f = 0; f < n; ++f)
-                    for (int k = 0; k < s.nout; ++k)
+            // the results leave on the D2H stream once the slot's kernels are done, beside the next
+            // chunk's H2D on the other slot's stream (the two directions of the link at once); the
+            // slot's buffers are reused only after finish_slot has waited for done[sl]
+            HIPCHK(ctx, hipEventRecord(g->kdone[sl], st));
+            HIPCHK(ctx, hipStreamWaitEvent(g->d2h, g->kdone[sl], 0));
+            st = g->d2h;
+            // per output: straight into the caller's pinned frames, or through the pinned ring
+            uint32_t zout = 0;
+            uint8_t *op = g->pin_out[sl];
+            for (int k = 0; k < s.nout; ++k) {
+                bool z = true;
+                for (int f = 0; f < n && z; ++f) z = frame_direct(dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
+                if (z) {
+                    zout |= 1u << k;
+                    for (int f = 0; f < n; ++f)
                         HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_out[sl][k]) + (int64_t)f * g->lay_out[k].fstride,
                                                       g->lay_out[k], dst[(int64_t)(f0 + f) * s.nout + k], false, st));
-            } else {
-                uint8_t *op = g->pin_out[sl];
-                for (int k = 0; k < s.nout; ++k) {
+                } else {
                     HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
-                    op += (int64_t)B * g->lay_out[k].fstride;
                 }
+                op += (int64_t)B * g->lay_out[k].fstride;
             }
             g->p_zout[sl] = zout;
             if (s.quality || g->ref)

@@ -231,21 +231,23 @@ class PinnedBuffer:
             self.ptr = None
 
 
-def alloc_frames_pinned(w, h, fmt, n):
+def alloc_frames_pinned(w, h, fmt, n, pitch_align=16):
     """n frames of (w, h, fmt) in one pinned buffer: ([planes per frame], the PinnedBuffer,
-    which must outlive the frames)."""
+    which must outlive the frames).  Row pitches are rounded up to pitch_align bytes: with 16
+    (the host path's device layout) every plane crosses PCIe as one DMA (ABI 7)."""
     shapes = plane_shapes(w, h, fmt)
-    fb = sum(s[0] * s[1] for s in shapes if s is not None)
+    pitches = [None if s is None else (s[1] + pitch_align - 1) // pitch_align * pitch_align for s in shapes]
+    fb = sum(s[0] * p for s, p in zip(shapes, pitches) if s is not None)
     buf = PinnedBuffer(max(1, fb * n))
     frames = []
     for i in range(n):
         off, planes = i * fb, []
-        for s in shapes:
+        for s, p in zip(shapes, pitches):
             if s is None:
                 planes.append(None)
                 continue
-            planes.append(buf.array[off:off + s[0] * s[1]].reshape(s[0], s[1]))
-            off += s[0] * s[1]
+            planes.append(buf.array[off:off + s[0] * p].reshape(s[0], p)[:, :s[1]])
+            off += s[0] * p
         frames.append(planes)
     return frames, buf
 
@@ -427,13 +429,15 @@ class Graph:
         """frames: list of source frames (plane lists; with deint, n + 2 of them: one
         context frame each side).  Returns (outputs, qstats): outputs[f][k] is output
         k of frame f as a plane list.  pinned_out: the outputs are allocated with
-        dts_host_alloc (the library DMAs straight into them; ABI 7)."""
+        dts_host_alloc (the library DMAs straight into them; ABI 7); an int is the outputs'
+        row-pitch alignment (16, the default for True: every plane direct)."""
         s = self.spec
         ns = len(frames)
         n = ns - 2 if s.deint else ns
         src = (Frame * ns)(*[frame_struct(f) for f in frames])
         if pinned_out:
-            per = [alloc_frames_pinned(s.out[k].w, s.out[k].h, s.out[k].fmt, n) for k in range(s.nout)]
+            pa = 16 if pinned_out is True else int(pinned_out)
+            per = [alloc_frames_pinned(s.out[k].w, s.out[k].h, s.out[k].fmt, n, pa) for k in range(s.nout)]
             self._pinned_keep = [b for (_f, b) in per]
             outs = [[per[k][0][f] for k in range(s.nout)] for f in range(n)]
         else:

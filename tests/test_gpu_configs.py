@@ -87,13 +87,17 @@ def test_cfg2_ladder_4k_host_path_two_frames(ctx):
     g.close()
 
 
-@pytest.mark.parametrize("pin_src,pin_out", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("pin_src,pin_out", [(True, 16), (True, False), (False, 1)])
 def test_host_path_pinned_frames(ctx, pin_src, pin_out):
     """ABI 7: frames in dts_host_alloc memory go to / come from the device by DMA straight
     from / into the caller's planes (no pass through the pinned rings); every combination
-    of pinned and pageable sources / outputs over several chunks is bit-exact."""
+    of pinned and pageable sources / outputs over several chunks is bit-exact; with pinned
+    outputs packed at their row bytes (pin_out 1) the 86 x 48 rendition's 86-byte rows differ
+    from the device layout's 96-byte pitch, so that rendition goes through the ring and the
+    others straight into the caller's frames."""
     sw, sh, n, batch = 384, 216, 7, 3
-    outs_spec = [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC), (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS)]
+    outs_spec = [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC), (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS),
+                 (86, 48, D.FMT_NV12, D.SCALE_BICUBIC)]
     frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, 77, f) for f in range(n)]
     keep = None
     if pin_src:

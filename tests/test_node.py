@@ -433,3 +433,41 @@ def test_worker_gpu_ffmpeg_decode_encode(tmp_path):
     log = [json.loads(x) for x in (tmp_path / "argv.log").read_text().splitlines()]
     assert any("-i" in a and str(src) in a for a in log)           # the decoder child
     assert sum(1 for a in log if "concat" in a) == 2               # one concat per job
+
+
+@pytest.mark.gpu
+def test_addon_pinned_frames(tmp_path):
+    """addon.hostAlloc (ABI 7): frames carved from pinned Buffers (pitches rounded to 16) go
+    through run() by direct DMA and give the same bytes as pageable frames."""
+    addon = os.path.join(ROOT, "distributed-transcoding-server_amd", "addon", "dts_napi.node")
+    script = r"""
+const a = require(%s);
+const ctx = a.createContext(0);
+const W = 384, H = 216, w = 192, h = 108, N = 5;
+const g = a.createGraph(ctx, {src: {w: W, h: H, fmt: 0}, outputs: [{w: w, h: h, fmt: 1, method: 4}], maxBatch: 2});
+function frame(buf, off, fw, fh, fmt) {         // planes at pitches rounded up to 16 bytes
+  const cw = (fw + 1) >> 1, ch = (fh + 1) >> 1, r16 = function (x) { return (x + 15) & ~15; };
+  const rows = fmt === 0 ? [[fh, fw], [ch, cw], [ch, cw]] : [[fh, fw], [ch, 2 * cw]];
+  const data = [], pitch = [];
+  rows.forEach(function (r) { const p = r16(r[1]); data.push(buf.subarray(off, off + p * r[0])); pitch.push(p); off += p * r[0]; });
+  if (fmt !== 0) { data.push(null); pitch.push(0); }
+  return {data: data, pitch: pitch, end: off};
+}
+function frames(alloc, fw, fh, fmt, n) {
+  const one = frame(Buffer.alloc(1 << 24), 0, fw, fh, fmt).end, buf = alloc(one * n), out = [];
+  for (let i = 0; i < n; ++i) out.push(frame(buf, i * one, fw, fh, fmt));
+  return out;
+}
+const pinned = function (n) { return a.hostAlloc(n); }, plain = function (n) { return Buffer.alloc(n); };
+const srcP = frames(pinned, W, H, 0, N), srcQ = frames(plain, W, H, 0, N);
+for (let i = 0; i < N; ++i) { a.synthFrame(W, H, 0, 0, 9, i, srcP[i]); a.synthFrame(W, H, 0, 0, 9, i, srcQ[i]); }
+const dstP = frames(pinned, w, h, 1, N), dstQ = frames(plain, w, h, 1, N);
+a.run(g, srcP, dstP, null).then(function () { return a.run(g, srcQ, dstQ, null); }).then(function () {
+  let same = true;
+  for (let i = 0; i < N; ++i) for (let p = 0; p < 2; ++p) same = same && dstP[i].data[p].equals(dstQ[i].data[p]);
+  console.log(JSON.stringify({same: same}));
+});
+""" % json.dumps(addon)
+    r = subprocess.run([NODE, "-e", script], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip().split("\n")[-1]) == {"same": True}
