@@ -662,8 +662,15 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
     __shared__ unsigned long long red_e[2][kThreads / 64];
     const int t = threadIdx.x;
     const int total = P.tile_base[3];
-    const int frame = blockIdx.x / ngt;
-    const int gt = gt0 + blockIdx.x % ngt;
+    // XCD-aware order (round 5): workgroup b runs on XCD b % 8, and item e = (b % 8) per + b / 8
+    // gives each XCD a contiguous run of (frame, tile) items, so a strip's neighbours run beside it
+    // on the same L2 and its apron column (the first block of the next strip: a 128-byte line per
+    // row read for 4 bytes) is an L2 hit rather than a third line fetched per 256-byte strip row
+    const int nitems = P.nframes * ngt, per = (nitems + 7) >> 3;
+    const int e = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+    if (e >= nitems) return;
+    const int frame = e / ngt;
+    const int gt = gt0 + e % ngt;
     const int plane = gt >= P.tile_base[2] ? 2 : (gt >= P.tile_base[1] ? 1 : 0);
     const int tile = gt - P.tile_base[plane];
     const int tx = tile % P.tiles_x[plane], tw = tile / P.tiles_x[plane];
@@ -919,14 +926,14 @@ hipError_t launch_qsum(const dts_qraw *raw, int n, dts_qraw *sum, hipStream_t s)
 
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s)
 {
+    auto grid = [&](int ngt) { return dim3((unsigned)(8 * ((ngt * p.nframes + 7) / 8))); };   // (k_quality: XCD order)
     if (!p.interleaved) {
-        hipLaunchKernelGGL(k_quality<false>, dim3((unsigned)(total_tiles * p.nframes)), dim3(kThreads), 0, s, p, 0,
-                           total_tiles);
+        hipLaunchKernelGGL(k_quality<false>, grid(total_tiles), dim3(kThreads), 0, s, p, 0, total_tiles);
     } else {                                        // nv12: plane 1's workgroups score plane 2 as well
         const int nl = p.tile_base[1], nc = p.tile_base[2] - p.tile_base[1];
-        hipLaunchKernelGGL(k_quality<false>, dim3((unsigned)(nl * p.nframes)), dim3(kThreads), 0, s, p, 0, nl);
+        hipLaunchKernelGGL(k_quality<false>, grid(nl), dim3(kThreads), 0, s, p, 0, nl);
         if (nc > 0 && hipPeekAtLastError() == hipSuccess)
-            hipLaunchKernelGGL(k_quality<true>, dim3((unsigned)(nc * p.nframes)), dim3(kThreads), 0, s, p, nl, nc);
+            hipLaunchKernelGGL(k_quality<true>, grid(nc), dim3(kThreads), 0, s, p, nl, nc);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
