@@ -212,6 +212,7 @@ struct dts_graph {
     dts_qraw *pin_qraw[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     hipEvent_t kdone[2] = {nullptr, nullptr};  // the slot's kernels are done (its D2H may start)
+    hipEvent_t h2d_done[2] = {nullptr, nullptr};  // the slot's inputs have crossed (its ring may refill)
     hipStream_t d2h = nullptr;            // the host path's device -> host copies (both slots), so a
                                           // chunk's D2H runs beside the next chunk's H2D
     int64_t pin_in_bytes = 0, pin_out_bytes = 0;
@@ -1851,7 +1852,8 @@ static void free_host_path(dts_graph *g)
         if (g->pin_qraw[sl]) hipHostFree(g->pin_qraw[sl]);
         if (g->done[sl]) hipEventDestroy(g->done[sl]);
         if (g->kdone[sl]) hipEventDestroy(g->kdone[sl]);
-        g->kdone[sl] = nullptr;
+        if (g->h2d_done[sl]) hipEventDestroy(g->h2d_done[sl]);
+        g->done[sl] = g->kdone[sl] = g->h2d_done[sl] = nullptr;
         g->dev_src[sl] = g->dev_q[sl] = nullptr;
         for (int k = 0; k < DTS_MAX_OUTPUTS; ++k) g->dev_out[sl][k] = nullptr;
         g->dev_qraw[sl] = g->pin_qraw[sl] = nullptr;
@@ -1902,15 +1904,55 @@ bool frame_direct(const dts_frame &f, const DevLayout &lay)
     }
     return true;
 }
-// one frame between a caller frame in pinned memory and a frame of a device batch: one
-// contiguous DMA per plane (frame_direct)
-hipError_t copy_frame_direct(uint8_t *dev, const DevLayout &lay, const dts_frame &f, bool h2d, hipStream_t st)
+// bytes of one frame image in layout lay, from plane 0 to the last byte of the last plane
+int64_t image_bytes(const DevLayout &lay)
 {
-    for (int p = 0; p < 3; ++p) {
-        if (!lay.rows[p]) continue;
-        const size_t nb = (size_t)((lay.rows[p] - 1) * lay.pitch[p] + lay.rowb[p]);
-        const hipError_t e = h2d ? hipMemcpyAsync(dev + lay.off[p], f.data[p], nb, hipMemcpyHostToDevice, st)
-                                 : hipMemcpyAsync(f.data[p], dev + lay.off[p], nb, hipMemcpyDeviceToHost, st);
+    int64_t e = 0;
+    for (int p = 0; p < 3; ++p)
+        if (lay.rows[p]) e = std::max(e, lay.off[p] + (lay.rows[p] - 1) * lay.pitch[p] + lay.rowb[p]);
+    return e;
+}
+// frame f's planes sit at base + lay.off[p] with the layout's pitches: the frame is the
+// device frame's image byte for byte
+bool same_image(const dts_frame &f, const DevLayout &lay, const uint8_t *base)
+{
+    for (int p = 0; p < 3; ++p)
+        if (lay.rows[p] && (f.data[p] != base + lay.off[p] || f.pitch[p] != lay.pitch[p])) return false;
+    return true;
+}
+// Frames fr[0], fr[step], .. (n of them) in pinned memory between a device batch's frames
+// dev, dev + fstride, ..: runs of frames laid out exactly as the batch (one image after another,
+// fstride apart: dtsffi.alloc_frames_pinned) cross as one DMA per run, every other frame as one
+// DMA per plane (frame_direct).  (Per-plane copies of 1-4 MB each cost ~10 % of the link rate in
+// per-copy overhead on the box: cfg2 3.2 k against 3.6 k fps through the pinned ring.)
+hipError_t copy_frames_direct(uint8_t *dev, const DevLayout &lay, const dts_frame *fr, int64_t step, int n, bool h2d,
+                              hipStream_t st)
+{
+    const int64_t img = image_bytes(lay);
+    for (int f = 0; f < n;) {
+        const uint8_t *b0 = static_cast<const uint8_t *>(fr[f * step].data[0]) - lay.off[0];
+        int m = 0;
+        while (f + m < n && same_image(fr[(f + m) * step], lay, b0 + (int64_t)m * lay.fstride)) ++m;
+        while (m > 1 && !pinned_range(b0, (size_t)((m - 1) * lay.fstride + img))) m = 1;
+        hipError_t e;
+        if (m > 1) {
+            const size_t nb = (size_t)((m - 1) * lay.fstride + img);
+            uint8_t *d = dev + (int64_t)f * lay.fstride;
+            e = h2d ? hipMemcpyAsync(d, b0, nb, hipMemcpyHostToDevice, st)
+                    : hipMemcpyAsync(const_cast<uint8_t *>(b0), d, nb, hipMemcpyDeviceToHost, st);
+            f += m;
+        } else {
+            const dts_frame &fm = fr[f * step];
+            uint8_t *d = dev + (int64_t)f * lay.fstride;
+            e = hipSuccess;
+            for (int p = 0; p < 3 && e == hipSuccess; ++p) {
+                if (!lay.rows[p]) continue;
+                const size_t nb = (size_t)((lay.rows[p] - 1) * lay.pitch[p] + lay.rowb[p]);
+                e = h2d ? hipMemcpyAsync(d + lay.off[p], fm.data[p], nb, hipMemcpyHostToDevice, st)
+                        : hipMemcpyAsync(fm.data[p], d + lay.off[p], nb, hipMemcpyDeviceToHost, st);
+            }
+            ++f;
+        }
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1963,6 +2005,7 @@ static int alloc_host_path(dts_graph *g)
         HIPCHK(ctx, hipHostMalloc(&g->pin_out[sl], (size_t)g->pin_out_bytes, hipHostMallocDefault));
         HIPCHK(ctx, hipEventCreateWithFlags(&g->done[sl], hipEventDisableTiming));
         HIPCHK(ctx, hipEventCreateWithFlags(&g->kdone[sl], hipEventDisableTiming));
+        HIPCHK(ctx, hipEventCreateWithFlags(&g->h2d_done[sl], hipEventDisableTiming));
     }
     HIPCHK(ctx, hipStreamCreateWithFlags(&g->d2h, hipStreamNonBlocking));
     return DTS_OK;
@@ -2082,8 +2125,11 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
         for (int f0 = 0; f0 < nframes; f0 += B, ++chunk) {
             const int sl = chunk & 1;
             const int n = std::min(B, nframes - f0);
-            e = finish_slot(g, sl);              // slot reuse: drain chunk-2 first
-            if (e) return e;
+            // Slot reuse without a host stall before the inputs go out: the input ring only waits
+            // for chunk c - 2's H2D (h2d_done), the slot's device inputs for its kernels (stream
+            // order), its device outputs for its D2H (done, on the device), and chunk c - 2's
+            // results are handed over (finish_slot) only before this chunk's D2H reuses the output
+            // ring -- so chunk c's H2D is queued while c - 2's results are still crossing
             hipStream_t st = ctx->stream[sl];
             uint8_t *hp = g->pin_in[sl];
             const int cf = s.deint ? 2 : 0;              // deint: src[f0 .. f0 + n + 1] (context frames)
@@ -2092,10 +2138,10 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             bool zin = true;
             for (int f = 0; f < n + cf && zin; ++f) zin = frame_direct(src[f0 + f], g->lay_src);
             for (int f = 0; f < n && zin && s.quality; ++f) zin = frame_direct(qref[f0 + f], g->lay_q);
+            if (!zin) HIPCHK(ctx, hipEventSynchronize(g->h2d_done[sl]));   // the input ring refills
             if (zin) {
-                for (int f = 0; f < n + cf; ++f)
-                    HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_src[sl]) + (int64_t)f * g->lay_src.fstride,
-                                                  g->lay_src, src[f0 + f], true, st));
+                HIPCHK(ctx, copy_frames_direct(static_cast<uint8_t *>(g->dev_src[sl]), g->lay_src, src + f0, 1, n + cf,
+                                               true, st));
             } else {
                 parallel_for(n + cf, [&](int f) {
                     pack_frame(hp + (int64_t)f * g->lay_src.fstride, src[f0 + f], g->lay_src);
@@ -2104,15 +2150,15 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
             }
             uint8_t *qhp = hp + (int64_t)(B + cf) * g->lay_src.fstride;
             if (s.quality && zin) {
-                for (int f = 0; f < n; ++f)
-                    HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_q[sl]) + (int64_t)f * g->lay_q.fstride, g->lay_q,
-                                                  qref[f0 + f], true, st));
+                HIPCHK(ctx, copy_frames_direct(static_cast<uint8_t *>(g->dev_q[sl]), g->lay_q, qref + f0, 1, n, true, st));
             } else if (s.quality) {
                 parallel_for(n, [&](int f) {
                     pack_frame(qhp + (int64_t)f * g->lay_q.fstride, qref[f0 + f], g->lay_q);
                 });
                 HIPCHK(ctx, copy_frames(g->dev_q[sl], g->lay_q, qhp, n, true, st));
             }
+            HIPCHK(ctx, hipEventRecord(g->h2d_done[sl], st));
+            HIPCHK(ctx, hipStreamWaitEvent(st, g->done[sl], 0));    // chunk c - 2's outputs have left
             dts_dev_frames dsrc = dev_frames(g->dev_src[sl], g->lay_src);
             dts_dev_frames ddst[DTS_MAX_OUTPUTS];
             for (int k = 0; k < s.nout; ++k) ddst[k] = dev_frames(g->dev_out[sl][k], g->lay_out[k]);
@@ -2121,10 +2167,11 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
                            (s.quality || g->ref) ? g->dev_qraw[sl] : nullptr, st);
             if (e) return e;
             // the results leave on the D2H stream once the slot's kernels are done, beside the next
-            // chunk's H2D on the other slot's stream (the two directions of the link at once); the
-            // slot's buffers are reused only after finish_slot has waited for done[sl]
+            // chunks' H2D (the two directions of the link at once)
             HIPCHK(ctx, hipEventRecord(g->kdone[sl], st));
             HIPCHK(ctx, hipStreamWaitEvent(g->d2h, g->kdone[sl], 0));
+            e = finish_slot(g, sl);              // chunk c - 2's results out of the output ring
+            if (e) return e;
             st = g->d2h;
             // per output: straight into the caller's pinned frames, or through the pinned ring
             uint32_t zout = 0;
@@ -2134,9 +2181,8 @@ int dts_graph_submit(dts_graph *g, const dts_frame *src, int nframes, const dts_
                 for (int f = 0; f < n && z; ++f) z = frame_direct(dst[(int64_t)(f0 + f) * s.nout + k], g->lay_out[k]);
                 if (z) {
                     zout |= 1u << k;
-                    for (int f = 0; f < n; ++f)
-                        HIPCHK(ctx, copy_frame_direct(static_cast<uint8_t *>(g->dev_out[sl][k]) + (int64_t)f * g->lay_out[k].fstride,
-                                                      g->lay_out[k], dst[(int64_t)(f0 + f) * s.nout + k], false, st));
+                    HIPCHK(ctx, copy_frames_direct(static_cast<uint8_t *>(g->dev_out[sl][k]), g->lay_out[k],
+                                                   dst + (int64_t)f0 * s.nout + k, s.nout, n, false, st));
                 } else {
                     HIPCHK(ctx, copy_frames(g->dev_out[sl][k], g->lay_out[k], op, n, false, st));
                 }

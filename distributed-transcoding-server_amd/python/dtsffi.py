@@ -233,21 +233,23 @@ class PinnedBuffer:
 
 def alloc_frames_pinned(w, h, fmt, n, pitch_align=16):
     """n frames of (w, h, fmt) in one pinned buffer: ([planes per frame], the PinnedBuffer,
-    which must outlive the frames).  Row pitches are rounded up to pitch_align bytes: with 16
-    (the host path's device layout) every plane crosses PCIe as one DMA (ABI 7)."""
+    which must outlive the frames).  Row pitches are rounded up to pitch_align bytes and planes
+    to 256: with 16 this is the host path's device batch layout (api.cpp DevLayout, tight), so
+    every plane crosses PCIe by DMA and consecutive frames of the buffer as one DMA (ABI 7)."""
     shapes = plane_shapes(w, h, fmt)
     pitches = [None if s is None else (s[1] + pitch_align - 1) // pitch_align * pitch_align for s in shapes]
-    fb = sum(s[0] * p for s, p in zip(shapes, pitches) if s is not None)
+    sizes = [0 if s is None else (s[0] * p + 255) // 256 * 256 for s, p in zip(shapes, pitches)]
+    fb = sum(sizes)
     buf = PinnedBuffer(max(1, fb * n))
     frames = []
     for i in range(n):
         off, planes = i * fb, []
-        for s, p in zip(shapes, pitches):
+        for s, p, z in zip(shapes, pitches, sizes):
             if s is None:
                 planes.append(None)
                 continue
             planes.append(buf.array[off:off + s[0] * p].reshape(s[0], p)[:, :s[1]])
-            off += s[0] * p
+            off += z
         frames.append(planes)
     return frames, buf
 

@@ -87,14 +87,16 @@ def test_cfg2_ladder_4k_host_path_two_frames(ctx):
     g.close()
 
 
-@pytest.mark.parametrize("pin_src,pin_out", [(True, 16), (True, False), (False, 1)])
+@pytest.mark.parametrize("pin_src,pin_out", [(True, 16), (True, False), (False, 1), ("perm", 16)])
 def test_host_path_pinned_frames(ctx, pin_src, pin_out):
     """ABI 7: frames in dts_host_alloc memory go to / come from the device by DMA straight
     from / into the caller's planes (no pass through the pinned rings); every combination
     of pinned and pageable sources / outputs over several chunks is bit-exact; with pinned
     outputs packed at their row bytes (pin_out 1) the 86 x 48 rendition's 86-byte rows differ
     from the device layout's 96-byte pitch, so that rendition goes through the ring and the
-    others straight into the caller's frames."""
+    others straight into the caller's frames.  Consecutive frames of one alloc_frames_pinned
+    buffer cross as one DMA per run; "perm" hands the pinned frames over out of buffer order,
+    so runs break (single frames by plane, a two-frame run at the end)."""
     sw, sh, n, batch = 384, 216, 7, 3
     outs_spec = [(192, 108, D.FMT_NV12, D.SCALE_BICUBIC), (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS),
                  (86, 48, D.FMT_NV12, D.SCALE_BICUBIC)]
@@ -107,6 +109,8 @@ def test_host_path_pinned_frames(ctx, pin_src, pin_out):
                 if pa is not None:
                     pa[...] = pb
         frames = pf
+        if pin_src == "perm":
+            frames = [pf[i] for i in (1, 0, 2, 4, 3, 5, 6)]
     g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, outs_spec, max_batch=batch))
     for _rep in range(2):
         outs, _ = g.run_host(frames, pinned_out=pin_out)
