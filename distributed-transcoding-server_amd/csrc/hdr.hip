@@ -404,6 +404,17 @@ __device__ __forceinline__ float2 cdec(uint32_t v)   // one p010 (Cb, Cr) pair, 
     return make_float2((float)((int)((v & 0xffffu) >> 6) - 512) * (1.f / 896.f), (float)((int)(v >> 22) - 512) * (1.f / 896.f));
 }
 
+// a plane of this frame as a buffer resource (wave-uniform base and size): the row offsets of a
+// step are scalar (soffset) and each lane's column offset is fixed for the walk (voffset), so no
+// vector address arithmetic is left in the loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(uint64_t base, int64_t bytes)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
 template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams P, int nstrips, int nchunks)
 {
@@ -412,7 +423,7 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
     for (int i = threadIdx.x; i < kTabs * (kTmLutN + 1); i += 64 * kTwWaves) tl[i] = P.lut[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int item = blockIdx.x * kTwWaves + (threadIdx.x >> 6);
+    const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kTwWaves + (threadIdx.x >> 6)));
     if (item >= nstrips * nchunks) return;
     const int strip = item % nstrips, chunk = item / nstrips, f = blockIdx.z;
     const int cw = P.w >> 1, ch = P.h >> 1;
@@ -428,20 +439,37 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
     const int jA = cxc, jB = min(cxc + 1, cw - 1);
     const bool lsplit = cx >= 0;                             // two luma samples (else column 0 twice)
     const uint64_t sf = (uint64_t)f * P.src.fstride, df = (uint64_t)f * P.dst.fstride;
-    const uint64_t sy0 = P.src.data[0] + sf, sc0 = P.src.data[1] + sf;
-    const int64_t lp = P.src.pitch[0], cp = P.src.pitch[1];
-    const uint64_t lcol = 2 * (uint64_t)xL;                  // byte of xL in a luma row (xR follows it)
+    const int lp = (int)P.src.pitch[0], cp = (int)P.src.pitch[1];
+    const __amdgpu_buffer_rsrc_t rY = plane_rsrc(P.src.data[0] + sf, (int64_t)lp * P.h);
+    const __amdgpu_buffer_rsrc_t rC = plane_rsrc(P.src.data[1] + sf, (int64_t)cp * ch);
+    const int dp0 = (int)P.dst.pitch[0], dp1 = (int)P.dst.pitch[1], dp2 = (int)P.dst.pitch[2];
+    const bool nv12 = P.dst_fmt == DTS_FMT_NV12;
+    const __amdgpu_buffer_rsrc_t wY = plane_rsrc(P.dst.data[0] + df, (int64_t)dp0 * P.h);
+    const __amdgpu_buffer_rsrc_t wU = plane_rsrc(P.dst.data[1] + df, (int64_t)dp1 * ch);
+    const __amdgpu_buffer_rsrc_t wV = plane_rsrc(P.dst.data[nv12 ? 1 : 2] + df, (int64_t)(nv12 ? dp1 : dp2) * ch);
+    const int oA = 4 * jA, oB = 4 * jB, oL = 2 * xL;        // this lane's byte in a chroma / luma row
     auto crow = [&](int r, uint32_t &a, uint32_t &b) {     // chroma row r (clamped), columns jA, jB
-        const uint64_t rb = sc0 + (uint64_t)min(max(r, 0), ch - 1) * cp;
-        a = gld<uint32_t>(rb + 4 * (uint64_t)jA);
-        b = gld<uint32_t>(rb + 4 * (uint64_t)jB);
+        const int so = min(max(r, 0), ch - 1) * cp;
+        a = __builtin_amdgcn_raw_buffer_load_b32(rC, oA, so, 0);
+        b = __builtin_amdgcn_raw_buffer_load_b32(rC, oB, so, 0);
     };
-    auto lrow = [&](int y) -> uint32_t { return gld<uint32_t>(sy0 + (uint64_t)y * lp + lcol); };
+    auto lrow = [&](int y) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(rY, oL, y * lp, 0); };
     const int s0 = r0 > 0 ? r0 - 1 : 0, s1 = r1 < ch ? r1 : ch - 1;
-    // carried chroma input rows (s - 1, s) and the next row / luma, loaded a step ahead
-    uint32_t mA, mB, aA, aB, pA, pB, l0, l1;
-    crow(s0 - 1, mA, mB);
-    crow(s0, aA, aB);
+    // chroma input rows s - 1 (m) and s (a) carried decoded and interpolated to column cx + 1/2
+    // (the h values), row s + 1 (p) and the block's luma loaded raw a step ahead
+    uint32_t pA, pB, l0, l1;
+    float2 m0, mh, a0, ah;
+    {
+        uint32_t xA, xB;
+        crow(s0 - 1, xA, xB);
+        const float2 u0 = cdec(xA), u1 = cdec(xB);
+        m0 = u0;
+        mh = make_float2(u0.x + fx * (u1.x - u0.x), u0.y + fx * (u1.y - u0.y));
+        crow(s0, xA, xB);
+        const float2 v0 = cdec(xA), v1 = cdec(xB);
+        a0 = v0;
+        ah = make_float2(v0.x + fx * (v1.x - v0.x), v0.y + fx * (v1.y - v0.y));
+    }
     crow(s0 + 1, pA, pB);
     l0 = lrow(2 * s0);
     l1 = lrow(2 * s0 + 1);
@@ -453,7 +481,7 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
         return make_float2(0.25f * l.x + 0.5f * m.x + 0.25f * r.x, 0.25f * l.y + 0.5f * m.y + 0.25f * r.y);
     };
     auto emit = [&](int by, float2 a, float2 b, float2 c, float2 d) {
-        if (!out_col || by < r0 || by >= r1) return;
+        if (by < r0 || by >= r1) return;
         const float2 h[4] = {a, b, c, d};
         float sb = 0.f, sr = 0.f;
 #pragma unroll
@@ -462,43 +490,42 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
             sr += wy[k] * h[k].y;
         }
         const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
-        if (P.dst_fmt == DTS_FMT_NV12) {
-            gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * cx, (uint16_t)(u | (v << 8)));
+        if (!out_col) return;
+        if (nv12) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u | (v << 8)), wU, 2 * cx, by * dp1, 0);
         } else {
-            gst<uint8_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + cx, (uint8_t)u);
-            gst<uint8_t>(P.dst.data[2] + df + (uint64_t)by * P.dst.pitch[2] + cx, (uint8_t)v);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u, wU, cx, by * dp1, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, wV, cx, by * dp2, 0);
         }
     };
     for (int s = s0; s <= s1; ++s) {
-        const float2 m0 = cdec(mA), m1 = cdec(mB), a0 = cdec(aA), a1 = cdec(aB), p0 = cdec(pA), p1 = cdec(pB);
+        const float2 p0 = cdec(pA), p1 = cdec(pB);
+        const float2 ph = make_float2(p0.x + fx * (p1.x - p0.x), p0.y + fx * (p1.y - p0.y));
         const uint32_t q0 = l0, q1 = l1;
         // the next step's loads fly during this step's conversion
-        mA = aA;
-        mB = aB;
-        aA = pA;
-        aB = pB;
         if (s < s1) {
             crow(s + 2, pA, pB);
             l0 = lrow(2 * s + 2);
             l1 = lrow(2 * s + 3);
         }
-        const float2 ah = make_float2(a0.x + fx * (a1.x - a0.x), a0.y + fx * (a1.y - a0.y));
-        const float2 mh = make_float2(m0.x + fx * (m1.x - m0.x), m0.y + fx * (m1.y - m0.y));
-        const float2 ph = make_float2(p0.x + fx * (p1.x - p0.x), p0.y + fx * (p1.y - p0.y));
         const float2 c[4] = {make_float2(0.75f * a0.x + 0.25f * m0.x, 0.75f * a0.y + 0.25f * m0.y),
                              make_float2(0.75f * ah.x + 0.25f * mh.x, 0.75f * ah.y + 0.25f * mh.y),
                              make_float2(0.75f * a0.x + 0.25f * p0.x, 0.75f * a0.y + 0.25f * p0.y),
                              make_float2(0.75f * ah.x + 0.25f * ph.x, 0.75f * ah.y + 0.25f * ph.y)};
+        m0 = a0;
+        mh = ah;
+        a0 = p0;
+        ah = ph;
         const float y0 = (float)__builtin_amdgcn_ubfe(q0, 6, 10), y2 = (float)__builtin_amdgcn_ubfe(q1, 6, 10);
         const float y10[4] = {y0, lsplit ? (float)(q0 >> 22) : y0, y2, lsplit ? (float)(q1 >> 22) : y2};
         float Yv[4];
         float2 C[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) pixel<MODE, DESAT>(P, tl, y10[q], c[q], Yv[q], C[q]);
-        if (out_col && s >= r0 && s < r1) {
-            const uint64_t yd = P.dst.data[0] + df + (uint64_t)(2 * s) * P.dst.pitch[0] + 2 * cx;
-            gst<uint16_t>(yd, (uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)));
-            gst<uint16_t>(yd + P.dst.pitch[0], (uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8)));
+        if (s >= r0 && s < r1 && out_col) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(q8y(Yv[0]) | (q8y(Yv[1]) << 8)), wY, 2 * cx, 2 * s * dp0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(q8y(Yv[2]) | (q8y(Yv[3]) << 8)), wY, 2 * cx,
+                                                  (2 * s + 1) * dp0, 0);
         }
         // this step's rows as horizontal sums, column 2cx - 1 from lane - 1 (all lanes active here)
         const float2 ht = hsum(make_float2(shr1(C[1].x), shr1(C[1].y)), C[0], C[1]);
