@@ -320,6 +320,7 @@ TonemapParams tonemap_params(const dts_tonemap_spec &t)
     p.peak = (float)peak;
     p.hpeak = (float)hable((float)peak);
     p.inv_hpeak = 1.0f / p.hpeak;
+    p.inv_hpeak_n = (float)kTmLutN / p.hpeak;
     p.scale = (float)(10000.0 / npl);
     bt2020_to_bt709(p.m);
     return p;
@@ -341,12 +342,15 @@ std::vector<float> tonemap_luts(const dts_tonemap_spec &t)
         v[i] = (float)(std::pow(std::max(p - c1, 0.0) / (c2 - c3 * p), 1.0 / m1) * scale);
         v[kTmLutN + 1 + i] = (float)(x < beta ? 4.5 * x : alpha * std::pow(x, 0.45) - (alpha - 1.0));
     }
+    // entry i: (intercept, slope) of the chord from i to i + 1 in table units, so that the
+    // interpolation at x in [i, i + 1] is one fma, intercept + x slope (hdr.hip lut)
     std::vector<float> o(4 * (kTmLutN + 1));
     for (int c = 0; c < 2; ++c)
         for (int i = 0; i <= kTmLutN; ++i) {
             const float *t = v.data() + c * (kTmLutN + 1);
-            o[2 * (c * (kTmLutN + 1) + i)] = t[i];
-            o[2 * (c * (kTmLutN + 1) + i) + 1] = i < kTmLutN ? t[i + 1] - t[i] : 0.0f;
+            const double sl = i < kTmLutN ? (double)t[i + 1] - (double)t[i] : 0.0;
+            o[2 * (c * (kTmLutN + 1) + i)] = (float)((double)t[i] - i * sl);
+            o[2 * (c * (kTmLutN + 1) + i) + 1] = (float)sl;
         }
     return o;
 }

@@ -407,8 +407,10 @@ struct TonemapParams {
     int32_t dst_fmt, w, h, nframes; // w, h even; nframes <= 65535
     int32_t mode;                   // DTS_TM_*
     float param, desat, peak, hpeak, inv_hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
+    float inv_hpeak_n;              // kTmLutN / hpeak (hable's normalisation folded into the OETF table scale)
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
-    const float2 *lut;              // device [2][kTmLutN + 1] (value, slope): PQ EOTF x 10000 / npl, BT.709 OETF
+    const float2 *lut;              // device [2][kTmLutN + 1] (intercept, slope) chords in table units: PQ EOTF
+                                    // x 10000 / npl, BT.709 OETF
 };
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s);     // tiled (k_tonemap)
 hipError_t launch_tonemap_w(const TonemapParams &p, hipStream_t s);   // column walk (k_tonemap_w)

@@ -42,15 +42,15 @@ __device__ __forceinline__ float pw(float x, float y)
     return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 }
 
-// table t[0..kTmLutN] of (value, slope to the next entry) of a curve on [0, 1],
+// table t[0..kTmLutN] of a curve on [0, 1] as chords (intercept, slope) in table units,
 // linearly interpolated; the argument arrives pre-scaled by kTmLutN (the scale is
-// folded into the producing FMA): clamp (v_med3), truncate / fract, one 8-byte LDS
-// read, fma
+// folded into the producing FMA): clamp (v_med3), truncate, one 8-byte LDS read, one
+// fma intercept + x slope (api.cpp tonemap_luts: no fract, the intercept absorbs it)
 __device__ __forceinline__ float lut(const float2 *t, float xn)
 {
     const float x = __builtin_amdgcn_fmed3f(xn, 0.f, (float)kTmLutN);
     const float2 e = t[(int)x];
-    return __builtin_fmaf(__builtin_amdgcn_fractf(x), e.y, e.x);   // x >= 0: fract(x) = x - (int)x exactly
+    return __builtin_fmaf(x, e.y, e.x);
 }
 
 #if DTS_TM_OETF_POW
@@ -83,10 +83,11 @@ __device__ __forceinline__ float mobius(float in, float j, float peak)
     return (b * b + 2.f * b * j + j * j) / (b - a) * (in + a) / (in + b);
 }
 
-__device__ __forceinline__ int q8(float v)
+// a v + b rounded and clipped to [0, 255]: floor(a v + b + 0.5) with the half folded into the fma;
+// after the clip the value is >= 0, so truncation is the floor
+__device__ __forceinline__ int q8fma(float a, float v, float b)
 {
-    // floor(v + 0.5) clipped to [0, 255]: after the clip the value is >= 0, so truncation is the floor
-    return (int)__builtin_amdgcn_fmed3f(v + 0.5f, 0.f, 255.f);
+    return (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(a, v, b + 0.5f), 0.f, 255.f);
 }
 
 // One pixel: 10-bit Y code, chroma (Cb', Cr' already centred) -> bt709 (Y', Cb', Cr').
@@ -108,7 +109,9 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     // non-linear R'G'B' x N (the table scale)
     const float yy = __builtin_fmaf(y10, N / 876.f, -64.f * N / 876.f);
     const float rp = __builtin_fmaf(c.y, 2.f * (1.f - kr2) * N, yy), bp = __builtin_fmaf(c.x, 2.f * (1.f - kb2) * N, yy);
-    const float gp = __builtin_fmaf(-kb2 / kg2, bp, __builtin_fmaf(-kr2 / kg2, rp, yy * (1.f / kg2)));
+    // g' = (y' - kr r' - kb b') / kg with r' = y' + 2 (1 - kr) Cr, b' = y' + 2 (1 - kb) Cb
+    const float gp = __builtin_fmaf(c.x, -2.f * kb2 * (1.f - kb2) / kg2 * N,
+                                    __builtin_fmaf(c.y, -2.f * kr2 * (1.f - kr2) / kg2 * N, yy));
     const float r0 = lut(pq, rp), g0 = lut(pq, gp), b0 = lut(pq, bp);
     float r = P.m[0] * r0 + P.m[1] * g0 + P.m[2] * b0;
     float g = P.m[3] * r0 + P.m[4] * g0 + P.m[5] * b0;
@@ -130,18 +133,18 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
         break;
     case DTS_TM_CLIP: sig = fminf(fmaxf(sig * P.param, 0.f), 1.f); break;
     case DTS_TM_REINHARD: sig = sig / (sig + P.param) * (P.peak + P.param) / P.peak; break;
-    case DTS_TM_HABLE: sig = hable(sig) * P.inv_hpeak; break;
+    case DTS_TM_HABLE: sig = hable(sig); break;               // / hpeak: folded into k below
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
 #if DTS_TM_OETF_POW
     (void)oetf;
-    const float k = sig * rcp(sig0);
+    const float k = sig * ((MODE == DTS_TM_HABLE ? P.inv_hpeak : 1.f) * rcp(sig0));
     r = oetf709(r * k);
     g = oetf709(g * k);
     b = oetf709(b * k);
 #else
-    const float k = sig * N * rcp(sig0);
+    const float k = sig * ((MODE == DTS_TM_HABLE ? P.inv_hpeak_n : N) * rcp(sig0));
     r = lut(oetf, r * k);
     g = lut(oetf, g * k);
     b = lut(oetf, b * k);
@@ -150,7 +153,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     C = make_float2((b - Y) * (1.f / (2.f * (1.f - kb7))), (r - Y) * (1.f / (2.f * (1.f - kr7))));
 }
 
-__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)q8(__builtin_fmaf(219.f, Y, 16.f)); }
+__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)q8fma(219.f, Y, 16.f); }
 
 } // namespace
 
@@ -356,7 +359,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             sb += wy[a] * (0.25f * l.x + 0.5f * mr.x + 0.25f * mr.z);
             sr += wy[a] * (0.25f * l.y + 0.5f * mr.y + 0.25f * mr.w);
         }
-        const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
+        const int u = q8fma(224.f, sb, 128.f), v = q8fma(224.f, sr, 128.f);
         if (P.dst_fmt == DTS_FMT_NV12) {
             gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx, (uint16_t)(u | (v << 8)));
         } else {
@@ -489,7 +492,7 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
             sb += wy[k] * h[k].x;
             sr += wy[k] * h[k].y;
         }
-        const int u = q8(128.f + 224.f * sb), v = q8(128.f + 224.f * sr);
+        const int u = q8fma(224.f, sb, 128.f), v = q8fma(224.f, sr, 128.f);
         if (!out_col) return;
         if (nv12) {
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u | (v << 8)), wU, 2 * cx, by * dp1, 0);

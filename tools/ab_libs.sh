@@ -1,9 +1,10 @@
 #!/bin/bash
-# A/B of libdts builds on the cfg2 bench: tools/ab_libs.sh <lib-suffix>... ("" = lib/libdts.so)
+# A/B of libdts builds on the cfg2 bench: tools/ab_libs.sh <lib-suffix>... ("" or base = lib/libdts.so)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 L=distributed-transcoding-server_amd/lib
 for v in "$@"; do
+  [ "$v" = base ] && v=""
   lib=$L/libdts${v:+_$v}.so
   for wl in ${AB_WORKLOADS:-cfg2}; do
     DTS_LIB=$PWD/$lib timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu --workload $wl > gpurun_out/ab_${v:-base}_$wl.log 2>&1
