@@ -320,10 +320,14 @@ __global__ void __launch_bounds__(256) k_yadif(const YadifParams P)
 // rows y0 - 2 .. y1 + 1 and 16 columns each side: every row and column filter_line reads,
 // reflections at the plane's top / bottom included) by LDS-DMA, one step ahead of its use.
 // HBM and L2 see each source frame about once per output instead of the 2.5 frames the
-// per-output kernel above fetches.  A thread computes 16 pixels of one interpolated row
-// from LDS (cur rows y -+ 1 as 48-byte windows for the x -+ 3 spatial search) and copies 16
-// bytes of one kept row; the 3-byte window sums of the spatial search are v_sad_u8 of
-// v_perm-aligned operands.  Sources and outputs 16-byte aligned, w >= 16.
+// per-output kernel above fetches.  A thread computes kYtNP (16) pixels of one interpolated
+// row from LDS (cur rows y -+ 1 as 48-byte windows for the x -+ 3 spatial search) and copies
+// 16 bytes of one kept row; the 3-byte window sums of the spatial search are v_sad_u8 of
+// v_perm-aligned operands.  The spatial search runs first and the other frames' rows are read
+// after it a dword at a time (round 5: 90 registers instead of 93).  Round-5 A/B:
+// 8 pixels per thread in 1024-thread workgroups fits 64 registers, two workgroups per CU and
+// 8 waves per SIMD, yet runs 69.0 k fps against 78.4 k here -- the window sharing of the
+// spatial search is worth more than the occupancy.  Sources and outputs 16-byte aligned, w >= 16.
 // ---------------------------------------------------------------------------
 constexpr int kYtW = 512;                       // output columns per tile (32 lanes x 16)
 constexpr int kYtH = 32;                        // output rows per tile (16 interpolated + 16 kept)
@@ -332,11 +336,23 @@ constexpr int kYtRows = kYtH + 4;               // rows y0 - 2 .. y0 + kYtH + 1
 constexpr int kYtChunks = kYtPitch / 16;        // 16-byte chunks per LDS row (34)
 constexpr int kYtSlot = kYtRows * kYtPitch;     // one frame tile (19,584 B)
 constexpr int kYtPieces = (kYtRows * kYtChunks + 63) / 64;   // 1-KB LDS-DMA pieces per frame tile
-constexpr int kYtThreads = 512;
+#ifndef DTS_YT_NP
+#define DTS_YT_NP 16
+#endif
+constexpr int kYtNP = DTS_YT_NP;                // pixels of an interpolated row per thread (8 or 16)
+constexpr int kYtCB = kYtNP == 16 ? 16 : 8;     // cur-row bytes staged in registers left / right of them
+constexpr int kYtThreads = (kYtW / kYtNP) * (kYtH / 2);
+static_assert(kYtNP == 8 || kYtNP == 16, "8 or 16 pixels per thread");
+#ifndef DTS_YT_WPE
+#define DTS_YT_WPE (kYtNP == 8 ? 8 : 1)         // waves per SIMD the register budget is sized for
+#endif
 #ifndef DTS_YADIF_WALK
 #define DTS_YADIF_WALK 16
 #endif
 constexpr int kYtWalk = DTS_YADIF_WALK;         // input frames per workgroup
+#ifndef DTS_YT_SB
+#define DTS_YT_SB 1                             // pixels of the spatial search between scheduling barriers
+#endif
 #ifndef DTS_YT_ABLATE
 #define DTS_YT_ABLATE 0                         // diagnostic bits (wrong output): 1 no arithmetic
 #endif
@@ -392,52 +408,28 @@ __device__ __forceinline__ i16x2y absd16(i16x2y a, i16x2y b)
     return __builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b);
 }
 
-template <bool FAR>
-__device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t (&cp)[12], const uint32_t (&pm)[4],
-                                        const uint32_t (&pp)[4], const uint32_t (&nm)[4], const uint32_t (&np)[4],
-                                        const uint32_t (&p2)[4], const uint32_t (&n2)[4], const uint32_t (&p2m)[4],
-                                        const uint32_t (&p2p)[4], const uint32_t (&n2m)[4], const uint32_t (&n2p)[4],
-                                        uint32_t ne, uint32_t (&out)[4])
+// the spatial search of NP pixels: pr[] = 2 x 16-bit predictions per dword
+template <int NP>
+__device__ __forceinline__ void yspatial(const uint32_t (&cm)[(2 * kYtCB + NP) / 4], const uint32_t (&cp)[(2 * kYtCB + NP) / 4],
+                                         uint32_t ne, uint32_t (&pr)[NP / 2])
 {
-    i16x2y lo[8], hi[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int q = i >> 1, h = i & 1;
-        const i16x2y c = pair16(cm[4 + q], h), e = pair16(cp[4 + q], h);
-        const i16x2y a2 = pair16(p2[q], h), b2 = pair16(n2[q], h);
-        const i16x2y d = (a2 + b2) >> 1;
-        const i16x2y td0 = absd16(a2, b2);
-        const i16x2y td1 = (absd16(pair16(pm[q], h), c) + absd16(pair16(pp[q], h), e)) >> 1;
-        const i16x2y td2 = (absd16(pair16(nm[q], h), c) + absd16(pair16(np[q], h), e)) >> 1;
-        i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0 >> 1, td1), td2);
-        if (FAR) {
-            const i16x2y b = (pair16(p2m[q], h) + pair16(n2m[q], h)) >> 1;
-            const i16x2y f = (pair16(p2p[q], h) + pair16(n2p[q], h)) >> 1;
-            const i16x2y de = d - e, dc = d - c, bc = b - c, fe = f - e;
-            const i16x2y mx = __builtin_elementwise_max(__builtin_elementwise_max(de, dc), __builtin_elementwise_min(bc, fe));
-            const i16x2y mn = __builtin_elementwise_min(__builtin_elementwise_min(de, dc), __builtin_elementwise_max(bc, fe));
-            diff = __builtin_elementwise_max(__builtin_elementwise_max(diff, mn), -mx);
-        }
-        lo[i] = d - diff;
-        hi[i] = d + diff;
-    }
-    // the 3-byte windows of cm / cp starting at byte 13 + i (i = 0 .. 19), made as the walk
-    // reaches them and passed through an empty asm: what depends on a window cannot be
+    constexpr int CB = kYtCB;                          // pixel k of cm / cp at byte CB + k
+    // the 3-byte windows of cm / cp starting at byte CB - 3 + i (i = 0 .. NP + 3), made as the
+    // walk reaches them and passed through an empty asm: what depends on a window cannot be
     // scheduled before it, so the sliding ten are all that is live
-    uint32_t wm[20], wp[20];
+    uint32_t wm[NP + 4], wp[NP + 4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        wm[i] = win3(cm, 13 + i);
-        wp[i] = win3(cp, 13 + i);
+        wm[i] = win3(cm, CB - 3 + i);
+        wp[i] = win3(cp, CB - 3 + i);
         asm volatile("" : "+v"(wm[i]), "+v"(wp[i]));
     }
     auto b8 = [](uint32_t w, int i) { return (int)((w >> (8 * i)) & 255u); };
-    uint32_t pr[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        // pixel X = 16 + k: windows starting at X - 3 .. X + 1 = indices k .. k + 4
-        wm[k + 4] = win3(cm, 17 + k);
-        wp[k + 4] = win3(cp, 17 + k);
+    for (int k = 0; k < NP; ++k) {
+        // pixel X = CB + k: windows starting at X - 3 .. X + 1 = indices k .. k + 4
+        wm[k + 4] = win3(cm, CB + 1 + k);
+        wp[k + 4] = win3(cp, CB + 1 + k);
         asm volatile("" : "+v"(wm[k + 4]), "+v"(wp[k + 4]));
         const uint32_t m3 = wm[k], m2 = wm[k + 1], m1 = wm[k + 2], m0 = wm[k + 3], m_1 = wm[k + 4];
         const uint32_t p3 = wp[k], p2_ = wp[k + 1], p1 = wp[k + 2], p0 = wp[k + 3], p_1 = wp[k + 4];
@@ -462,50 +454,89 @@ __device__ __forceinline__ void yadif16(const uint32_t (&cm)[12], const uint32_t
         ps = b4 ? b8(m0, 2) + b8(p2_, 0) : ps;            // cm[X + 2] + cp[X - 2]
         const uint32_t pv = (uint32_t)ps >> 1;
         pr[k >> 1] = (k & 1) ? pr[k >> 1] | (pv << 16) : pv;
-        __builtin_amdgcn_sched_barrier(0);
+        if ((k + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
-    if (ne != 0xffffu) {                                  // filter_edges: no spatial search
+    if (ne != (1u << NP) - 1) {                           // filter_edges: no spatial search
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < NP; ++k)
             if (!((ne >> k) & 1u)) {
-                const uint32_t pv = (uint32_t)(byte_at(cm, 16 + k) + byte_at(cp, 16 + k)) >> 1;
+                const uint32_t pv = (uint32_t)(byte_at(cm, CB + k) + byte_at(cp, CB + k)) >> 1;
                 pr[k >> 1] = (k & 1) ? (pr[k >> 1] & 0xffffu) | (pv << 16) : (pr[k >> 1] & 0xffff0000u) | pv;
             }
     }
-    // the reference's two-sided clamp (diff >= 0: a median), then two 16-bit pairs per dword of bytes
+}
+
+// the temporal bounds d -+ diff of NP pixels (two per dword as packed 16-bit lanes: v_pk_*
+// arithmetic, no value leaves [-510, 510]) and the reference's two-sided clamp of the
+// spatial predictions pr[] (diff >= 0: a median), packed back to bytes.  ld(r, q) reads dword
+// q of row r: 0 / 1 prev mrefs / prefs, 2 / 3 next, 4 / 5 prev2 / next2 on this row, 6 .. 9
+// prev2 / next2 two rows away (FAR) -- loaded per dword, so one dword of each is live at a time
+template <int NP, bool FAR, class LD>
+__device__ __forceinline__ void ytemporal(const uint32_t (&cm)[(2 * kYtCB + NP) / 4], const uint32_t (&cp)[(2 * kYtCB + NP) / 4],
+                                          LD ld, const uint32_t (&pr)[NP / 2], uint32_t (&out)[NP / 4])
+{
+    constexpr int CQ = kYtCB / 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const i16x2y r0 = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q]), lo[2 * q]), hi[2 * q]);
-        const i16x2y r1 = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q + 1]), lo[2 * q + 1]),
-                                                    hi[2 * q + 1]);
-        out[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, r1), __builtin_bit_cast(uint32_t, r0), 0x06040200u);
+    for (int q = 0; q < NP / 4; ++q) {
+        const uint32_t pm = ld(0, q), pp = ld(1, q), nm = ld(2, q), np = ld(3, q), p2 = ld(4, q), n2 = ld(5, q);
+        const uint32_t p2m = FAR ? ld(6, q) : 0u, p2p = FAR ? ld(7, q) : 0u, n2m = FAR ? ld(8, q) : 0u,
+                       n2p = FAR ? ld(9, q) : 0u;
+        i16x2y r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const i16x2y c = pair16(cm[CQ + q], h), e = pair16(cp[CQ + q], h);
+            const i16x2y a2 = pair16(p2, h), b2 = pair16(n2, h);
+            const i16x2y d = (a2 + b2) >> 1;
+            const i16x2y td0 = absd16(a2, b2);
+            const i16x2y td1 = (absd16(pair16(pm, h), c) + absd16(pair16(pp, h), e)) >> 1;
+            const i16x2y td2 = (absd16(pair16(nm, h), c) + absd16(pair16(np, h), e)) >> 1;
+            i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0 >> 1, td1), td2);
+            if (FAR) {
+                const i16x2y b = (pair16(p2m, h) + pair16(n2m, h)) >> 1;
+                const i16x2y f = (pair16(p2p, h) + pair16(n2p, h)) >> 1;
+                const i16x2y de = d - e, dc = d - c, bc = b - c, fe = f - e;
+                const i16x2y mx = __builtin_elementwise_max(__builtin_elementwise_max(de, dc), __builtin_elementwise_min(bc, fe));
+                const i16x2y mn = __builtin_elementwise_min(__builtin_elementwise_min(de, dc), __builtin_elementwise_max(bc, fe));
+                diff = __builtin_elementwise_max(__builtin_elementwise_max(diff, mn), -mx);
+            }
+            r[h] = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q + h]), d - diff), d + diff);
+        }
+        out[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, r[1]), __builtin_bit_cast(uint32_t, r[0]), 0x06040200u);
     }
 }
 
 typedef unsigned int u32x4y __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4y g_u32x4y;
 typedef __attribute__((address_space(1))) uint8_t g_u8y;
-__device__ __forceinline__ u32x4y lds16(const uint8_t *p) { return *reinterpret_cast<const u32x4y *>(p); }
-__device__ __forceinline__ void put16(uint64_t dst, u32x4y v, int room)
+typedef unsigned int u32x2y __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2y g_u32x2y;
+// NP bytes of an LDS row into NP / 4 dwords (one ds_read_b128 or b64)
+template <int NP> __device__ __forceinline__ void ldsn(const uint8_t *p, uint32_t *o)
 {
-    if (room >= 16) {
-        *(g_u32x4y *)(uintptr_t)dst = v;
+    if (NP == 16) {
+        const u32x4y v = *reinterpret_cast<const u32x4y *>(p);
+        o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
     } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        for (int i = 0; i < room; ++i) ((g_u8y *)(uintptr_t)dst)[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        const u32x2y v = *reinterpret_cast<const u32x2y *>(p);
+        o[0] = v.x, o[1] = v.y;
     }
 }
-__device__ __forceinline__ void unpack4(u32x4y v, uint32_t *o)
+// NP bytes to a plane row (room: bytes left in the row)
+template <int NP> __device__ __forceinline__ void putn(uint64_t dst, const uint32_t *w, int room)
 {
-    o[0] = v.x;
-    o[1] = v.y;
-    o[2] = v.z;
-    o[3] = v.w;
+    if (room >= NP) {
+        if (NP == 16)
+            *(g_u32x4y *)(uintptr_t)dst = (u32x4y){w[0], w[1], w[2], w[3]};
+        else
+            *(g_u32x2y *)(uintptr_t)dst = (u32x2y){w[0], w[1]};
+    } else {
+        for (int i = 0; i < room; ++i) ((g_u8y *)(uintptr_t)dst)[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
 }
 
 } // namespace
 
-__global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int tiles_l, int tiles_c, int txl, int txc,
+__global__ void __launch_bounds__(kYtThreads, DTS_YT_WPE) k_yadif_t(const YadifParams P, int tiles_l, int tiles_c, int txl, int txc,
                                                         int count)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t yl[];
@@ -554,8 +585,11 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int nst = 0;                               // this wave's stores of the previous step (when counted)
-    const int ci = t & 31, ri = t >> 5;        // 16 columns of one interpolated and one kept row
-    const int x = x0 + 16 * ci;
+    constexpr int NP = kYtNP, NQ = NP / 4, CW = (2 * kYtCB + NP) / 4;
+    // NP columns of one interpolated and one kept row (8 pixels: one row pair per wave, its row
+    // arithmetic scalar)
+    const int ci = t % (kYtW / NP), ri = kYtW / NP == 64 ? __builtin_amdgcn_readfirstlane(t / 64) : t / (kYtW / NP);
+    const int x = x0 + NP * ci;
     const uint64_t obase0 = P.dst.data[p] + (uint64_t)x;
     for (int j = j0; j < j1; ++j) {
         const int s = j - j0;
@@ -578,8 +612,9 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
             {
                 const int y = y0 + 2 * ri + (1 - off);
                 if (y < h && x < w) {
-                    const u32x4y v = lds16(sl_c + (y - y0 + 2) * kYtPitch + 16 * ci + 16);
-                    put16(obase + (uint64_t)((int64_t)y * dp), v, w - x);
+                    uint32_t v[NQ];
+                    ldsn<NP>(sl_c + (y - y0 + 2) * kYtPitch + NP * ci + 16, v);
+                    putn<NP>(obase + (uint64_t)((int64_t)y * dp), v, w - x);
                 }
             }
             const int y = y0 + 2 * ri + off;
@@ -588,37 +623,34 @@ __global__ void __launch_bounds__(kYtThreads) k_yadif_t(const YadifParams P, int
                 const bool far = !((P.mode & 2) || y == 1 || y + 2 == h);
                 const uint8_t *prv = sl_p, *cur = sl_c, *nxt = sl_n;
                 const uint8_t *pv2 = parity ? prv : cur, *nx2 = parity ? cur : nxt;
-                auto row = [&](const uint8_t *sl, int yy) { return sl + (yy - y0 + 2) * kYtPitch + 16 * ci + 16; };
-                uint32_t cm[12], cp[12], pm[4], pp[4], nm[4], np[4], p2[4], n2[4], p2m[4], p2p[4], n2m[4], n2p[4];
+                auto row = [&](const uint8_t *sl, int yy) { return sl + (yy - y0 + 2) * kYtPitch + NP * ci + 16; };
+                uint32_t cm[CW], cp[CW];
 #pragma unroll
-                for (int h3 = 0; h3 < 3; ++h3) {
-                    unpack4(lds16(row(cur, rm) - 16 + 16 * h3), cm + 4 * h3);
-                    unpack4(lds16(row(cur, rp) - 16 + 16 * h3), cp + 4 * h3);
+                for (int h3 = 0; h3 < 3; ++h3) {       // cur rows: bytes x - CB .. x + NP + CB - 1
+                    ldsn<NP>(row(cur, rm) - kYtCB + NP * h3, cm + NQ * h3);
+                    ldsn<NP>(row(cur, rp) - kYtCB + NP * h3, cp + NQ * h3);
                 }
-                unpack4(lds16(row(prv, rm)), pm);
-                unpack4(lds16(row(prv, rp)), pp);
-                unpack4(lds16(row(nxt, rm)), nm);
-                unpack4(lds16(row(nxt, rp)), np);
-                unpack4(lds16(row(pv2, y)), p2);
-                unpack4(lds16(row(nx2, y)), n2);
                 uint32_t ne = 0;
 #pragma unroll
-                for (int k = 0; k < 16; ++k) ne |= (x + k >= 3 && x + k < w - 3) ? 1u << k : 0u;
-                uint32_t res[4];
+                for (int k = 0; k < NP; ++k) ne |= (x + k >= 3 && x + k < w - 3) ? 1u << k : 0u;
+                // the spatial search first, then the other frames' rows (loaded past a scheduling
+                // barrier, a dword at a time: the two phases' operands are not live at once)
+                uint32_t pr[NP / 2], res[NQ];
+                if (!(DTS_YT_ABLATE & 1)) yspatial<NP>(cm, cp, ne, pr);
+                __builtin_amdgcn_sched_barrier(0);
+                const int rm2 = 2 * rm - y, rp2 = 2 * rp - y;   // 2 mrefs / 2 prefs
+                const uint8_t *rows[10] = {row(prv, rm), row(prv, rp), row(nxt, rm), row(nxt, rp), row(pv2, y),
+                                           row(nx2, y), row(pv2, rm2), row(pv2, rp2), row(nx2, rm2), row(nx2, rp2)};
+                auto ld = [&](int r, int q) { return *reinterpret_cast<const uint32_t *>(rows[r] + 4 * q); };
                 if (DTS_YT_ABLATE & 1) {               // diagnostic: no arithmetic (wrong output)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) res[q] = cm[4 + q] ^ cp[4 + q] ^ pm[q] ^ np[q] ^ p2[q] ^ n2[q];
+                    for (int q = 0; q < NQ; ++q) res[q] = cm[NQ + q] ^ cp[NQ + q] ^ ld(0, q) ^ ld(3, q) ^ ld(4, q) ^ ld(5, q);
                 } else if (far) {
-                    const int rm2 = 2 * rm - y, rp2 = 2 * rp - y;   // 2 mrefs / 2 prefs
-                    unpack4(lds16(row(pv2, rm2)), p2m);
-                    unpack4(lds16(row(pv2, rp2)), p2p);
-                    unpack4(lds16(row(nx2, rm2)), n2m);
-                    unpack4(lds16(row(nx2, rp2)), n2p);
-                    yadif16<true>(cm, cp, pm, pp, nm, np, p2, n2, p2m, p2p, n2m, n2p, ne, res);
+                    ytemporal<NP, true>(cm, cp, ld, pr, res);
                 } else {
-                    yadif16<false>(cm, cp, pm, pp, nm, np, p2, n2, p2m, p2p, n2m, n2p, ne, res);
+                    ytemporal<NP, false>(cm, cp, ld, pr, res);
                 }
-                put16(obase + (uint64_t)((int64_t)y * dp), (u32x4y){res[0], res[1], res[2], res[3]}, w - x);
+                putn<NP>(obase + (uint64_t)((int64_t)y * dp), res, w - x);
             }
             nst += 2;
         }
