@@ -470,8 +470,9 @@ int validate_spec(const dts_graph_spec &s)
     }
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
     if ((s.range & ~0x11) != 0) return DTS_E_INVAL;              // DTS_RANGE_* in bits 0 and 4
-    if ((s.range & 1) != ((s.range >> 4) & 1) && (s.hdr_to_sdr || s.src_fmt == DTS_FMT_P010LE))
-        return DTS_E_UNSUPPORTED;                                // range conversion: k_ladder7 sources only
+    // range conversion: the ladder's (k_ladder7) 15-bit converters, every source format; the HDR
+    // path's ranges are zscale's (tonemap), not a swscale conversion
+    if ((s.range & 1) != ((s.range >> 4) & 1) && s.hdr_to_sdr) return DTS_E_UNSUPPORTED;
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
     for (int k = 0; k < s.nout; ++k) {                  // rendition quality (ABI 6)
         const dts_output_spec &o = s.out[k];

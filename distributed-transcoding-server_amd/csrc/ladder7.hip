@@ -1003,9 +1003,11 @@ hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_b
 {
     if (waves < 1 || waves > kL7MaxWaves || (hsplit != 128 && hsplit != 256)) return hipErrorInvalidValue;
     const dim3 g(grid), b(64 * waves);
-    if (src_kind == kSrcP010) {          // p010 sources (no range conversion: dts_graph_create refuses it)
-        if (range_conv) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_ladder7<false, 256, 2>), g, b, lds_bytes, s, p);
+    if (src_kind == kSrcP010) {          // p010 sources (the 15-bit converters too: dstBpc <= 14)
+        if (range_conv)
+            hipLaunchKernelGGL((k_ladder7<true, 256, 2>), g, b, lds_bytes, s, p);
+        else
+            hipLaunchKernelGGL((k_ladder7<false, 256, 2>), g, b, lds_bytes, s, p);
         return hipGetLastError();
     }
     if (src_kind == kSrcNV12) {          // nv12 sources

@@ -176,7 +176,13 @@ async function encodeSegment(bin, out, frames, w, h, fmt, fps, job, settings) {
 async function encodeRenditions(bin, items) {
     const encs = [];
     try {
-        items.forEach(function (it) { encs.push(new FfmpegEncoder(bin, it.out, it.w, it.h, it.fps, it.fmt, it.job, it.settings)); });
+        // one spawn per turn of the event loop: a spawn forks this process (~10 ms each), and
+        // a burst of them would hold the loop -- and every other GPU slot -- for all of them
+        for (let k = 0; k < items.length; ++k) {
+            const it = items[k];
+            if (k) await new Promise(setImmediate);
+            encs.push(new FfmpegEncoder(bin, it.out, it.w, it.h, it.fps, it.fmt, it.job, it.settings));
+        }
     } catch (e) {
         encs.forEach(function (en) { en.kill(); });
         throw new Error("ffmpeg encode: " + e.message);

@@ -260,12 +260,13 @@ def test_v7_geometries(ctx, sw, sh, outs, method):
 @pytest.mark.parametrize("kernel", ["v7", "v5"])
 @pytest.mark.parametrize("src_range,dst_range", [(0, 1), (1, 0)])
 @pytest.mark.parametrize("method", [BIC, LAN, BIL])
-@pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12])
+@pytest.mark.parametrize("sfmt", [D.FMT_YUV420P, D.FMT_NV12, D.FMT_P010LE])
 def test_range_conversion(ctx, monkeypatch, kernel, src_range, dst_range, method, sfmt):
     """`scale=in_range:out_range`: swscale.c's lum/chrRange{To,From}Jpeg_c on the
     15-bit H output, in k_ladder7's H epilogue, bit-exact vs the oracle (random and
-    full-swing frames, nv12 and yuv420p renditions; planar and nv12 sources -- nv12
-    chroma de-interleaved in the A reads).  Other kernels refuse it."""
+    full-swing frames, nv12 and yuv420p renditions; planar, nv12 and p010 sources -- nv12
+    chroma de-interleaved in the A reads; p010 sources (round 5) through the same 15-bit
+    converters, since every rendition has dstBpc <= 14).  Other kernels refuse it."""
     sw, sh = 384, 216
     outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_YUV420P, method), (384, 216, D.FMT_NV12, method)]
     spec = D.make_spec(sw, sh, sfmt, outs, src_range=src_range, dst_range=dst_range)
@@ -281,6 +282,12 @@ def test_range_conversion(ctx, monkeypatch, kernel, src_range, dst_range, method
     if sfmt == D.FMT_NV12:                    # the same pictures, chroma interleaved
         frames = [[f[0], np.ascontiguousarray(np.stack([f[1], f[2]], -1).reshape(f[1].shape[0], -1)), None]
                   for f in frames]
+    if sfmt == D.FMT_P010LE:                  # the same pictures as 10-bit codes (x 4, and random low bits)
+        def p010(f):
+            w16 = lambda a: (a.astype(np.uint16) << 8) | rng.integers(0, 256, a.shape, dtype=np.uint16)
+            uv = np.stack([w16(f[1]), w16(f[2])], -1).reshape(f[1].shape[0], -1)
+            return [w16(f[0]).view(np.uint8), np.ascontiguousarray(uv).view(np.uint8), None]
+        frames = [p010(f) for f in frames]
     g = D.Graph(ctx, spec)
     got, _ = g.run_host(frames)
     for f, src in enumerate(frames):
