@@ -597,13 +597,13 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
 bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
 {
     if (!v7_enabled() || s.src_fmt != DTS_FMT_P010LE) return false;
-    if ((s.range & 1) != ((s.range >> 4) & 1)) return false;
     Plan5In ins[2];
     for (int kind = 0; kind < 2; ++kind) {
         Plan5In &in = ins[kind];
         in.chroma = kind == 1;
         in.nv12_chroma = kind == 1;
         in.p10 = true;
+        if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
         in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
         for (int k = 0; k < s.nout; ++k) {
