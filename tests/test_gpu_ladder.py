@@ -269,6 +269,8 @@ def test_range_conversion(ctx, monkeypatch, kernel, src_range, dst_range, method
     converters, since every rendition has dstBpc <= 14).  Other kernels refuse it."""
     sw, sh = 384, 216
     outs = [(192, 108, D.FMT_NV12, method), (128, 72, D.FMT_YUV420P, method), (384, 216, D.FMT_NV12, method)]
+    if sfmt == D.FMT_P010LE:                  # renditions k_ladder7's p010 walks plan (else k_ladder4: refused)
+        outs = [(192, 108, D.FMT_NV12, method), (160, 90, D.FMT_YUV420P, method), (256, 144, D.FMT_P010LE, method)]
     spec = D.make_spec(sw, sh, sfmt, outs, src_range=src_range, dst_range=dst_range)
     if kernel != "v7":
         monkeypatch.setenv("DTS_LADDER", kernel[1])
