@@ -563,7 +563,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     }
     if (diag_env("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
         for (const Group7 &g : out.groups)
-            std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d\n", g.kind, g.X0, g.npc, g.nwaves);
+            std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d scr %d\n", g.kind, g.X0, g.npc, g.nwaves, g.scr);
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
     // the staging waves: a group's spare waves, else all of its waves
