@@ -62,9 +62,12 @@ WORKLOADS = {
              "desc": "cfg3: 4K60 10-bit p010 HDR10 (PQ, bt2020nc) -> SDR bt709 8-bit 1080p yuv420p: bit-exact "
                      "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB)"},
     "cfg4": {"src": (7680, 4320, D.FMT_YUV420P), "outs": [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)],
-             "tonemap": None, "quality": True, "batch": 64,
+             # one launch = one 10 s segment of 8K30 (300 frames: the JobChunk unit, as cfg5's
+             # 600-frame 4K60 segments); round 5: 64-frame launches left a 1.5-wave launch tail
+             "tonemap": None, "quality": True, "batch": 300, "ring": 300,
              "desc": "cfg4: 8K30 yuv420p -> 4K lanczos + per-frame vf_psnr/vf_ssim of the output vs its own 4K "
-                     "reference frame (a device-resident reference ring as long as the source ring)"},
+                     "reference frame (a device-resident reference ring as long as the source ring), one "
+                     "10 s segment (300 frames) per launch"},
     # BASELINE config 5 on one GPU: a step is one 600-frame segment of the cfg2 ladder plus
     # vf_psnr/vf_ssim of every rendition against a reference rendition of the same size
     # (the source scaled with lanczos: computed once, outside the timed region); the

@@ -557,6 +557,21 @@ bool l7_narrow()
     return f ? f[0] == '1' : false;
 }
 
+// k_ladder7's plan with its group width: 8 waves, two groups per CU, unless two such groups do
+// not fit the CU's 160 KB of LDS (8K sources: cfg4 plans 90 KB per group).  Then a CU holds one
+// group whatever its width, and a 10-wave group keeps more waves resident (round-5 cfg4 A/B,
+// 300-frame launches: W 8 / 10 / 12 / 14 / 16 52.1 k / 54.4 k / 53.2 k / 53.5 k / 52.8 k fps).
+// The diagnostic DTS_L7_W fixes the width.
+bool plan7_sized(const Plan5In *ins, bool narrow, Plan7 &out)
+{
+    if (!plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), narrow, out)) return false;
+    if (diag_env("DTS_L7_W") || 2 * out.lds_bytes <= 160 * 1024) return true;
+    Plan7 wide;
+    if (plan7_graph(ins, 10, l7_stages(), l7_pb(), l7_by_rung(), narrow, wide) && wide.lds_bytes <= 160 * 1024)
+        out = std::move(wide);
+    return true;
+}
+
 // k_ladder5 for every (rendition, kind) of an 8-bit 4:2:0 source with 8-bit outputs,
 // and k_ladder7 too where it fits
 bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
@@ -587,7 +602,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
     gp.v5 = true;
     // k_ladder7 takes planar and nv12 sources (k_ladder5: the fallback for frames that are
     // not 16-byte aligned)
-    gp.v7 = v7_enabled() && plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), l7_narrow(), gp.p7);
+    gp.v7 = v7_enabled() && plan7_sized(ins, l7_narrow(), gp.p7);
     return true;
 }
 
@@ -613,7 +628,7 @@ bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
                                          s.hdr_to_sdr ? (int)DTS_FMT_P010LE : s.out[k].fmt});
         }
     }
-    return plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), false, gp.p7);
+    return plan7_sized(ins, false, gp.p7);
 }
 
 bool plan4_for(const dts_graph_spec &s, const KindTables &kt, int kind, Plan4 &pl)
