@@ -343,15 +343,28 @@ std::vector<float> tonemap_luts(const dts_tonemap_spec &t)
         v[kTmLutN + 1 + i] = (float)(x < beta ? 4.5 * x : alpha * std::pow(x, 0.45) - (alpha - 1.0));
     }
     // entry i: (intercept, slope) of the chord from i to i + 1 in table units, so that the
-    // interpolation at x in [i, i + 1] is one fma, intercept + x slope (hdr.hip lut)
-    std::vector<float> o(4 * (kTmLutN + 1));
-    for (int c = 0; c < 2; ++c)
-        for (int i = 0; i <= kTmLutN; ++i) {
-            const float *t = v.data() + c * (kTmLutN + 1);
-            const double sl = i < kTmLutN ? (double)t[i + 1] - (double)t[i] : 0.0;
-            o[2 * (c * (kTmLutN + 1) + i)] = (float)((double)t[i] - i * sl);
-            o[2 * (c * (kTmLutN + 1) + i) + 1] = (float)sl;
+    // interpolation at x in [i, i + 1] is one fma, intercept + x slope (hdr.hip lut).  The PQ
+    // table first, indexed by x + kTmPqOff over kTmPqN entries (flat at 0 below x = 0 and at
+    // PQ(1) above x = kTmLutN: no clamp in the lookup), then the OETF table over [0, kTmLutN]
+    std::vector<float> o(2 * (kTmPqN + kTmLutN + 1));
+    for (int i = 0; i < kTmPqN; ++i) {
+        const int j = i - kTmPqOff;                  // the chord over x in [j, j + 1]
+        double sl = 0.0, y0 = 0.0;
+        if (j >= kTmLutN) {
+            y0 = v[kTmLutN];
+        } else if (j >= 0) {
+            y0 = v[j];
+            sl = (double)v[j + 1] - (double)v[j];
         }
+        o[2 * i] = (float)(y0 - (double)i * sl);     // in units of x + kTmPqOff
+        o[2 * i + 1] = (float)sl;
+    }
+    for (int i = 0; i <= kTmLutN; ++i) {
+        const float *t = v.data() + kTmLutN + 1;
+        const double sl = i < kTmLutN ? (double)t[i + 1] - (double)t[i] : 0.0;
+        o[2 * (kTmPqN + i)] = (float)((double)t[i] - i * sl);
+        o[2 * (kTmPqN + i) + 1] = (float)sl;
+    }
     return o;
 }
 

@@ -396,7 +396,11 @@ struct QualityParams {
 // ---------------------------------------------------------------------------
 // HDR10 -> SDR (hdr.hip)
 // ---------------------------------------------------------------------------
-constexpr int kTmLutN = 1024;      // intervals of the PQ EOTF / BT.709 OETF tables
+constexpr int kTmLutN = 1024;      // intervals of the PQ EOTF / BT.709 OETF tables over [0, 1]
+// The PQ table is indexed by x + kTmPqOff for every x the 10-bit codes can produce (R', G', B' x
+// kTmLutN lie in [-1176, 2220]: hdr.hip pixel<>), flat outside [0, kTmLutN], so its lookup
+// needs no clamp: kTmPqN entries
+constexpr int kTmPqOff = 1280, kTmPqN = 3584;
 #ifndef DTS_TM_ROWS
 #define DTS_TM_ROWS 64
 #endif

@@ -52,6 +52,13 @@ __device__ __forceinline__ float lut(const float2 *t, float xn)
     const float2 e = t[(int)x];
     return __builtin_fmaf(x, e.y, e.x);
 }
+// the PQ table (api.cpp tonemap_luts): x already offset by kTmPqOff and inside the table by
+// construction (pixel<>), so no clamp
+__device__ __forceinline__ float lut_pq(const float2 *t, float x)
+{
+    const float2 e = t[(int)x];
+    return __builtin_fmaf(x, e.y, e.x);
+}
 
 #if DTS_TM_OETF_POW
 // BT.709 OETF on [0, 1] (the host table's curve, api.cpp tonemap_luts)
@@ -83,12 +90,6 @@ __device__ __forceinline__ float mobius(float in, float j, float peak)
     return (b * b + 2.f * b * j + j * j) / (b - a) * (in + a) / (in + b);
 }
 
-// a v + b rounded and clipped to [0, 255]: floor(a v + b + 0.5) with the half folded into the fma;
-// after the clip the value is >= 0, so truncation is the floor
-__device__ __forceinline__ int q8fma(float a, float v, float b)
-{
-    return (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(a, v, b + 0.5f), 0.f, 255.f);
-}
 
 // One pixel: 10-bit Y code, chroma (Cb', Cr' already centred) -> bt709 (Y', Cb', Cr').
 // The curve and the desaturation switch are template parameters: a branch per pixel
@@ -102,17 +103,19 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
         C = c;
         return;
     }
-    const float2 *pq = tl, *oetf = tl + kTmLutN + 1;          // pq already scaled by 10000 / npl
+    const float2 *pq = tl, *oetf = tl + kTmPqN;              // pq already scaled by 10000 / npl
     constexpr float N = (float)kTmLutN;
     constexpr float kr2 = 0.2627f, kb2 = 0.0593f, kg2 = 1.f - kr2 - kb2;
     constexpr float kr7 = 0.2126f, kb7 = 0.0722f, kg7 = 1.f - kr7 - kb7;
-    // non-linear R'G'B' x N (the table scale)
-    const float yy = __builtin_fmaf(y10, N / 876.f, -64.f * N / 876.f);
+    // non-linear R'G'B' x N (the table scale) + kTmPqOff (the PQ table's index offset): from
+    // 10-bit codes, y' x N in [-74.8, 1120.5] and Cb, Cr in [-512, 511] / 896, so R' in [-938, 1982],
+    // B' in [-1176, 2220], G' in [-505, 1552] (x N): the PQ lookups index [104, 3500] of kTmPqN
+    const float yy = __builtin_fmaf(y10, N / 876.f, -64.f * N / 876.f + (float)kTmPqOff);
     const float rp = __builtin_fmaf(c.y, 2.f * (1.f - kr2) * N, yy), bp = __builtin_fmaf(c.x, 2.f * (1.f - kb2) * N, yy);
     // g' = (y' - kr r' - kb b') / kg with r' = y' + 2 (1 - kr) Cr, b' = y' + 2 (1 - kb) Cb
     const float gp = __builtin_fmaf(c.x, -2.f * kb2 * (1.f - kb2) / kg2 * N,
                                     __builtin_fmaf(c.y, -2.f * kr2 * (1.f - kr2) / kg2 * N, yy));
-    const float r0 = lut(pq, rp), g0 = lut(pq, gp), b0 = lut(pq, bp);
+    const float r0 = lut_pq(pq, rp), g0 = lut_pq(pq, gp), b0 = lut_pq(pq, bp);
     float r = P.m[0] * r0 + P.m[1] * g0 + P.m[2] * b0;
     float g = P.m[3] * r0 + P.m[4] * g0 + P.m[5] * b0;
     float b = P.m[6] * r0 + P.m[7] * g0 + P.m[8] * b0;
@@ -153,7 +156,11 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     C = make_float2((b - Y) * (1.f / (2.f * (1.f - kb7))), (r - Y) * (1.f / (2.f * (1.f - kr7))));
 }
 
-__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)q8fma(219.f, Y, 16.f); }
+// Y' = kr R' + kg G' + kb B' with R', G', B' in [0, 1] (the OETF table's values, or oetf709's):
+// 219 Y' + 16.5 lies in [16.5, 235.5], so the quantiser needs no clip
+__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)__builtin_fmaf(219.f, Y, 16.5f); }
+// Cb', Cr' in [-1/2, 1/2] for the same reason: 224 C + 128.5 in [16.5, 240.5]
+__device__ __forceinline__ int q8c(float C) { return (int)__builtin_fmaf(224.f, C, 128.5f); }
 
 } // namespace
 
@@ -173,10 +180,10 @@ constexpr int kTmCW = 66, kTmCH = kTmCRows + 2;        // chroma samples staged:
 template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
 {
-    constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
+    constexpr int kTabN = kTmPqN + (DTS_TM_OETF_POW ? 0 : kTmLutN + 1);   // PQ, then OETF
     constexpr int kRow = 129;                       // ring row: columns x0 - 1 .. x0 + 127
     constexpr int kCin = kTmCH * kTmCW;             // staged chroma samples per tile (660: 3 per thread)
-    __shared__ float2 tl[kTabs * (kTmLutN + 1)];
+    __shared__ float2 tl[kTabN];
     __shared__ float2 cin[kTmCH][kTmCW];            // (Cb', Cr') centred, 4:2:0
     __shared__ __attribute__((aligned(16))) float2 cc[kTmLH][kTmLP];   // output (Cb, Cr) at full resolution
     const int t = threadIdx.x, f = blockIdx.z;
@@ -187,7 +194,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
     const uint64_t sy0 = P.src.data[0] + sf, sc0 = P.src.data[1] + sf;
     const int lp = P.src.pitch[0], cp = P.src.pitch[1];
     const bool a4 = ((P.src.data[0] + sf) & 3) == 0 && (P.src.pitch[0] & 3) == 0;
-    for (int i = t; i < kTabs * (kTmLutN + 1); i += 256) tl[i] = P.lut[i];
+    for (int i = t; i < kTabN; i += 256) tl[i] = P.lut[i];
     // a thread's staged chroma samples (rows / columns fixed over the tiles) and block positions
     int cr[3], cxo[3];
 #pragma unroll
@@ -359,7 +366,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             sb += wy[a] * (0.25f * l.x + 0.5f * mr.x + 0.25f * mr.z);
             sr += wy[a] * (0.25f * l.y + 0.5f * mr.y + 0.25f * mr.w);
         }
-        const int u = q8fma(224.f, sb, 128.f), v = q8fma(224.f, sr, 128.f);
+        const int u = q8c(sb), v = q8c(sr);
         if (P.dst_fmt == DTS_FMT_NV12) {
             gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx, (uint16_t)(u | (v << 8)));
         } else {
@@ -421,9 +428,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(uint64_t base, int6
 template <int MODE, bool DESAT>
 __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams P, int nstrips, int nchunks)
 {
-    constexpr int kTabs = DTS_TM_OETF_POW ? 1 : 2;
-    __shared__ float2 tl[kTabs * (kTmLutN + 1)];
-    for (int i = threadIdx.x; i < kTabs * (kTmLutN + 1); i += 64 * kTwWaves) tl[i] = P.lut[i];
+    constexpr int kTabN = kTmPqN + (DTS_TM_OETF_POW ? 0 : kTmLutN + 1);   // PQ, then OETF
+    __shared__ float2 tl[kTabN];
+    for (int i = threadIdx.x; i < kTabN; i += 64 * kTwWaves) tl[i] = P.lut[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kTwWaves + (threadIdx.x >> 6)));
@@ -492,7 +499,7 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
             sb += wy[k] * h[k].x;
             sr += wy[k] * h[k].y;
         }
-        const int u = q8fma(224.f, sb, 128.f), v = q8fma(224.f, sr, 128.f);
+        const int u = q8c(sb), v = q8c(sr);
         if (!out_col) return;
         if (nv12) {
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u | (v << 8)), wU, 2 * cx, by * dp1, 0);
