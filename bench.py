@@ -58,9 +58,13 @@ WORKLOADS = {
              "desc": "cfg2: 4K60 8-bit yuv420p -> 1080p/720p/854x480 nv12 ABR ladder, bicubic "
                      "(SWS_BITEXACT|ACCURATE_RND semantics), one fused launch per batch"},
     "cfg3": {"src": (SRC_W, SRC_H, D.FMT_P010LE), "outs": [(1920, 1080, D.FMT_YUV420P, D.SCALE_BICUBIC)],
+             # one launch = one 10 s 4K60 segment (600 frames, the JobChunk unit; round 5: 256-frame
+             # launches 86.9 k fps, 600 90.0 k -- the launch tail)
              "tonemap": {"mode": D.TM_HABLE, "desat": 2.0, "peak": 0.0, "npl": 100.0}, "quality": False,
+             "batch": 600, "ring": 600,
              "desc": "cfg3: 4K60 10-bit p010 HDR10 (PQ, bt2020nc) -> SDR bt709 8-bit 1080p yuv420p: bit-exact "
-                     "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB)"},
+                     "bicubic scale to p010 + float zscale/vf_tonemap hable (+-1 LSB), one 10 s segment "
+                     "(600 frames) per launch"},
     "cfg4": {"src": (7680, 4320, D.FMT_YUV420P), "outs": [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)],
              # one launch = one 10 s segment of 8K30 (300 frames: the JobChunk unit, as cfg5's
              # 600-frame 4K60 segments); round 5: 64-frame launches left a 1.5-wave launch tail
