@@ -198,7 +198,7 @@ struct dts_graph {
     const Unit7 *dev_units7 = nullptr;
     const uint32_t *dev_frag7 = nullptr;
     const int32_t *dev_fire7 = nullptr;
-    int ngroups7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
+    int ngroups7 = 0, nluma7 = 0, lds7 = 0, waves7 = 0, hsplit7 = 256;
 
     QScratch qs;                          // dts_graph_run_device's quality partials
     QScratch hqs[2];                      // the host path's, one per slot / stream
@@ -1081,6 +1081,8 @@ static int upload_v7(dts_graph *g, const GraphPlan &gp)
     g->dev_frag7 = reinterpret_cast<const uint32_t *>(base + f_off);
     g->dev_fire7 = reinterpret_cast<const int32_t *>(base + r_off);
     g->ngroups7 = (int)gp.p7.groups.size();
+    g->nluma7 = 0;
+    while (g->nluma7 < g->ngroups7 && gp.p7.groups[(size_t)g->nluma7].kind == 0) ++g->nluma7;
     g->lds7 = gp.p7.lds_bytes;
     g->waves7 = gp.p7.waves;
     g->hsplit7 = gp.p7.hsplit;
@@ -1445,6 +1447,13 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
             q.ngroups = g->ngroups7;
             q.nframes = n;
+            // every frame octet's luma groups, then its chroma groups (round-5 A/B, one box each:
+            // cfg2 171.6-172.5 k -> 179.7-179.9 k fps, cfg1 +5 %, cfg4 +3 %, cfg5 +4 %, cfg3 +1 %
+            // against the octets' groups in plan order); diagnostic DTS_L7_ORDER=0 / 2 for the
+            // plan order / chroma first
+            q.nluma = g->nluma7;
+            q.order = g->nluma7 > 0 && g->nluma7 < g->ngroups7 ? 1 : 0;
+            if (const char *o = diag_env("DTS_L7_ORDER")) q.order = q.order ? std::atoi(o) % 3 : 0;
             q.groups = g->dev_groups7;
             q.units = g->dev_units7;
             q.frag = g->dev_frag7;

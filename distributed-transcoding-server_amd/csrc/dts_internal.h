@@ -354,7 +354,10 @@ struct Group7 {                     // one workgroup's strip of one frame
 struct Ladder7Params {
     DevPlanes src;
     DevPlanes dst[kMaxRungs];
-    int32_t ngroups, nframes, pad_[2];
+    int32_t ngroups, nframes;
+    int32_t order, nluma;           // dispatch order (1: each frame octet's luma groups first, then the
+                                    // chroma groups; 0: plan order; 2: chroma first), the plan's
+                                    // leading kind-0 (luma) groups
     const Group7 *groups;
     const Unit7 *units;
     const uint32_t *frag;           // as Ladder6Params

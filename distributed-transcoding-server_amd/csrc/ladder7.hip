@@ -934,12 +934,30 @@ __attribute__((amdgpu_waves_per_eu(DTS_L7_WPE)))
 #endif
 void k_ladder7(Ladder7Params P)
 {
-    // workgroup b: XCD b % 8; frame 8 (k / ngroups) + b % 8, group k % ngroups (k = b / 8)
+    // workgroup b: XCD b % 8, frame 8 fq + b % 8 of frame octet fq, k = b / 8.  Order 1 (the
+    // default): k runs over every octet's luma groups, then over every octet's chroma groups;
+    // order 0: each octet's groups in plan order (k / ngroups, k % ngroups); order 2: chroma first
     const int b = (int)blockIdx.x, k = b >> 3;
-    const int fq = k / P.ngroups;
+    int fq, gi;
+    if (P.order == 0) {
+        fq = k / P.ngroups;
+        gi = k - fq * P.ngroups;
+    } else {
+        const int nfq = (P.nframes + 7) >> 3;
+        const int n0 = P.order == 1 ? P.nluma : P.ngroups - P.nluma, a0 = P.order == 1 ? 0 : P.nluma;
+        const int n1 = P.ngroups - n0, a1 = P.order == 1 ? P.nluma : 0;
+        if (k < nfq * n0) {
+            fq = k / n0;
+            gi = a0 + (k - fq * n0);
+        } else {
+            const int k1 = k - nfq * n0;
+            fq = k1 / n1;
+            gi = a1 + (k1 - fq * n1);
+        }
+    }
     const int f = 8 * fq + (b & 7);
     if (f >= P.nframes) return;
-    const Group7 G = kld6(P.groups + (k - fq * P.ngroups));
+    const Group7 G = kld6(P.groups + gi);
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), waves = (int)blockDim.x >> 6;
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
