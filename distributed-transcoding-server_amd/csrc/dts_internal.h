@@ -355,6 +355,8 @@ struct Ladder7Params {
     DevPlanes src;
     DevPlanes dst[kMaxRungs];
     int32_t ngroups, nframes;
+    int32_t sup;                    // (diagnostic order 3: octets per luma-then-chroma run)
+    int32_t pad7_;
     int32_t order, nluma;           // dispatch order (1: each frame octet's luma groups first, then the
                                     // chroma groups; 0: plan order; 2: chroma first), the plan's
                                     // leading kind-0 (luma) groups

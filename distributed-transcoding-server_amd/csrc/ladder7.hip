@@ -942,6 +942,18 @@ void k_ladder7(Ladder7Params P)
     if (P.order == 0) {
         fq = k / P.ngroups;
         gi = k - fq * P.ngroups;
+    } else if (P.order == 3) {              // diagnostic: luma then chroma per run of P.sup octets
+        const int run = P.sup * P.ngroups, r = k / run, kr = k - r * run;
+        const int nfq = (P.nframes + 7) >> 3, s0 = r * P.sup, ns = min(P.sup, nfq - s0);
+        const int nl = P.nluma, nc = P.ngroups - nl;
+        if (kr < ns * nl) {
+            fq = s0 + kr / nl;
+            gi = kr % nl;
+        } else {
+            const int k1 = kr - ns * nl;
+            fq = s0 + k1 / nc;
+            gi = nl + k1 % nc;
+        }
     } else {
         const int nfq = (P.nframes + 7) >> 3;
         const int n0 = P.order == 1 ? P.nluma : P.ngroups - P.nluma, a0 = P.order == 1 ? 0 : P.nluma;
