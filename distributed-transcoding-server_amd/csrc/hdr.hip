@@ -136,18 +136,27 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
         break;
     case DTS_TM_CLIP: sig = fminf(fmaxf(sig * P.param, 0.f), 1.f); break;
     case DTS_TM_REINHARD: sig = sig / (sig + P.param) * (P.peak + P.param) / P.peak; break;
-    case DTS_TM_HABLE: sig = hable(sig); break;               // / hpeak: folded into k below
+    case DTS_TM_HABLE: break;                                 // folded into k below
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
 #if DTS_TM_OETF_POW
     (void)oetf;
-    const float k = sig * ((MODE == DTS_TM_HABLE ? P.inv_hpeak : 1.f) * rcp(sig0));
+    const float k = (MODE == DTS_TM_HABLE ? hable(sig0) * P.inv_hpeak : sig) * rcp(sig0);
     r = oetf709(r * k);
     g = oetf709(g * k);
     b = oetf709(b * k);
 #else
-    const float k = sig * ((MODE == DTS_TM_HABLE ? P.inv_hpeak_n : N) * rcp(sig0));
+    // k = sig / sig0 x N; hable's sig / sig0 = (num / den - e / f) / sig0 = (num - (e / f) den) /
+    // (den sig0): one reciprocal instead of two (1 / hpeak and N in inv_hpeak_n)
+    float k;
+    if (MODE == DTS_TM_HABLE) {
+        const float num = __builtin_fmaf(sig0, __builtin_fmaf(sig0, 0.15f, 0.05f), 0.004f);
+        const float den = __builtin_fmaf(sig0, __builtin_fmaf(sig0, 0.15f, 0.50f), 0.06f);
+        k = __builtin_fmaf(-0.02f / 0.30f, den, num) * (P.inv_hpeak_n * rcp(den * sig0));
+    } else {
+        k = sig * (N * rcp(sig0));
+    }
     r = lut(oetf, r * k);
     g = lut(oetf, g * k);
     b = lut(oetf, b * k);
