@@ -1453,7 +1453,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             // plan order / chroma first
             q.nluma = g->nluma7;
             q.order = g->nluma7 > 0 && g->nluma7 < g->ngroups7 ? 1 : 0;
-            if (const char *o = diag_env("DTS_L7_ORDER")) q.order = q.order ? std::atoi(o) % 4 : 0;
+            if (const char *o = diag_env("DTS_L7_ORDER")) q.order = q.order ? std::min(std::max(std::atoi(o), 0), 3) : 0;
             q.sup = 4;
             if (const char *o = diag_env("DTS_L7_SUP")) q.sup = std::max(1, std::atoi(o));
             q.groups = g->dev_groups7;
