@@ -1447,10 +1447,11 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             for (int k = 0; k < kMaxRungs; ++k) q.dst[k] = pp.dst[k];
             q.ngroups = g->ngroups7;
             q.nframes = n;
-            // every frame octet's luma groups, then its chroma groups (round-5 A/B, one box each:
-            // cfg2 171.6-172.5 k -> 179.7-179.9 k fps, cfg1 +5 %, cfg4 +3 %, cfg5 +4 %, cfg3 +1 %
-            // against the octets' groups in plan order); diagnostic DTS_L7_ORDER=0 / 2 for the
-            // plan order / chroma first
+            // the luma groups of every frame octet, then the chroma groups of every octet: one
+            // switch of plane kind per launch (round-5 A/B, one box each: cfg2 171.6-172.5 k ->
+            // 179.7-179.9 k fps, cfg1 +5 %, cfg4 +3 %, cfg5 +4 %, cfg3 +1 % against each octet's
+            // groups in plan order); diagnostic DTS_L7_ORDER=0 / 2 / 3 for the plan order, chroma
+            // first, luma-then-chroma runs of DTS_L7_SUP octets
             q.nluma = g->nluma7;
             q.order = g->nluma7 > 0 && g->nluma7 < g->ngroups7 ? 1 : 0;
             if (const char *o = diag_env("DTS_L7_ORDER")) q.order = q.order ? std::min(std::max(std::atoi(o), 0), 3) : 0;
