@@ -266,8 +266,11 @@ int dts_graph_wait(dts_graph *g);
  * DMA straight from the caller's planes, and a chunk whose output frames all do is copied
  * straight into them: no pass through the library's pinned rings (the host threads'
  * pack / unpack copies, which bound the pageable path).  Frames anywhere else take the
- * ring as before.  dts_host_alloc: page-locked memory usable by every device
- * (hipHostMalloc portable), released by dts_host_free.  dts_host_register: page-lock a
+ * ring as before.  Direct frames need the device batch's row pitch (row bytes rounded up
+ * to 16); consecutive frames laid out exactly as the device batch (planes rounded up to
+ * 256 bytes, frames back to back) move as one DMA per run, the padding bytes between their
+ * planes included (an output run overwrites them).  dts_host_alloc: page-locked memory
+ * usable by every device (hipHostMalloc portable), released by dts_host_free.  dts_host_register: page-lock a
  * caller range (hipHostRegister portable) until dts_host_unregister.  Replaces the
  * pageable frame buffers an ffmpeg worker's decoder / encoder hand around. */
 int dts_host_alloc(size_t bytes, void **out);
