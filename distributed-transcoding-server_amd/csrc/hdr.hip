@@ -76,11 +76,13 @@ template <class T> __device__ __forceinline__ void gst(uint64_t a, T v) { *(__at
 
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+#if DTS_TM_OETF_POW
 __device__ __forceinline__ float hable(float in)
 {
     const float a = 0.15f, b = 0.50f, c = 0.10f, d = 0.20f, e = 0.02f, f = 0.30f;
     return (in * (in * a + b * c) + d * e) * rcp(in * (in * a + b) + d * f) - e / f;
 }
+#endif
 
 __device__ __forceinline__ float mobius(float in, float j, float peak)
 {
