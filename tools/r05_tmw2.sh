@@ -7,7 +7,7 @@ mkdir -p gpurun_out/r05t2
 timeout -k 10 300 python -u -m pytest tests/test_gpu_hdr.py tests/test_gpu_bench_paths.py -m gpu -q -k "hdr or cfg3 or tonemap or p010" \
     --timeout 150 --timeout-method thread > gpurun_out/r05t2/tests.log 2>&1
 rc=$?; echo "hdr tests rc=$rc $(tail -1 gpurun_out/r05t2/tests.log)"; [ $rc -ne 0 ] && exit $rc
-AB_WORKLOADS=cfg3 bash tools/ab_libs.sh ${AB_LIBS:-tmold "" tmold ""} || exit 1
+AB_WORKLOADS=cfg3 bash tools/ab_libs.sh ${AB_LIBS:-base} || exit 1
 timeout -k 10 -s KILL 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r05t2/kt -o kt --output-format csv -- \
     python3 bench.py --workload cfg3 --steps 8 --warmup 2 --no-cpu --no-verify > gpurun_out/r05t2/kt.log 2>&1
 echo "kt rc=$?"
