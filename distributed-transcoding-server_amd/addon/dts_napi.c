@@ -9,6 +9,7 @@
  * blocks; results resolve a Promise.  Written for Node 12 / N-API 8 (plain C,
  * no node-addon-api), built by gcc against /usr/include/node.
  */
+#include <pthread.h>
 #include <node_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -658,13 +659,30 @@ static napi_value js_synth_frame(napi_env env, napi_callback_info info)
 /* ---- hostAlloc(bytes) -> Buffer in pinned memory (dts_host_alloc, ABI 7) ----------
  * Frames whose planes are views of such a Buffer (pitches = the device layout's, i.e.
  * row bytes rounded up to 16) cross PCIe by one DMA per plane in run(), without the
- * library's ring copies.  The memory is released (dts_host_free) when the Buffer is
- * garbage collected; keep it alive until run() settles. */
+ * library's ring copies.  The memory is released (dts_host_free) after the Buffer is
+ * garbage collected; keep it alive until run() settles.  The release runs on a detached
+ * thread of its own, never in the finalizer on the event loop: hipHostFree synchronises
+ * the device, which would block the loop until every slot's in-flight work had drained
+ * (ADVICE r05). */
+static void *host_free_thread(void *p)
+{
+    dts_host_free(p);
+    return NULL;
+}
+
 static void host_free_cb(napi_env env, void *data, void *hint)
 {
     (void)env;
     (void)hint;
-    dts_host_free(data);
+    pthread_t t;
+    pthread_attr_t a;
+    if (pthread_attr_init(&a) == 0) {
+        pthread_attr_setdetachstate(&a, PTHREAD_CREATE_DETACHED);
+        const int ok = pthread_create(&t, &a, host_free_thread, data) == 0;
+        pthread_attr_destroy(&a);
+        if (ok) return;
+    }
+    dts_host_free(data);                /* (no thread: free here rather than leak) */
 }
 
 static napi_value js_host_alloc(napi_env env, napi_callback_info info)

@@ -2297,11 +2297,22 @@ int dts_host_register(void *p, size_t bytes)
     if (!p || !bytes) return DTS_E_INVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return DTS_E_NODEV;
+    // a range overlapping one the set already holds (an allocation or another registration) is
+    // refused: one record per byte keeps dts_host_free / pinned_range unambiguous
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    PinnedSet &ps = pinned_set();
+    std::lock_guard<std::mutex> lk(ps.m);
+    {
+        auto it = ps.r.lower_bound(a);                  // first base >= a: must start at or past a + bytes
+        if (it != ps.r.end() && it->first < a + bytes) return DTS_E_INVAL;
+        if (it != ps.r.begin()) {                       // the base below a: must end at or before a
+            --it;
+            if (it->first + it->second.first > a) return DTS_E_INVAL;
+        }
+    }
     if (hipHostRegister(p, bytes, hipHostRegisterPortable) != hipSuccess) return DTS_E_HIP;
     try {
-        PinnedSet &ps = pinned_set();
-        std::lock_guard<std::mutex> lk(ps.m);
-        ps.r[reinterpret_cast<uintptr_t>(p)] = {bytes, true};
+        ps.r[a] = {bytes, true};
     } catch (...) {
         hipHostUnregister(p);
         return DTS_E_NOMEM;

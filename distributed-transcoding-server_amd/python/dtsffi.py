@@ -10,6 +10,7 @@ nv12 / p010le -> [Y, UV, None] (p010 planes hold raw little-endian bytes).
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -223,7 +224,20 @@ class PinnedBuffer:
         check(lib().dts_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
         self.ptr = p.value
         self.nbytes = nbytes
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.ptr))
+        self._arr = None
+
+    @property
+    def array(self):
+        """The buffer as a uint8 array.  Every view of it keeps this object (and so the pinned
+        memory) alive: the ctypes array under the numpy base holds a reference to it, so
+        dropping the PinnedBuffer while frames carved from it live frees nothing."""
+        a = self._arr() if self._arr is not None else None
+        if a is None:
+            carr = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+            carr._owner = self
+            a = np.ctypeslib.as_array(carr)
+            self._arr = weakref.ref(a)
+        return a
 
     def __del__(self):
         if getattr(self, "ptr", None):
@@ -241,6 +255,7 @@ def alloc_frames_pinned(w, h, fmt, n, pitch_align=16):
     sizes = [0 if s is None else (s[0] * p + 255) // 256 * 256 for s, p in zip(shapes, pitches)]
     fb = sum(sizes)
     buf = PinnedBuffer(max(1, fb * n))
+    arr = buf.array
     frames = []
     for i in range(n):
         off, planes = i * fb, []
@@ -248,7 +263,7 @@ def alloc_frames_pinned(w, h, fmt, n, pitch_align=16):
             if s is None:
                 planes.append(None)
                 continue
-            planes.append(buf.array[off:off + s[0] * p].reshape(s[0], p)[:, :s[1]])
+            planes.append(arr[off:off + s[0] * p].reshape(s[0], p)[:, :s[1]])
             off += z
         frames.append(planes)
     return frames, buf
@@ -439,8 +454,8 @@ class Graph:
         src = (Frame * ns)(*[frame_struct(f) for f in frames])
         if pinned_out:
             pa = 16 if pinned_out is True else int(pinned_out)
+            # (each output plane is a view that keeps its PinnedBuffer alive)
             per = [alloc_frames_pinned(s.out[k].w, s.out[k].h, s.out[k].fmt, n, pa) for k in range(s.nout)]
-            self._pinned_keep = [b for (_f, b) in per]
             outs = [[per[k][0][f] for k in range(s.nout)] for f in range(n)]
         else:
             outs = [[alloc_frame(s.out[k].w, s.out[k].h, s.out[k].fmt) for k in range(s.nout)] for _ in range(n)]

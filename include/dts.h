@@ -271,7 +271,8 @@ int dts_graph_wait(dts_graph *g);
  * 256 bytes, frames back to back) move as one DMA per run, the padding bytes between their
  * planes included (an output run overwrites them).  dts_host_alloc: page-locked memory
  * usable by every device (hipHostMalloc portable), released by dts_host_free.  dts_host_register: page-lock a
- * caller range (hipHostRegister portable) until dts_host_unregister.  Replaces the
+ * caller range (hipHostRegister portable) until dts_host_unregister; a range overlapping an
+ * allocation or another registered range is refused (DTS_E_INVAL).  Replaces the
  * pageable frame buffers an ffmpeg worker's decoder / encoder hand around. */
 int dts_host_alloc(size_t bytes, void **out);
 void dts_host_free(void *p);

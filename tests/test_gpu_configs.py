@@ -122,6 +122,33 @@ def test_host_path_pinned_frames(ctx, pin_src, pin_out):
     del keep
 
 
+def test_pinned_outputs_outlive_the_next_call(ctx):
+    """Pinned outputs of one run_host call stay valid after later pinned calls and after the
+    PinnedBuffer object itself is dropped: every plane view keeps its allocation alive (ADVICE
+    r05: the second call used to free the first call's buffers under the caller's views)."""
+    import gc
+    sw, sh, n = 256, 144, 3
+    spec = [(128, 72, D.FMT_NV12, D.SCALE_BICUBIC), (64, 36, D.FMT_YUV420P, D.SCALE_BILINEAR)]
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_YUV420P, spec, max_batch=2))
+    runs = []
+    for seed in (5, 6, 7):
+        frames = [D.synth_host(sw, sh, D.FMT_YUV420P, 0, seed, f) for f in range(n)]
+        outs, _ = g.run_host(frames, pinned_out=True)
+        runs.append((frames, outs))
+        gc.collect()
+    g.close()
+    for frames, outs in runs:
+        for f in range(n):
+            for k, (w, h, fmt, m) in enumerate(spec):
+                want = orc.scale_frame(frames[f], sw, sh, D.FMT_YUV420P, w, h, fmt, m)
+                assert planes_equal(outs[f][k], want), (f, k)
+    frames, buf = D.alloc_frames_pinned(64, 36, D.FMT_YUV420P, 2)
+    del buf
+    gc.collect()
+    frames[1][0][...] = 9                       # the allocation is still there
+    assert int(frames[1][0].sum()) == 9 * 64 * 36
+
+
 def test_host_register_roundtrip(ctx):
     """dts_host_register / dts_host_unregister a caller range; frees of unknown pointers are
     ignored and a double unregister is an error."""
@@ -135,3 +162,15 @@ def test_host_register_roundtrip(ctx):
     p = D.PinnedBuffer(4096)
     p.array[:] = 7
     assert int(p.array.sum()) == 7 * 4096
+    # overlapping ranges are refused (one record per pinned byte): inside an allocation, across
+    # a registered range's start or end, and the same base twice
+    assert L.dts_host_register(ctypes.c_void_p(p.ptr + 1024), 1024) == D.E_INVAL
+    base = buf.ctypes.data
+    assert L.dts_host_register(ctypes.c_void_p(base + 65536), 65536) == 0
+    assert L.dts_host_register(ctypes.c_void_p(base + 65536), 4096) == D.E_INVAL
+    assert L.dts_host_register(ctypes.c_void_p(base), 65536 + 1) == D.E_INVAL
+    assert L.dts_host_register(ctypes.c_void_p(base + 65536 + 4096), 65536) == D.E_INVAL
+    assert L.dts_host_register(ctypes.c_void_p(base), 65536) == 0          # adjacent: fine
+    assert L.dts_host_unregister(ctypes.c_void_p(base)) == 0
+    assert L.dts_host_unregister(ctypes.c_void_p(base + 65536)) == 0
+    assert int(p.array.sum()) == 7 * 4096                                   # (the allocation untouched)
