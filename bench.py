@@ -417,7 +417,7 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="time the host-memory path (dts_graph_submit / wait) instead of device-resident batches")
-    # (round 5, tools/r05_e2e.sh: submits of 512 frames in chunks of 64 3,174-3,270 fps against 2,918-3,032 for
+    # (round 5, tools/e2e.sh: submits of 512 frames in chunks of 64 3,174-3,270 fps against 2,918-3,032 for
     # 128 / 32, pageable or pinned alike)
     ap.add_argument("--e2e-batch", type=int, default=64, help="--e2e: frames per device chunk (max_batch)")
     ap.add_argument("--e2e-submit", type=int, default=512, help="--e2e: frames per submit")
