@@ -633,7 +633,8 @@ def main():
                     "frames per GPU",
             "config": {"workload": wl["desc"], "src": f"{sw}x{sh} {FMTS[sfmt]}",
                        "outputs": [f"{w}x{h} {FMTS[fmt]}" for (w, h, fmt, _m) in wl["outs"]],
-                       "batch_frames": B, "parallelism": f"segments x{world} (one process per GPU)"},
+                       "batch_frames": B, "frames_per_launch": B,
+                       "parallelism": f"segments x{world} (one process per GPU)"},
             "mpixel_per_s": round(fps * sw * sh / 1e6, 1),
             "verified_vs_oracle": verified, "hip_runtime": runtimes,
             "algo_bytes_per_frame": algo,

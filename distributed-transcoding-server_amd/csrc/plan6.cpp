@@ -286,6 +286,12 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
         }
         const int ngran = (in.srcH + kL6Gran - 1) / kL6Gran;
         const int nrb = (int)p.r.fire.size();
+        // k_ladder7 reads a fire entry's granule from its low 10 bits (the fragment index of
+        // a deduplicated rendition rides above them): a granule that does not fit keeps the
+        // graph off v7 rather than corrupt its V schedule (validate_spec's 16384-row
+        // cap gives at most 1024 granules today)
+        for (int jb = 0; jb < nrb; ++jb)
+            if (p.r.fire[jb] < 0 || p.r.fire[jb] >= 1024) return false;
         // V fragment slots: the fragments of the row blocks firing in granules q .. q + fs_window - 1
         // are in LDS together (each is DMA'd with the source of its fire granule)
         int fs = 1;
