@@ -321,6 +321,9 @@ TonemapParams tonemap_params(const dts_tonemap_spec &t)
     p.hpeak = (float)hable((float)peak);
     p.inv_hpeak = 1.0f / p.hpeak;
     p.inv_hpeak_n = (float)kTmLutN / p.hpeak;
+    // (hdr.hip pixel<>: the constant terms of hable(x) - hable's E / F cancel, DE = (E / F) DF)
+    p.hk1 = (float)(0.15 * (1.0 - 0.02 / 0.30) * kTmLutN / (double)p.hpeak);
+    p.hk0 = (float)(0.50 * (0.10 - 0.02 / 0.30) * kTmLutN / (double)p.hpeak);
     p.scale = (float)(10000.0 / npl);
     bt2020_to_bt709(p.m);
     return p;

@@ -417,6 +417,7 @@ struct TonemapParams {
     int32_t mode;                   // DTS_TM_*
     float param, desat, peak, hpeak, inv_hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
     float inv_hpeak_n;              // kTmLutN / hpeak (hable's normalisation folded into the OETF table scale)
+    float hk1, hk0;                 // hable(x) / x = (A (1 - E/F) x + B (C - E/F)) / den, x kTmLutN / hpeak
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
     const float2 *lut;              // device [2][kTmLutN + 1] (intercept, slope) chords in table units: PQ EOTF
                                     // x 10000 / npl, BT.709 OETF

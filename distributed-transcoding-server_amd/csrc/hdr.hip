@@ -101,7 +101,7 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
                                       float2 &C)
 {
     if (DTS_TM_ABLATE & 4) {
-        Y = y10 * (1.f / 1024.f);
+        Y = y10 * (219.f / 1024.f) + 16.5f;
         C = c;
         return;
     }
@@ -118,18 +118,25 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     const float gp = __builtin_fmaf(c.x, -2.f * kb2 * (1.f - kb2) / kg2 * N,
                                     __builtin_fmaf(c.y, -2.f * kr2 * (1.f - kr2) / kg2 * N, yy));
     const float r0 = lut_pq(pq, rp), g0 = lut_pq(pq, gp), b0 = lut_pq(pq, bp);
-    float r = P.m[0] * r0 + P.m[1] * g0 + P.m[2] * b0;
-    float g = P.m[3] * r0 + P.m[4] * g0 + P.m[5] * b0;
-    float b = P.m[6] * r0 + P.m[7] * g0 + P.m[8] * b0;
-    // vf_tonemap.c tonemap()
+    const float r = P.m[0] * r0 + P.m[1] * g0 + P.m[2] * b0;
+    const float g = P.m[3] * r0 + P.m[4] * g0 + P.m[5] * b0;
+    const float b = P.m[6] * r0 + P.m[7] * g0 + P.m[8] * b0;
+    // vf_tonemap.c tonemap(), desaturation as one affine map per channel (round 6): MIX(x, luma,
+    // ob) = u x + ol with u = 1 - ob and ol = ob luma, where ob = max(luma - desat, 1e-6) /
+    // max(luma, 1e-6); ol = min(t, luma) for t = max(luma - desat, 1e-6) (luma >= 1e-6: t;
+    // below: luma).  u >= 0, so sig = max(r', g', b') = u max(r, g, b) + ol, and the final
+    // r' sig / sig0 folds into the OETF argument as one fma per channel: r (u k) + ol k
+    float u = 1.f, ol = 0.f, sig0;
+    const float mx = __builtin_fmaxf(__builtin_fmaxf(r, g), b);
     if (DESAT) {
         const float luma = kr7 * r + kg7 * g + kb7 * b;
-        const float ob = fmaxf(luma - P.desat, 1e-6f) * rcp(fmaxf(luma, 1e-6f));   // (v_rcp: an IEEE divide is ~10 VALU)
-        r = r * (1.f - ob) + luma * ob;
-        g = g * (1.f - ob) + luma * ob;
-        b = b * (1.f - ob) + luma * ob;
+        const float lm = fmaxf(luma, 1e-6f), t = fmaxf(luma - P.desat, 1e-6f);
+        u = (lm - t) * rcp(lm);                               // (v_rcp: an IEEE divide is ~10 VALU)
+        ol = fminf(t, luma);
+        sig0 = fmaxf(__builtin_fmaf(u, mx, ol), 1e-6f);
+    } else {
+        sig0 = fmaxf(mx, 1e-6f);
     }
-    const float sig0 = fmaxf(fmaxf(fmaxf(r, g), b), 1e-6f);
     float sig = sig0;
     switch (MODE) {
     case DTS_TM_LINEAR: sig = sig * P.param / P.peak; break;
@@ -142,34 +149,47 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
     case DTS_TM_MOBIUS: sig = mobius(sig, P.param, P.peak); break;
     default: break;
     }
+    float rr, gg, bb;
 #if DTS_TM_OETF_POW
     (void)oetf;
     const float k = (MODE == DTS_TM_HABLE ? hable(sig0) * P.inv_hpeak : sig) * rcp(sig0);
-    r = oetf709(r * k);
-    g = oetf709(g * k);
-    b = oetf709(b * k);
+    rr = oetf709(__builtin_fmaf(r, u, ol) * k);
+    gg = oetf709(__builtin_fmaf(g, u, ol) * k);
+    bb = oetf709(__builtin_fmaf(b, u, ol) * k);
 #else
-    // k = sig / sig0 x N; hable's sig / sig0 = (num / den - e / f) / sig0 = (num - (e / f) den) /
-    // (den sig0): one reciprocal instead of two (1 / hpeak and N in inv_hpeak_n)
+    // k = sig / sig0 x N.  hable: hable(x) = (x (Ax + CB) + DE) / (x (Ax + B) + DF) - E / F, and the
+    // constant terms cancel exactly (DE - (E / F) DF = 0), so hable(x) / x = (A (1 - E/F) x +
+    // B (C - E/F)) / (x (Ax + B) + DF): k = (hk1 sig0 + hk0) / den with N / hable(peak) folded
+    // into hk1, hk0 (api.cpp tonemap_params) -- one reciprocal, no cancellation near 0
     float k;
     if (MODE == DTS_TM_HABLE) {
-        const float num = __builtin_fmaf(sig0, __builtin_fmaf(sig0, 0.15f, 0.05f), 0.004f);
         const float den = __builtin_fmaf(sig0, __builtin_fmaf(sig0, 0.15f, 0.50f), 0.06f);
-        k = __builtin_fmaf(-0.02f / 0.30f, den, num) * (P.inv_hpeak_n * rcp(den * sig0));
+        k = __builtin_fmaf(sig0, P.hk1, P.hk0) * rcp(den);
     } else {
         k = sig * (N * rcp(sig0));
     }
-    r = lut(oetf, r * k);
-    g = lut(oetf, g * k);
-    b = lut(oetf, b * k);
+    if (DESAT) {
+        const float ku = u * k, ko = ol * k;
+        rr = lut(oetf, __builtin_fmaf(r, ku, ko));
+        gg = lut(oetf, __builtin_fmaf(g, ku, ko));
+        bb = lut(oetf, __builtin_fmaf(b, ku, ko));
+    } else {
+        rr = lut(oetf, r * k);
+        gg = lut(oetf, g * k);
+        bb = lut(oetf, b * k);
+    }
 #endif
-    Y = kr7 * r + kg7 * g + kb7 * b;
-    C = make_float2((b - Y) * (1.f / (2.f * (1.f - kb7))), (r - Y) * (1.f / (2.f * (1.f - kr7))));
+    // Y returned as 219 Y' + 16.5 (the quantiser's scale and rounding half folded into the
+    // weights: q8y is one truncation); Cb' = (B' - Y') / (2 (1 - kb)) from that
+    constexpr float sb = 1.f / (2.f * (1.f - kb7)), sr = 1.f / (2.f * (1.f - kr7));
+    Y = __builtin_fmaf(219.f * kb7, bb, __builtin_fmaf(219.f * kg7, gg, __builtin_fmaf(219.f * kr7, rr, 16.5f)));
+    C = make_float2(__builtin_fmaf(bb, sb, __builtin_fmaf(Y, -sb / 219.f, sb * 16.5f / 219.f)),
+                    __builtin_fmaf(rr, sr, __builtin_fmaf(Y, -sr / 219.f, sr * 16.5f / 219.f)));
 }
 
 // Y' = kr R' + kg G' + kb B' with R', G', B' in [0, 1] (the OETF table's values, or oetf709's):
-// 219 Y' + 16.5 lies in [16.5, 235.5], so the quantiser needs no clip
-__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)__builtin_fmaf(219.f, Y, 16.5f); }
+// pixel<> returns 219 Y' + 16.5, in [16.5, 235.5], so the quantiser is a truncation, no clip
+__device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)Y; }
 // Cb', Cr' in [-1/2, 1/2] for the same reason: 224 C + 128.5 in [16.5, 240.5]
 __device__ __forceinline__ int q8c(float C) { return (int)__builtin_fmaf(224.f, C, 128.5f); }
 
