@@ -580,14 +580,10 @@ bool l7_narrow()
 // The diagnostic DTS_L7_W fixes the width.
 bool plan7_sized(const Plan5In *ins, bool narrow, Plan7 &out)
 {
-    // a k_ladder7 built with its store wave (DTS_L7_SW) gets groups of one unit fewer plus that wave
-    int stw = 0, defer = 0;
-    ladder7_store_wave(&stw, &defer);
-    const int sw = stw ? 1 + defer : 0;
-    if (!plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), narrow, out, sw)) return false;
+    if (!plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), narrow, out)) return false;
     if (diag_env("DTS_L7_W") || 2 * out.lds_bytes <= 160 * 1024) return true;
     Plan7 wide;
-    if (plan7_graph(ins, 10, l7_stages(), l7_pb(), l7_by_rung(), narrow, wide, sw) && wide.lds_bytes <= 160 * 1024)
+    if (plan7_graph(ins, 10, l7_stages(), l7_pb(), l7_by_rung(), narrow, wide) && wide.lds_bytes <= 160 * 1024)
         out = std::move(wide);
     return true;
 }

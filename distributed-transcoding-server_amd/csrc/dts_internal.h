@@ -349,10 +349,6 @@ struct Group7 {                     // one workgroup's strip of one frame
                                     // chroma: U V 16-bit pairs); bpc npc pieces per plane and granule
     int32_t st0;                    // first staging wave: waves st0.. deal the source pieces (a group's spare
                                     // waves when it has fewer units than the workgroup has waves, else all)
-    int32_t stw;                    // 1: the workgroup's last wave is the group's store wave (DTS_L7_SW builds):
-                                    // the unit waves leave each row block in an LDS slot (two per unit wave,
-                                    // by batch parity, at scr) and it writes them out, so no unit wave's
-                                    // vmcnt ever counts a store; it stages nothing
 };
 
 struct Ladder7Params {
@@ -373,7 +369,6 @@ struct Ladder7Params {
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
                           int src_kind, hipStream_t s);   // src_kind: SrcKind
 void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
-void ladder7_store_wave(int *store_wave, int *defer);   // DTS_L7_SW / DTS_L7_DEFER of the linked k_ladder7
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

@@ -140,10 +140,6 @@ struct Plan7 {
 };
 // Groups of at most wmax units; a group's spare waves (if any) stage its pieces, else all its
 // waves deal them, and each rendition's lead wave DMAs its V fragments.
-// stw (> 0: the kernel has a store wave; its value - 1 is the kernel's V deferral, DTS_L7_DEFER):
-// groups of at most wmax - 1 units and one more wave that stores their row blocks, unless a unit
-// would leave two row blocks in one staging batch (then the plan is made without it)
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out,
-                 int stw = 0);
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out);
 
 } // namespace dts

@@ -73,9 +73,6 @@
 #ifndef DTS_L7_PAIR
 #define DTS_L7_PAIR (kL7Batch == 2)  // 1: stage 2 granules per batch (one barrier per 2 granules); plan with DTS_L7_PB=2
 #endif
-#ifndef DTS_L7_SW
-#define DTS_L7_SW 0         // 1: a store wave per group writes the unit waves' row blocks out (Group7::stw)
-#endif
 #ifndef DTS_L7_STAMP
 #define DTS_L7_STAMP 0      // diagnostic builds only: per-variant, per-phase s_memtime sums (tools/stamp7.py)
 #endif
@@ -168,10 +165,9 @@ struct Stage7 {
         ppp = bpc * npc;
         npieces = np * ppp;
         nown = min(ppp, ((G.xown - G.X0) * bpc + 63) >> 6);
-        // the staging waves st0.. deal the pieces (Group7::st0); never the store wave (the last)
-        const int last = waves - G.stw;
-        w = wave >= G.st0 && wave < last ? wave - G.st0 : npieces;
-        nw = last - G.st0;
+        // the staging waves st0.. deal the pieces (Group7::st0)
+        w = wave >= G.st0 ? wave - G.st0 : npieces;
+        nw = waves - G.st0;
         srcH1 = G.srcH - 1;
         ngran = G.ngran;
         stage_bytes = PB7 * npieces * 1024;
@@ -325,14 +321,15 @@ __device__ __forceinline__ void xchg7p(const UT &U, const uint32_t (&v)[Walk6<VA
 
 // the stores of row block j from x (xchg7); returns the store instructions issued (edge
 // units' byte stores are not counted, which only makes the next source wait longer)
-template <int CTv, int NPv, class UT>
-__device__ __forceinline__ int vstore7c(const UT &U, int j, const uint32_t (&x)[4], const uint64_t (&ob)[2],
-                                        const uint32_t (&op)[2], int lane)
+template <int VAR, class UT>
+__device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4], const uint64_t (&ob)[2],
+                                       const uint32_t (&op)[2], int lane)
 {
+    using W = Walk6<VAR>;
     const int y = (DTS_L7_ABLATE & 512) ? 0 : 16 * j + (lane >> 2), q4 = lane & 3;
     if (y < U.dstH) {
-        if (CTv == 1 && U.fmt == DTS_FMT_P010LE) {        // p010 renditions (xchg7p)
-            if (NPv == 1) {
+        if (W::CT == 1 && U.fmt == DTS_FMT_P010LE) {        // p010 renditions (xchg7p)
+            if (W::NP == 1) {
                 const uint32_t o[2] = {x[0], x[1]};
                 const int at = 2 * U.col0 + 8 * q4;
                 put_row6<8>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
@@ -341,24 +338,24 @@ __device__ __forceinline__ int vstore7c(const UT &U, int j, const uint32_t (&x)[
                 const int at = 4 * U.col0 + 16 * q4;
                 put_row6<16>(ob[0] + (uint64_t)y * op[0], at, 4 * U.dstW - at, o);
             }
-        } else if (NPv == 1) {
-            if (CTv == 4) {
+        } else if (W::NP == 1) {
+            if (W::CT == 4) {
                 const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
                 put_row6<16>(ob[0] + (uint64_t)y * op[0], U.col0 + 16 * q4, U.dstW - U.col0 - 16 * q4, o);
-            } else if (CTv == 1) {
+            } else if (W::CT == 1) {
                 const uint32_t o[1] = {x[0]};
                 put_row6<4>(ob[0] + (uint64_t)y * op[0], U.col0 + 4 * q4, U.dstW - U.col0 - 4 * q4, o);
             } else {
                 const uint32_t o[2] = {x[0], x[1]};
                 put_row6<8>(ob[0] + (uint64_t)y * op[0], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
             }
-        } else if (U.fmt == DTS_FMT_NV12 && CTv == 2) {
+        } else if (U.fmt == DTS_FMT_NV12 && W::CT == 2) {
             const uint32_t o[4] = {x[0], x[1], x[2], x[3]};
             const int at = 2 * U.col0 + 16 * q4;
             put_row6<16>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
         } else if (U.fmt == DTS_FMT_NV12) {
 #pragma unroll
-            for (int c = 0; c < CTv; ++c) {
+            for (int c = 0; c < W::CT; ++c) {
                 const uint32_t o[2] = {x[2 * c], x[2 * c + 1]};
                 const int at = 2 * U.col0 + 32 * c + 8 * q4;
                 put_row6<8>(ob[0] + (uint64_t)y * op[0], at, 2 * U.dstW - at, o);
@@ -366,7 +363,7 @@ __device__ __forceinline__ int vstore7c(const UT &U, int j, const uint32_t (&x)[
         } else {
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                if (CTv == 2) {
+                if (W::CT == 2) {
                     const uint32_t o[2] = {x[2 * p], x[2 * p + 1]};
                     put_row6<8>(ob[p] + (uint64_t)y * op[p], U.col0 + 8 * q4, U.dstW - U.col0 - 8 * q4, o);
                 } else {
@@ -376,14 +373,7 @@ __device__ __forceinline__ int vstore7c(const UT &U, int j, const uint32_t (&x)[
             }
         }
     }
-    return NPv == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
-}
-
-template <int VAR, class UT>
-__device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4], const uint64_t (&ob)[2],
-                                       const uint32_t (&op)[2], int lane)
-{
-    return vstore7c<Walk6<VAR>::CT, Walk6<VAR>::NP>(U, j, x, ob, op, lane);
+    return W::NP == 1 ? 1 : (U.fmt == DTS_FMT_NV12 ? 1 : 2);
 }
 
 // V of one row block over the whole ring, as vcalc (ladder_mfma.h): 65536 hh + 256 (hl +
@@ -498,104 +488,9 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
         sq = sq + 1 == NS7 ? 0 : sq + 1;
         L7_STAMP(2);
     }
-    if (DTS_L7_SW && G.stw) {                   // the unit waves' barriers A and B (walk7)
-        group_barrier7();
-        group_barrier7();
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     L7_STAMP_DONE(kL7Variants, G.ngran);
 }
-
-#if DTS_L7_SW
-// The group's store wave (Group7::stw, the workgroup's last wave).  A unit wave leaves row block
-// j, exchanged into row segments, in its slot of the batch's parity and sets the slot's header to
-// j + 1 (walk7 vfire); after the next barrier this wave reads the slot and writes the row block
-// out exactly as the unit wave would have (vstore7c), then clears the header.  The slots of
-// parity b & 1 are written in batch b, drained in batch b + 1 and written again in batch b + 2:
-// the barrier between is the handover both ways.  After the walk: barrier A (batch nb - 1's row
-// blocks), the unit waves' last row blocks into parity nb & 1, barrier B.  The unit waves' vmcnt
-// then counts only their loads, so the counted wait for a staging batch never waits on a store.
-// the fields of a Unit7 vstore7c reads (the store wave's copy, from lane registers)
-struct UnitS7 {
-    int32_t dstH, fmt, col0, dstW;
-};
-
-template <int SK>
-__device__ __forceinline__ void store7(const Ladder7Params &P, const Group7 &G, int f, int waves)
-{
-    extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
-    const int lane = (int)threadIdx.x & 63;
-    const int nu = waves - 1, nw = G.nwaves;
-    uint32_t *shdr = reinterpret_cast<uint32_t *>(lds7 + G.scr + 2048 * nu);
-    if (lane < 2 * nu) shdr[lane] = 0;           // (before the first barrier: no unit wave wrote yet)
-    // lane u < nw holds unit u's store geometry and its output plane(s) of this frame, so a slot's
-    // stores need no memory access but the slot itself
-    int mv = 0, mdh = 0, mfmt = 0, mc0 = 0, mdw = 0;
-    uint64_t mb0 = 0, mb1 = 0;
-    uint32_t mp0 = 0, mp1 = 0;
-    if (lane < nw) {
-        const Unit7 *up = P.units + G.u0 + lane;
-        mv = up->variant;
-        mdh = up->dstH;
-        mfmt = up->fmt;
-        mc0 = up->col0;
-        mdw = up->dstW;
-        const int kind = up->kind, rung = up->rung;
-        const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
-        const DevPlanes *D = reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, dst)) + rung;
-        const uint64_t fo = (uint64_t)f * (uint64_t)D->fstride;
-        mb0 = (kind ? D->data[1] : D->data[0]) + fo;
-        mb1 = (kind ? D->data[2] : D->data[0]) + fo;
-        mp0 = (uint32_t)(kind ? D->pitch[1] : D->pitch[0]);
-        mp1 = (uint32_t)(kind ? D->pitch[2] : D->pitch[0]);
-    }
-    auto rl = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
-    auto drain = [&](int buf) {
-        // every unit's header at once, then every present slot's LDS read, then the stores
-        const uint32_t h = lane < nw ? shdr[buf * nu + lane] : 0u;
-        const uint64_t live = __builtin_amdgcn_ballot_w64(h != 0u);
-        if (!live) return;
-        u32x4 v[kL7MaxWaves];
-#pragma unroll
-        for (int u = 0; u < kL7MaxWaves; ++u)
-            if ((live >> u) & 1) v[u] = *reinterpret_cast<const u32x4 *>(lds7 + G.scr + 1024 * (buf * nu + u) + 16 * lane);
-        if (lane < nw) shdr[buf * nu + lane] = 0u;
-#pragma unroll
-        for (int u = 0; u < kL7MaxWaves; ++u) {
-            if (!((live >> u) & 1)) continue;
-            const UnitS7 U = {rl(mdh, u), rl(mfmt, u), rl(mc0, u), rl(mdw, u)};
-            const uint64_t ob[2] = {((uint64_t)(uint32_t)rl((int)(mb0 >> 32), u) << 32) | (uint32_t)rl((int)mb0, u),
-                                    ((uint64_t)(uint32_t)rl((int)(mb1 >> 32), u) << 32) | (uint32_t)rl((int)mb1, u)};
-            const uint32_t op[2] = {(uint32_t)rl((int)mp0, u), (uint32_t)rl((int)mp1, u)};
-            const uint32_t x[4] = {v[u][0], v[u][1], v[u][2], v[u][3]};
-            const int j = rl((int)h, u) - 1, var = rl(mv, u), ct = l6_ct(var), np = l6_np(var);
-            if (np == 1) {
-                if (ct == 4)
-                    vstore7c<4, 1>(U, j, x, ob, op, lane);
-                else if (ct == 2)
-                    vstore7c<2, 1>(U, j, x, ob, op, lane);
-                else
-                    vstore7c<1, 1>(U, j, x, ob, op, lane);
-            } else {
-                if (ct == 2)
-                    vstore7c<2, 2>(U, j, x, ob, op, lane);
-                else
-                    vstore7c<1, 2>(U, j, x, ob, op, lane);
-            }
-        }
-    };
-    const int nb = (G.ngran + PB7 - 1) / PB7;
-#pragma unroll 1
-    for (int b = 0; b < nb; ++b) {
-        group_barrier7();
-        if (b) drain((b - 1) & 1);
-    }
-    group_barrier7();                            // A
-    drain((nb - 1) & 1);
-    group_barrier7();                            // B
-    drain(nb & 1);
-}
-#endif
 
 // HS: the H taps' split in the fragments (plan6.cpp put6).  256: c = 256 hi + lo (signed
 // bytes), the epilogue FFMIN(((hi << 8) + lo) >> 7, 32767).  128: c = 128 hi + lo, lo in
@@ -745,12 +640,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
 #pragma unroll
         for (int t = 0; t < T; ++t) rh[kb][t] = rl[kb][t] = zero;
     uint8_t *fb = lds7 + U.flds;
-    // the store exchange: 1 KB per wave; with the store wave (G.stw) the exchange happens in the
-    // wave's slot of the batch's parity, where the row block then waits for the store wave
-    // (store7): slot (buf, wave) at scr + (buf nu + wave) KB, its header dword after the slots
-    const int nu = waves - G.stw;
     uint8_t *scr = lds7 + G.scr + 1024 * wave;
-    uint32_t *shdr = reinterpret_cast<uint32_t *>(lds7 + G.scr + 2048 * nu);
     const int FS = U.fs;
     int fsi = 0, fsu = 0;
     // the V fragments of the row blocks firing at granule <= upto (lead wave only)
@@ -773,8 +663,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         }
     };
     // the row blocks firing at granule qq (their window's last granule is in the ring)
-    auto vfire = [&](int qq, int buf) {
-        if (DTS_L7_SW && G.stw) scr = lds7 + G.scr + 1024 * (buf * nu + wave);
+    auto vfire = [&](int qq) {
         if (DTS_L7_ABLATE & 8) return;
         while (fg == qq) {
             v4i vh[VKB], vl[VKB];
@@ -810,15 +699,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                     xchg7<VAR>(U, w, scr, m, g, lane, px);
                 }
             }
-            if (DTS_L7_SW && G.stw) {
-                // the row block for the store wave: the exchanged row segments lane-linear in the
-                // slot (after the exchange's own reads of it: in order within the wave) and the
-                // slot's header = j + 1
-                *reinterpret_cast<u32x4 *>(scr + 16 * lane) = (u32x4){px[0], px[1], px[2], px[3]};
-                if (lane == 0) shdr[buf * nu + wave] = (uint32_t)j + 1u;
-            } else if (!(DTS_L7_ABLATE & 96)) {
-                Z.ops += vstore7<VAR>(U, j, px, ob, op, lane);
-            }
+            if (!(DTS_L7_ABLATE & 96)) Z.ops += vstore7<VAR>(U, j, px, ob, op, lane);
             ++j;
             fg = fg1;
             fg1 = firev(j + 1);
@@ -929,7 +810,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 Z.shift();
             }
             L7_STAMP(2);
-            if (DTS_L7_DEFER) vfire(q - 1, (q / PB7) & 1);
+            if (DTS_L7_DEFER) vfire(q - 1);
             L7_STAMP(4);
             if (!(DTS_L7_ABLATE & 16)) {
                 v4i ah[T], al[T];
@@ -1028,18 +909,12 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             }
 #undef WRING
             L7_STAMP(3);
-            if (!DTS_L7_DEFER) vfire(q, (q / PB7) & 1);
+            if (!DTS_L7_DEFER) vfire(q);
             L7_STAMP(4);
             if (s % PB7 == PB7 - 1) sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
-    // the row blocks of the last granule (the V deferral); with the store wave they go to the
-    // slots of parity nb & 1 (the store wave has drained those before barrier A) and barrier B
-    // hands them over (store7)
-    const int nbt = (ngran + PB7 - 1) / PB7;
-    if (DTS_L7_SW && G.stw) group_barrier7();
-    if (DTS_L7_DEFER) vfire(ngran - 1, nbt & 1);
-    if (DTS_L7_SW && G.stw) group_barrier7();
+    if (DTS_L7_DEFER) vfire(ngran - 1);
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1099,12 +974,6 @@ void k_ladder7(Ladder7Params P)
     const uint8_t *ka = (const uint8_t *)__builtin_amdgcn_kernarg_segment_ptr();
     const DevPlanes S = kld6(reinterpret_cast<const DevPlanes *>(ka + offsetof(Ladder7Params, src)));
     if (wave >= G.nwaves) {
-#if DTS_L7_SW
-        if (G.stw && wave == waves - 1) {
-            store7<SK>(P, G, f, waves);
-            return;
-        }
-#endif
         idle7<SK>(G, S, f, wave, waves);
         return;
     }
@@ -1157,13 +1026,6 @@ void ladder7_compiled(int *stages, int *batch)
 {
     *stages = NS7;
     *batch = PB7;
-}
-
-// whether this build has the store wave (the planner then plans groups for it) and its V deferral
-void ladder7_store_wave(int *store_wave, int *defer)
-{
-    *store_wave = DTS_L7_SW;
-    *defer = DTS_L7_DEFER;
 }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,

@@ -366,10 +366,8 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out,
-                 int stw)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out)
 {
-    if (stw > 0 && wmax < 2) stw = 0;
     out = Plan7{};
     // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
     // granules (the batches in flight + the one-granule V deferral; ladder7.hip)
@@ -389,7 +387,7 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
         }
     out.frag = std::move(p6.frag);
     out.fire = std::move(p6.fire);
-    const int wmax0 = stw > 0 ? wmax - 1 : wmax;          // (the store wave is the group's last wave)
+    const int wmax0 = wmax;
     for (int kind = 0; kind < 2; ++kind) {
         const int srcW = kinds[kind].srcW, np = kinds[kind].chroma ? 2 : 1;
         if (srcW % 16) return false;
@@ -574,36 +572,10 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
             std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d scr %d\n", g.kind, g.X0, g.npc, g.nwaves, g.scr);
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
-    if (stw > 0) {
-        // The store wave takes a unit's row block from its slot one batch after the unit wrote it
-        // (ladder7.hip store7): two slots per unit wave, by the parity of the batch in which the
-        // row block runs (the granule after its fire granule with the V deferral; the row blocks
-        // after the walk count as batch nb).  A unit with two row blocks in one batch (upscales)
-        // would overwrite its slot: such graphs are planned without the store wave.
-        const int defer = stw - 1;
-        bool fits = true;
-        for (const Unit7 &u : out.units) {
-            const int nb = (u.ngran + pb - 1) / pb;
-            int last = -1;
-            for (int j = 0; j < u.nrb && fits; ++j) {
-                const int q = (out.fire[(size_t)u.fire + j] & 1023) + defer;
-                const int bid = q < u.ngran ? q / pb : nb;
-                fits = bid != last;
-                last = bid;
-            }
-        }
-        if (!fits) return plan7_graph(kinds, wmax, stages, pb, by_rung, narrow, out, 0);
-        ++out.waves;
-    }
-    // the staging waves: a group's spare waves, else all of its unit waves (never the store wave)
-    const int unit_waves = out.waves - (stw > 0 ? 1 : 0);
+    // the staging waves: a group's spare waves, else all of its waves
     for (Group7 &g : out.groups) {
-        g.st0 = g.nwaves < unit_waves ? g.nwaves : 0;
-        g.stw = stw > 0 ? 1 : 0;
-        // the per-wave store exchange (1 KB per wave); with the store wave, two 1-KB slots per unit
-        // wave (the exchange happens in the slot) and their two header dwords
-        const int ex = stw > 0 ? 2 * unit_waves * 1024 + 2 * unit_waves * 4 : out.waves * 1024;
-        out.lds_bytes = std::max(out.lds_bytes, g.scr + ex);
+        g.st0 = g.nwaves < out.waves ? g.nwaves : 0;
+        out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
     }
     return out.lds_bytes <= 160 * 1024;
 }
