@@ -280,12 +280,19 @@ def gather_quality(sse, ssim, world):
     RCCL (gloo in the CPU tests).  Returns both concatenated in rank order, which is
     segment order (rank r owns segments segment_base(r) ...), on the host."""
     if world > 1:
+        sse, ssim = _coll(sse), _coll(ssim)
         gs = [torch.zeros_like(sse) for _ in range(world)]
         gq = [torch.zeros_like(ssim) for _ in range(world)]
         dist.all_gather(gs, sse.contiguous())
         dist.all_gather(gq, ssim.contiguous())
         sse, ssim = torch.cat(gs), torch.cat(gq)
     return sse.cpu(), ssim.cpu()
+
+
+def _coll(t):
+    """A collective's operand on the process group's device: as is over RCCL, on the host
+    over gloo (the CPU tests and the one-GPU rehearsal, DTS_BENCH_SHARE_DEVICE)."""
+    return t.cpu() if dist.get_backend() == "gloo" else t
 
 
 def job_quality(outs, sse, ssim, frames_per_segment):
@@ -325,6 +332,7 @@ def gather_records(frames, checksum, wall, world, dev):
     rec = torch.tensor([float(frames), float(checksum)], dtype=torch.float64, device=dev)
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
+        rec, wall_t = _coll(rec), _coll(wall_t)
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
         gathered = [torch.zeros_like(rec) for _ in range(world)]
         dist.all_gather(gathered, rec)
@@ -437,9 +445,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DTS_BENCH_SHARE_DEVICE=1: a rehearsal of the N > 1 path on a one-GPU box -- every rank on
+    # device 0 with its own libdts context, the collectives over gloo (RCCL needs one device per
+    # rank).  Its rate is not a scaling number; the driver's multi-GPU runs never set it.
+    share = os.environ.get("DTS_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)          # a real (non-null) HIP stream shared by torch events and libdts
     torch.cuda.set_stream(stream)
@@ -644,6 +661,8 @@ def main():
                          "traffic_profile": traffic_tag, "kernel_ms_per_launch": round(kern_ms, 4),
                          "frames_per_launch": B},
         }
+        if share and world > 1:
+            line["config"]["parallelism"] += " -- rehearsal: every rank on device 0, collectives over gloo"
         if jq is not None:
             line["quality"] = jq
         if wl["quality"]:

@@ -1,8 +1,10 @@
 """N > 1 path on CPU: bench.py's per-rank segment sharding and its only
 collectives (record all-gather + wall-time max-reduce), run with the gloo
 backend at world sizes 2 and 4 (the GPU box runs the same code over RCCL)."""
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import pytest
@@ -117,3 +119,34 @@ def test_gather_records_single():
     import bench
     total, wall, recs = bench.gather_records(7, 3, 0.25, 1, torch.device("cpu"))
     assert (total, wall, recs) == (7, 0.25, [(7, 3)])
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_device():
+    """bench.py's N > 1 path on hardware (no 8-GPU node has run it yet): two ranks launched by
+    torch.distributed.run exactly as the driver launches them, each with its own libdts context
+    on device 0 (DTS_BENCH_SHARE_DEVICE=1: RCCL needs one device per rank, so the collectives go
+    over gloo), cfg5 -- per-rank segments, every segment's rendition-quality records all-gathered,
+    the wall time max-reduced.  Rank 0's line must count both ranks' frames and segments and
+    verify its renditions and quality records against the oracle."""
+    steps, batch = 2, 16
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--workload", "cfg5", "--steps", str(steps), "--warmup", "1",
+           "--batch", str(batch), "--ring", str(2 * batch), "--no-cpu"]
+    env = dict(os.environ, DTS_BENCH_SHARE_DEVICE="1", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1                                   # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2
+    assert line["verified_vs_oracle"] is True
+    q = line["quality"]
+    assert q["segments"] == 2 * steps and q["frames_per_segment"] == batch
+    assert [r["rendition"] for r in q["renditions"]] == ["1920x1080", "1280x720", "854x480"]
+    for rend in q["renditions"]:
+        assert rend["frames"] == 2 * steps * batch
+        assert 0.0 < rend["ssim_all"] <= 1.0 and rend["psnr_avg"] > 20.0
+    # frames of both ranks over the slower rank's wall time
+    assert line["value"] == pytest.approx(2 * steps * batch / (line["ms_per_step"] * steps / 1e3), rel=0.02)
