@@ -580,11 +580,10 @@ bool l7_narrow()
 // The diagnostic DTS_L7_W fixes the width.
 bool plan7_sized(const Plan5In *ins, bool narrow, Plan7 &out)
 {
-    const int pairs = ladder7_pairs();
-    if (!plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), narrow, out, pairs)) return false;
+    if (!plan7_graph(ins, l7_waves(), l7_stages(), l7_pb(), l7_by_rung(), narrow, out)) return false;
     if (diag_env("DTS_L7_W") || 2 * out.lds_bytes <= 160 * 1024) return true;
     Plan7 wide;
-    if (plan7_graph(ins, 10, l7_stages(), l7_pb(), l7_by_rung(), narrow, wide, pairs) && wide.lds_bytes <= 160 * 1024)
+    if (plan7_graph(ins, 10, l7_stages(), l7_pb(), l7_by_rung(), narrow, wide) && wide.lds_bytes <= 160 * 1024)
         out = std::move(wide);
     return true;
 }

@@ -333,12 +333,6 @@ struct Unit7 {                      // one wave of a group
     int32_t rc_cap, rc_mul, rc_add; //   y = (min(y, cap) * mul + add) >> sh, as swscale.c's lum/chr
                                     //   RangeToJpeg_c / RangeFromJpeg_c (int16 store)
     int32_t vdedup;                 // as Unit6
-    int32_t pair;                   // row-block stores as whole 128-byte lines with a partner (round 6):
-                                    // 0 none (the wave stores its own 64-byte row segments at once);
-                                    // 1 / 2 the left / right unit of a line pair -- the row block
-                                    // waits in the wave's LDS slot until the next batch, then the left
-                                    // wave stores rows 0-7 and the right wave rows 8-15 of both units
-    int32_t pw;                     // the partner's wave in the group (pair != 0)
 };
 
 struct Group7 {                     // one workgroup's strip of one frame
@@ -355,9 +349,6 @@ struct Group7 {                     // one workgroup's strip of one frame
                                     // chroma: U V 16-bit pairs); bpc npc pieces per plane and granule
     int32_t st0;                    // first staging wave: waves st0.. deal the source pieces (a group's spare
                                     // waves when it has fewer units than the workgroup has waves, else all)
-    int32_t pair;                   // 1: the group has line pairs (Unit7::pair): two 1-KB exchange slots per
-                                    // wave at scr (slot of batch parity p of wave w at scr + (p waves + w)
-                                    // KB) and two more barriers after the walk
 };
 
 struct Ladder7Params {
@@ -378,7 +369,6 @@ struct Ladder7Params {
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
                           int src_kind, hipStream_t s);   // src_kind: SrcKind
 void ladder7_compiled(int *stages, int *batch);   // NS7 / PB7 of the linked k_ladder7
-int ladder7_pairs();                               // 1 + DTS_L7_DEFER if the linked k_ladder7 stores line pairs, else 0
 
 // ---------------------------------------------------------------------------
 // Quality (vf_psnr + vf_ssim) launch geometry

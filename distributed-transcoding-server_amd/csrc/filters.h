@@ -140,9 +140,6 @@ struct Plan7 {
 };
 // Groups of at most wmax units; a group's spare waves (if any) stage its pieces, else all its
 // waves deal them, and each rendition's lead wave DMAs its V fragments.
-// pairs (> 0: the kernel stores line pairs; its value - 1 is the kernel's V deferral, DTS_L7_DEFER):
-// plan Unit7::pair / Group7::pair (plan6.cpp plan7_pairs)
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out,
-                 int pairs = 0);
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out);
 
 } // namespace dts

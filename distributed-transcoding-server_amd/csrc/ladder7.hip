@@ -319,47 +319,6 @@ __device__ __forceinline__ void xchg7p(const UT &U, const uint32_t (&v)[Walk6<VA
     __builtin_amdgcn_wave_barrier();
 }
 
-// Line pairs (Unit7::pair): the row block's exchange written into the wave's slot and left there
-// -- xchg7's writes without its reads -- for the pair store of the next batch.  The slot then holds
-// the block row-major, 64 bytes per row, logical 16-byte chunk k of row m at byte
-// 64 m + 16 (k ^ ((m >> 2) & 3)) (xchg7's bank swizzle), for both pairable shapes.
-template <int VAR, class UT>
-__device__ __forceinline__ void xchg7w(const UT &U, const uint32_t (&w)[Walk6<VAR>::T], uint8_t *slot, int m, int g)
-{
-    using W = Walk6<VAR>;
-    __builtin_amdgcn_wave_barrier();
-    if constexpr (W::NP == 1 && W::CT == 4) {
-        const int d = 4 * m + (g ^ ((m >> 2) & 3));
-        uint32_t o[4];
-        transpose4(w[0], w[1], w[2], w[3], o);
-        *reinterpret_cast<u32x4 *>(slot + 16 * d) = (u32x4){o[0], o[1], o[2], o[3]};
-    } else if constexpr (W::NP == 2 && W::CT == 2) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const uint32_t u = w[c], v = w[2 + c];
-            const int ch = (2 * c + (g >> 1)) ^ ((m >> 2) & 3);
-            *reinterpret_cast<u32x2 *>(slot + 64 * m + 16 * ch + 8 * (g & 1)) =
-                (u32x2){__builtin_amdgcn_perm(v, u, 0x05010400u), __builtin_amdgcn_perm(v, u, 0x07030602u)};
-        }
-    }
-    (void)U;
-    __builtin_amdgcn_wave_barrier();
-}
-
-// The pair store of row block j from the two units' slots (sl_left, sl_right): lane (r, c) = (lane
-// >> 3, lane & 7) writes 16 bytes of row half + r at byte 16 c of the line pair's 128 bytes -- the
-// left unit's chunk c, or the right unit's chunk c - 4 -- so one store instruction covers 8 rows as
-// 8 whole lines.  The left wave stores rows 0-7, the right wave rows 8-15.
-__device__ __forceinline__ void pair_store7(const uint8_t *sl_left, const uint8_t *sl_right, int half, int j,
-                                            int dstH, uint64_t line0, uint32_t pitch, int lane)
-{
-    const int r = lane >> 3, c = lane & 7, rr = half + r;
-    const uint8_t *src = (c < 4 ? sl_left : sl_right) + 64 * rr + 16 * ((c & 3) ^ ((rr >> 2) & 3));
-    const u32x4 v = *reinterpret_cast<const u32x4 *>(src);
-    const int y = 16 * j + rr;
-    if (y < dstH) *GP6(g_u32x4, line0 + (uint64_t)y * pitch + 16u * (uint32_t)c) = v;
-}
-
 // the stores of row block j from x (xchg7); returns the store instructions issued (edge
 // units' byte stores are not counted, which only makes the next source wait longer)
 template <int VAR, class UT>
@@ -368,17 +327,6 @@ __device__ __forceinline__ int vstore7(const UT &U, int j, const uint32_t (&x)[4
 {
     using W = Walk6<VAR>;
     const int y = (DTS_L7_ABLATE & 512) ? 0 : 16 * j + (lane >> 2), q4 = lane & 3;
-    if (DTS_L7_ABLATE & 1024) {
-        // diagnostic (wrong output): the row block's 1 KB as one contiguous run of 8 whole
-        // 128-byte lines inside its own band of rows (unit u at byte 1024 u of the band), instead
-        // of 16 half lines; whole bands only (the last partial band is not stored)
-        const int u = U.col0 / (16 * W::CT);
-        if (16 * j + 16 <= U.dstH && 1024 * u + 1024 <= 16 * (int)op[0]) {
-            const uint64_t a = ob[0] + (uint64_t)(16 * j) * op[0] + (uint64_t)(1024 * u + 16 * lane);
-            *GP6(g_u32x4, a) = (u32x4){x[0], x[1], x[2], x[3]};
-        }
-        return 1;
-    }
     if (y < U.dstH) {
         if (W::CT == 1 && U.fmt == DTS_FMT_P010LE) {        // p010 renditions (xchg7p)
             if (W::NP == 1) {
@@ -540,10 +488,6 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
         sq = sq + 1 == NS7 ? 0 : sq + 1;
         L7_STAMP(2);
     }
-    if (G.pair) {                               // the unit waves' two barriers after the walk (walk7)
-        group_barrier7();
-        group_barrier7();
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     L7_STAMP_DONE(kL7Variants, G.ngran);
 }
@@ -566,7 +510,7 @@ __device__ __forceinline__ void idle7(const Group7 &G, const DevPlanes &S, int f
 // p010 sources add the ordered dither ff_dither_8x8_128[y & 7][(x + off) & 7] << 12 (off 3
 // for V) instead of the flat 64; p010 outputs (any source) are yuv2p010lX / cX:
 // av_clip_uintp2((sum + (1 << 16)) >> 17, 10) << 6.
-template <int VAR, bool RC, int HS, int SK, bool PR = false>
+template <int VAR, bool RC, int HS, int SK>
 __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, const Unit7 &U, const DevPlanes &S,
                                       int f, int wave, int waves)
 {
@@ -697,23 +641,6 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         for (int t = 0; t < T; ++t) rh[kb][t] = rl[kb][t] = zero;
     uint8_t *fb = lds7 + U.flds;
     uint8_t *scr = lds7 + G.scr + 1024 * wave;
-    // line pairs (Unit7::pair): the row block left in the slot of its batch's parity, stored with the
-    // partner's after the next barrier
-    // PR: the instantiation for paired units (k_ladder7 dispatches on Unit7::pair)
-    static_assert(!PR || (!P10 && ((W::NP == 1 && W::CT == 4) || (W::NP == 2 && W::CT == 2))), "pairable shapes");
-    constexpr bool paired = PR;
-    int pend_j = -1, pend_buf = 0;
-    auto pair_flush = [&]() {
-        if (!paired || pend_j < 0) return;
-        const int left = U.pair == 1 ? wave : U.pw, right = U.pair == 1 ? U.pw : wave;
-        const uint8_t *sl = lds7 + G.scr + 1024 * (pend_buf * waves + left);
-        const uint8_t *sr = lds7 + G.scr + 1024 * (pend_buf * waves + right);
-        const int ub = W::NP == 1 ? U.col0 : 2 * U.col0;          // this unit's first byte of the row
-        const uint64_t line0 = ob[0] + (uint64_t)(ub - (U.pair == 2 ? 64 : 0));
-        pair_store7(sl, sr, U.pair == 2 ? 8 : 0, pend_j, U.dstH, line0, op[0], lane);
-        Z.ops += 1;
-        pend_j = -1;
-    };
     const int FS = U.fs;
     int fsi = 0, fsu = 0;
     // the V fragments of the row blocks firing at granule <= upto (lead wave only)
@@ -736,7 +663,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
         }
     };
     // the row blocks firing at granule qq (their window's last granule is in the ring)
-    auto vfire = [&](int qq, int buf) {
+    auto vfire = [&](int qq) {
         if (DTS_L7_ABLATE & 8) return;
         while (fg == qq) {
             v4i vh[VKB], vl[VKB];
@@ -765,19 +692,14 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 } else {
                     vcalc7<VAR, P10>(rh, rl, vh, vl, vdit, w);
                 }
-                if (paired) {
-                    // into the slot of this batch's parity; the pair store runs after the next barrier
-                    xchg7w<VAR>(U, w, lds7 + G.scr + 1024 * (buf * waves + wave), m, g);
-                    pend_j = j;
-                    pend_buf = buf;
-                } else if (DTS_L7_ABLATE & 64) {
+                if (DTS_L7_ABLATE & 64) {
 #pragma unroll
                     for (int t = 0; t < T; ++t) asm volatile("" ::"v"(w[t]));
                 } else {
                     xchg7<VAR>(U, w, scr, m, g, lane, px);
                 }
             }
-            if (!(DTS_L7_ABLATE & 96) && !paired) Z.ops += vstore7<VAR>(U, j, px, ob, op, lane);
+            if (!(DTS_L7_ABLATE & 96)) Z.ops += vstore7<VAR>(U, j, px, ob, op, lane);
             ++j;
             fg = fg1;
             fg1 = firev(j + 1);
@@ -815,7 +737,6 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 L7_STAMP(0);
                 group_barrier7();
                 L7_STAMP(1);
-                pair_flush();                   // the previous batch's row block, with the partner's
             }
             v4i a[T][RKB];
             if (DTS_L7_ABLATE & 16) {
@@ -889,7 +810,7 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
                 Z.shift();
             }
             L7_STAMP(2);
-            if (DTS_L7_DEFER) vfire(q - 1, (q / PB7) & 1);
+            if (DTS_L7_DEFER) vfire(q - 1);
             L7_STAMP(4);
             if (!(DTS_L7_ABLATE & 16)) {
                 v4i ah[T], al[T];
@@ -988,23 +909,12 @@ __device__ __forceinline__ void walk7(const Ladder7Params &P, const Group7 &G, c
             }
 #undef WRING
             L7_STAMP(3);
-            if (!DTS_L7_DEFER) vfire(q, (q / PB7) & 1);
+            if (!DTS_L7_DEFER) vfire(q);
             L7_STAMP(4);
             if (s % PB7 == PB7 - 1) sq = sq + 1 == NS7 ? 0 : sq + 1;
         }
     }
-    // the last batch's row blocks of line pairs (barrier A), the row blocks after the walk (into
-    // parity nb & 1, which every pair store of batch nb - 2 has read), then theirs (barrier B)
-    const int nbt = (ngran + PB7 - 1) / PB7;
-    if (G.pair) {
-        group_barrier7();
-        pair_flush();
-    }
-    if (DTS_L7_DEFER) vfire(ngran - 1, nbt & 1);
-    if (G.pair) {
-        group_barrier7();
-        pair_flush();
-    }
+    if (DTS_L7_DEFER) vfire(ngran - 1);
     // the pieces and fragments past the plane were not issued; drain the rest before the
     // workgroup's LDS goes away
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1082,21 +992,11 @@ void k_ladder7(Ladder7Params P)
         }
     } else {
     switch (U.variant) {
-    case 0:
-        if (U.pair)
-            walk7<0, RC, HS, SK, true>(P, G, U, S, f, wave, waves);
-        else
-            walk7<0, RC, HS, SK>(P, G, U, S, f, wave, waves);
-        break;
+    case 0: walk7<0, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 1: walk7<1, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 2: walk7<2, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 3: walk7<3, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
-    case 4:
-        if (U.pair)
-            walk7<4, RC, HS, SK, true>(P, G, U, S, f, wave, waves);
-        else
-            walk7<4, RC, HS, SK>(P, G, U, S, f, wave, waves);
-        break;
+    case 4: walk7<4, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 5: walk7<5, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 6: walk7<6, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
     case 7: walk7<7, RC, HS, SK>(P, G, U, S, f, wave, waves); break;
@@ -1127,11 +1027,6 @@ void ladder7_compiled(int *stages, int *batch)
     *stages = NS7;
     *batch = PB7;
 }
-
-#ifndef DTS_L7_PAIRS
-#define DTS_L7_PAIRS 1      // 0: no line pairs (A/B builds)
-#endif
-int ladder7_pairs() { return DTS_L7_PAIRS ? 1 + DTS_L7_DEFER : 0; }
 
 hipError_t launch_ladder7(const Ladder7Params &p, int grid, int waves, int lds_bytes, bool range_conv, int hsplit,
                           int src_kind, hipStream_t s)

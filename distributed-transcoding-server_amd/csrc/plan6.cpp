@@ -363,62 +363,10 @@ bool plan6_graph(const Plan5In kinds[2], Plan6 &out, int align, bool sort, bool 
     return !out.units.empty();
 }
 
-// Line pairs (round 6): two units of one rendition and plane kind whose 64-byte row segments
-// make whole 128-byte lines (the left one starting a line, both full width, a luma walk of four
-// 8-bit column tiles or an nv12 chroma walk of two) store their row blocks together, one batch
-// later, from LDS slots: 8 rows x 128 bytes per store instruction instead of 16 x 64 (a diagnostic
-// build writing each row block as whole lines ran cfg2 +5 %).  A unit qualifies only if its
-// rendition runs at most one row block per staging batch (the slot holds one), and a group only if
-// its second exchange slot per wave fits `budget` (the LDS two groups per CU, or one, already
-// need: pairing never changes the groups per CU).
-static void plan7_pairs(Plan7 &out, int pb, int defer, int budget)
-{
-    if (diag_env("DTS_L7_NOPAIR")) return;
-    auto one_per_batch = [&](const Unit7 &u) {
-        const int nb = (u.ngran + pb - 1) / pb;
-        int last = -1;
-        for (int j = 0; j < u.nrb; ++j) {
-            const int q = (out.fire[(size_t)u.fire + j] & 1023) + defer;
-            const int bid = q < u.ngran ? q / pb : nb;
-            if (bid == last) return false;
-            last = bid;
-        }
-        return true;
-    };
-    auto pairable = [&](const Unit7 &u) {
-        const int ct = l6_ct(u.variant), np = l6_np(u.variant);
-        const bool luma = np == 1 && ct == 4 && !(u.variant & 16) && u.fmt != DTS_FMT_P010LE;
-        const bool nv12c = np == 2 && ct == 2 && !(u.variant & 16) && u.fmt == DTS_FMT_NV12;
-        return (luma || nv12c) && u.ncols == 16 * ct && one_per_batch(u);
-    };
-    for (Group7 &g : out.groups) {
-        g.pair = 0;
-        if (g.scr + 2 * out.waves * 1024 > budget) continue;
-        for (int i = 0; i < g.nwaves; ++i) {
-            Unit7 &a = out.units[(size_t)(g.u0 + i)];
-            const int w = 16 * l6_ct(a.variant);           // output columns per unit
-            if (a.pair || !pairable(a) || a.col0 % (2 * w)) continue;
-            for (int k = 0; k < g.nwaves; ++k) {
-                Unit7 &b = out.units[(size_t)(g.u0 + k)];
-                if (k == i || b.pair || b.rung != a.rung || b.kind != a.kind || b.variant != a.variant ||
-                    b.fmt != a.fmt || b.col0 != a.col0 + w || !pairable(b))
-                    continue;
-                a.pair = 1;
-                a.pw = k;
-                b.pair = 2;
-                b.pw = i;
-                g.pair = 1;
-                break;
-            }
-        }
-    }
-}
-
 // v7: the v6 units with 16-column-aligned K windows, grouped per plane kind by source
 // position into workgroups of at most wmax waves; each group stages the columns
 // [X0, X0 + 64 npc) of its plane(s), which hold every K window of its waves.
-bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out,
-                 int pairs)
+bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_rung, bool narrow, Plan7 &out)
 {
     out = Plan7{};
     // stages of pb granules each; the V fragment slots hold the row blocks of pb (stages + 1)
@@ -622,28 +570,13 @@ bool plan7_graph(const Plan5In kinds[2], int wmax, int stages, int pb, bool by_r
     if (diag_env("DTS_PLAN_DEBUG"))                     // diagnostic: staged columns per plane kind
         for (const Group7 &g : out.groups)
             std::fprintf(stderr, "plan7 group kind %d X0 %d npc %d waves %d scr %d\n", g.kind, g.X0, g.npc, g.nwaves, g.scr);
-    if (diag_env("DTS_PLAN_DEBUG"))
-        for (const Group7 &g : out.groups) {
-            int np = 0;
-            for (int i = 0; i < g.nwaves; ++i) {
-                const Unit7 &u = out.units[(size_t)(g.u0 + i)];
-                np += u.pair == 1;
-                std::fprintf(stderr, "  unit rung %d var %d col0 %d ncols %d fmt %d pair %d\n", u.rung, u.variant, u.col0,
-                             u.ncols, u.fmt, u.pair);
-            }
-            std::fprintf(stderr, "plan7 group kind %d line pairs %d (group pair %d)\n", g.kind, np, g.pair);
-        }
     // the widest group sets the workgroup size; every group's LDS fits that many waves
     for (const Group7 &g : out.groups) out.waves = std::max(out.waves, g.nwaves);
     // the staging waves: a group's spare waves, else all of its waves
-    int lds1 = 0;
     for (Group7 &g : out.groups) {
         g.st0 = g.nwaves < out.waves ? g.nwaves : 0;
-        lds1 = std::max(lds1, g.scr + out.waves * 1024);
+        out.lds_bytes = std::max(out.lds_bytes, g.scr + out.waves * 1024);
     }
-    if (pairs > 0) plan7_pairs(out, pb, pairs - 1, lds1 <= 80 * 1024 ? 80 * 1024 : 160 * 1024);
-    for (const Group7 &g : out.groups)
-        out.lds_bytes = std::max(out.lds_bytes, g.scr + (g.pair ? 2 : 1) * out.waves * 1024);
     return out.lds_bytes <= 160 * 1024;
 }
 

@@ -149,11 +149,10 @@ def test_plan_8bit_graphs_run_on_v5(fmt, monkeypatch):
 def test_plan_l7_group_width():
     """k_ladder7 groups are 8 waves, two per CU, unless two such groups do not fit the CU's
     160 KB of LDS; then one 10-wave group per CU (api.cpp plan7_sized: cfg4's 8K source plans
-    90 KB per 8-wave group, 108.5 KB per 10-wave group, 112 KB with the line pairs' second exchange
-    slot per wave: round 6, plan6.cpp plan7_pairs).  cfg2 / cfg3 keep two groups."""
+    90 KB per 8-wave group, 108.5 KB per 10-wave group).  cfg2 / cfg3 keep two groups."""
     cfg4 = D.graph_plan(D.make_spec(7680, 4320, D.FMT_YUV420P, [(3840, 2160, D.FMT_YUV420P, D.SCALE_LANCZOS)]))
     assert cfg4.ladder_v5 == 3 and 80 * 1024 < cfg4.lds_bytes <= 160 * 1024
-    assert cfg4.lds_bytes == 114688
+    assert cfg4.lds_bytes == 108544
     for sf in (D.FMT_YUV420P, D.FMT_P010LE):
         assert D.graph_plan(D.make_spec(3840, 2160, sf, LADDER4K if sf != D.FMT_P010LE else
                                         [(1920, 1080, D.FMT_YUV420P, D.SCALE_BICUBIC)])).lds_bytes <= 80 * 1024
