@@ -10,6 +10,8 @@
 //
 // Node 12 (this image): no `??` / `?.`.
 
+const filtergraph = require("./filtergraph");
+
 const FMT = { yuv420p: 0, nv12: 1, p010le: 2, p010: 2 };
 // libswscale SWS_* flag values (swscale.h), as include/dts.h DTS_SCALE_*
 const METHOD = { bilinear: 0x2, bicubic: 0x4, x: 0x8, point: 0x10, neighbor: 0x10, area: 0x20, gauss: 0x80,
@@ -32,14 +34,25 @@ const MAX_OUTPUTS = 4;
 // quality: `[rendition][reference]psnr` / `ssim` per segment against a reference
 // rendition of the same size -- the source scaled with `qualityRef` (default
 // lanczos) -- reported in JobChunks.result.quality.
+// Or (round 6) the ffmpeg arguments / filtergraph a CPU worker would run with -- e.g.
+//   -vf scale=1920:1080:flags=bicubic+accurate_rnd+bitexact,format=nv12 -preset fast
+// -- read by filtergraph.js into the same object (its scale size and fps, when given, must agree
+// with the row's width / height / framerate).
 function parseSettings(text) {
     if (!text) return {};
+    let o = null;
     try {
-        const o = JSON.parse(text);
-        return o && typeof o === "object" ? o : {};
+        o = JSON.parse(text);
     } catch (e) {
-        return {};                        // plain encoder options: nothing for the filtergraph
+        const g = filtergraph.graphOfArgs(text);
+        if (g === null) return {};        // plain encoder options: nothing for the filtergraph
+        const r = filtergraph.parseFiltergraph(g);
+        const st = r.settings;
+        if (r.size) st._size = r.size;
+        if (r.fps) st._fps = r.fps;
+        return st;
     }
+    return o && typeof o === "object" ? o : {};
 }
 
 function outputOf(job) {
@@ -49,6 +62,10 @@ function outputOf(job) {
     const fmt = FMT[String(s.format || "nv12").toLowerCase()];
     if (fmt === undefined) throw new Error("job " + job.id + ": unknown output format " + s.format);
     const o = { w: job.width | 0, h: job.height | 0, fmt: fmt, method: method };
+    if (s._size && (s._size[0] !== o.w || s._size[1] !== o.h))
+        throw new Error("job " + job.id + ": the graph scales to " + s._size.join("x") + ", the row asks " + o.w + "x" + o.h);
+    if (s._fps && job.framerate && Math.abs(s._fps - job.framerate) > 1e-3 * job.framerate)
+        throw new Error("job " + job.id + ": the graph's fps=" + s._fps + " is not the row's framerate " + job.framerate);
     if (Array.isArray(s.param)) o.param = s.param.slice(0, 2);
     return o;
 }

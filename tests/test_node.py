@@ -50,7 +50,9 @@ def test_worker_gpu_bitexact(tmp_path):
     jobs = [{"id": 21, "sourceID": 5, "width": 192, "height": 108, "framerate": 60},
             {"id": 22, "sourceID": 5, "width": 128, "height": 72, "framerate": 60,
              "codecSettings": json.dumps({"scale": "lanczos", "format": "yuv420p"})},
-            {"id": 23, "sourceID": 5, "width": 86, "height": 48, "framerate": 60}]
+            # the row an ffmpeg CPU worker would be given: its -vf graph read by node/filtergraph.js
+            {"id": 23, "sourceID": 5, "width": 86, "height": 48, "framerate": 60,
+             "codecSettings": "-vf scale=86:48:flags=bilinear+accurate_rnd+bitexact,format=nv12 -preset fast"}]
     chunks = []
     for j in jobs:
         for off in range(2):
@@ -66,7 +68,7 @@ def test_worker_gpu_bitexact(tmp_path):
     assert r.returncode == 0, r.stderr
     res = json.loads(r.stdout)
     outs = {21: (192, 108, D.FMT_NV12, D.SCALE_BICUBIC), 22: (128, 72, D.FMT_YUV420P, D.SCALE_LANCZOS),
-            23: (86, 48, D.FMT_NV12, D.SCALE_BICUBIC)}
+            23: (86, 48, D.FMT_NV12, D.SCALE_BILINEAR)}
     for c in res["chunks"]:
         assert c["status"] == "done" and c["assignedTo"] == 3
         rec = json.loads(c["result"])
@@ -306,6 +308,18 @@ def test_ffpipe_cpu():
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().endswith("ok")
+
+
+def test_filtergraph_cpu():
+    """node/filtergraph.js: Jobs.codecSettings written for an ffmpeg worker (`-vf scale=W:H:flags=
+    bicubic+accurate_rnd+bitexact,format=nv12`, yadif, the zscale / tonemap HDR chain, fps,
+    in_range / out_range) read into the worker's settings; sizes / rates checked against the row;
+    filters, flags and options the GPU path would not run exactly refused; JSON settings and plain
+    encoder options unchanged; a three-row ffmpeg-style ladder planned as one graph."""
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "test_filtergraph.js")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().endswith("filtergraph ok")
 
 
 def _write_y4m_p010(path, frames, w, h, fps=(60, 1)):
