@@ -647,9 +647,6 @@ __device__ __forceinline__ int4 sums4(const uint32_t (&va)[4], const uint32_t (&
     return make_int4((int)s1, (int)s2, (int)ss, (int)s12);
 }
 
-#ifndef DTS_Q_NEWEST_FIRST
-#define DTS_Q_NEWEST_FIRST 0   // 1: diagnostic launch / frame order (newest frames, chroma first)
-#endif
 #ifndef DTS_Q_PREFETCH
 #define DTS_Q_PREFETCH 1    // 0: a tile's rows loaded when the tile starts (fewer VGPRs; A/B knob)
 #endif
@@ -669,21 +666,11 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
     // gives each XCD a contiguous run of (frame, tile) items, so a strip's neighbours run beside it
     // on the same L2 and its apron column (the first block of the next strip: a 128-byte line per
     // row read for 4 bytes) is an L2 hit rather than a third line fetched per 256-byte strip row
-#if DTS_Q_NEWEST_FIRST
-    // diagnostic order: frame f on XCD f mod 8 (all its tiles there, in order), the newest frames
-    // first -- the renditions the ladder wrote last may still be in the Infinity Cache
-    const int xcd = (int)blockIdx.x & 7, k8 = (int)blockIdx.x >> 3;
-    const int fl = k8 / ngt, fr = 8 * fl + xcd;
-    if (fr >= P.nframes) return;
-    const int frame = P.nframes - 1 - fr;
-    const int gt = gt0 + k8 % ngt;
-#else
     const int nitems = P.nframes * ngt, per = (nitems + 7) >> 3;
     const int e = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
     if (e >= nitems) return;
     const int frame = e / ngt;
     const int gt = gt0 + e % ngt;
-#endif
     const int plane = gt >= P.tile_base[2] ? 2 : (gt >= P.tile_base[1] ? 1 : 0);
     const int tile = gt - P.tile_base[plane];
     const int tx = tile % P.tiles_x[plane], tw = tile / P.tiles_x[plane];
@@ -939,18 +926,9 @@ hipError_t launch_qsum(const dts_qraw *raw, int n, dts_qraw *sum, hipStream_t s)
 
 hipError_t launch_quality(const QualityParams &p, int total_tiles, hipStream_t s)
 {
-#if DTS_Q_NEWEST_FIRST
-    auto grid = [&](int ngt) { return dim3((unsigned)(8 * ngt * ((p.nframes + 7) / 8))); };
-#else
     auto grid = [&](int ngt) { return dim3((unsigned)(8 * ((ngt * p.nframes + 7) / 8))); };   // (k_quality: XCD order)
-#endif
     if (!p.interleaved) {
         hipLaunchKernelGGL(k_quality<false>, grid(total_tiles), dim3(kThreads), 0, s, p, 0, total_tiles);
-    } else if (DTS_Q_NEWEST_FIRST) {                // (diagnostic: the chroma the ladder wrote last, first)
-        const int nl = p.tile_base[1], nc = p.tile_base[2] - p.tile_base[1];
-        if (nc > 0) hipLaunchKernelGGL(k_quality<true>, grid(nc), dim3(kThreads), 0, s, p, nl, nc);
-        if (hipPeekAtLastError() == hipSuccess)
-            hipLaunchKernelGGL(k_quality<false>, grid(nl), dim3(kThreads), 0, s, p, 0, nl);
     } else {                                        // nv12: plane 1's workgroups score plane 2 as well
         const int nl = p.tile_base[1], nc = p.tile_base[2] - p.tile_base[1];
         hipLaunchKernelGGL(k_quality<false>, grid(nl), dim3(kThreads), 0, s, p, 0, nl);
