@@ -298,7 +298,7 @@ void bt2020_to_bt709(float out[9])
 
 // vf_tonemap.c init() param defaults, peak fallback (ff_determine_signal_peak for
 // linear input without side data: 10) and zscale npl
-TonemapParams tonemap_params(const dts_tonemap_spec &t)
+TonemapParams tonemap_params(const dts_tonemap_spec &t, bool full_range)
 {
     TonemapParams p{};
     p.mode = t.mode;
@@ -326,6 +326,21 @@ TonemapParams tonemap_params(const dts_tonemap_spec &t)
     p.hk0 = (float)(0.50 * (0.10 - 0.02 / 0.30) * kTmLutN / (double)p.hpeak);
     p.scale = (float)(10000.0 / npl);
     bt2020_to_bt709(p.m);
+    // zimg's 8-bit quantisation of the final zscale (r=tv: Y 219 Y' + 16, C 224 C + 128; r=pc:
+    // 255 Y', 255 C + 128), rounding half folded into the offset; computed in float exactly as
+    // hdr.hip's pixel<> spells the products out
+    const float kr7 = 0.2126f, kb7 = 0.0722f, kg7 = 1.f - kr7 - kb7;
+    const float sb = 1.f / (2.f * (1.f - kb7)), sr = 1.f / (2.f * (1.f - kr7));
+    const float qy = full_range ? 255.f : 219.f, qo = full_range ? 0.5f : 16.5f;
+    p.qy[0] = qy * kr7;
+    p.qy[1] = qy * kg7;
+    p.qy[2] = qy * kb7;
+    p.qy[3] = qo;
+    p.qcb[0] = -sb / qy;
+    p.qcb[1] = sb * qo / qy;
+    p.qcr[0] = -sr / qy;
+    p.qcr[1] = sr * qo / qy;
+    p.qc = full_range ? 255.f : 224.f;
     return p;
 }
 
@@ -474,6 +489,13 @@ struct GraphPlan {
     dts_graph_info info{};
 };
 
+// a swscale range conversion in the ladder (scale=in_range:out_range); an HDR graph's output range
+// is the tone-map kernel's quantisation instead (tonemap_params)
+bool ladder_range_conv(const dts_graph_spec &s)
+{
+    return !s.hdr_to_sdr && (s.range & 1) != ((s.range >> 4) & 1);
+}
+
 int validate_spec(const dts_graph_spec &s)
 {
     if (s.src_w < 4 || s.src_h < 4 || s.src_w > 16384 || s.src_h > 16384 || !fmt_in_ok(s.src_fmt)) return DTS_E_INVAL;
@@ -486,9 +508,10 @@ int validate_spec(const dts_graph_spec &s)
     }
     if (s.quality < 0 || s.quality > DTS_Q_BOTH) return DTS_E_INVAL;
     if ((s.range & ~0x11) != 0) return DTS_E_INVAL;              // DTS_RANGE_* in bits 0 and 4
-    // range conversion: the ladder's (k_ladder7) 15-bit converters, every source format; the HDR
-    // path's ranges are zscale's (tonemap), not a swscale conversion
-    if ((s.range & 1) != ((s.range >> 4) & 1) && s.hdr_to_sdr) return DTS_E_UNSUPPORTED;
+    // range conversion: the ladder's (k_ladder7) 15-bit converters, every source format; an HDR
+    // graph's ranges are zscale's: HDR10 sources are limited range, the output range is the final
+    // zscale r=tv / r=pc quantisation in the tone-map kernel (ladder_range_conv: no swscale step)
+    if (s.hdr_to_sdr && (s.range & 1)) return DTS_E_UNSUPPORTED;
     if (s.quality && (s.quality_out < 0 || s.quality_out >= s.nout)) return DTS_E_INVAL;
     for (int k = 0; k < s.nout; ++k) {                  // rendition quality (ABI 6)
         const dts_output_spec &o = s.out[k];
@@ -601,7 +624,7 @@ bool plan5_graph(const dts_graph_spec &s, GraphPlan &gp)
         in.nv12_chroma = kind == 1 && s.src_fmt == DTS_FMT_NV12;
         in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
         in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
-        if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
+        if (ladder_range_conv(s)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         for (int k = 0; k < s.nout; ++k) {
             const KindTables &kt = gp.kts[(size_t)k * 2 + kind];
             in.rungs.push_back(Plan5Rung{&kt.fh, &kt.v, kt.dstW, kt.dstH, s.out[k].fmt});
@@ -634,7 +657,7 @@ bool plan7_p010(const dts_graph_spec &s, GraphPlan &gp)
         in.chroma = kind == 1;
         in.nv12_chroma = kind == 1;
         in.p10 = true;
-        if ((s.range & 1) != ((s.range >> 4) & 1)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
+        if (ladder_range_conv(s)) in.range_conv = (s.range & 1) ? 2 : 1;   // from / to JPEG
         in.srcW = kind ? (s.src_w + 1) >> 1 : s.src_w;
         in.srcH = kind ? (s.src_h + 1) >> 1 : s.src_h;
         for (int k = 0; k < s.nout; ++k) {
@@ -676,7 +699,7 @@ int make_plan(const dts_graph_spec &s, GraphPlan &gp)
     const bool v5 = plan5_graph(s, gp);
     if (!v5) gp.v7 = plan7_p010(s, gp);
     // range conversion runs in k_ladder7's H epilogue only
-    if ((s.range & 1) != ((s.range >> 4) & 1) && !gp.v7) return DTS_E_UNSUPPORTED;
+    if (ladder_range_conv(s) && !gp.v7) return DTS_E_UNSUPPORTED;
     int ndmax_need = 1;
     for (int k = 0; k < s.nout; ++k)
         for (int kind = 0; kind < 2; ++kind) {
@@ -1133,7 +1156,7 @@ int dts_graph_create(dts_ctx *ctx, const dts_graph_spec *spec, dts_graph **out)
         for (int k = 0; k < s.nout; ++k) g->lay_out[k].init(s.out[k].w, s.out[k].h, s.out[k].fmt, true);
         if (s.hdr_to_sdr) {
             g->hdr = true;
-            g->tm = tonemap_params(s.tonemap);
+            g->tm = tonemap_params(s.tonemap, (s.range >> 4) & 1);
             // chunks of `batch` frames: the ladder writes a chunk's p010 intermediates, k_tonemap
             // converts them on the same stream (measured in rounds 3 and 4: smaller chunks, which keep
             // the intermediates in the Infinity Cache, and the tonemap on a second stream beside the
@@ -1443,7 +1466,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             for (int pl = 0; pl < 3; ++pl) pp.dst[k].data[pl] += (uint64_t)(f0 * pp.dst[k].fstride);
         bool aligned7 = g->v7 && planes_aligned7(pp.src);
         for (int k = 0; k < s.nout && aligned7; ++k) aligned7 = planes_aligned4(pp.dst[k]);
-        if (!aligned7 && (s.range & 1) != ((s.range >> 4) & 1)) return DTS_E_UNSUPPORTED;   // range conversion: v7 only
+        if (!aligned7 && ladder_range_conv(s)) return DTS_E_UNSUPPORTED;   // range conversion: v7 only
         if (aligned7) {
             Ladder7Params q{};
             q.src = pp.src;
@@ -1466,7 +1489,7 @@ static int enqueue_ladder(dts_graph *g, const DevPlanes &src, const DevPlanes *d
             q.fire = g->dev_fire7;
             const int64_t grid = (int64_t)8 * ((n + 7) / 8) * g->ngroups7;
             if (grid > INT32_MAX) return DTS_E_RANGE;
-            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, (s.range & 1) != ((s.range >> 4) & 1),
+            HIPCHK(ctx, launch_ladder7(q, (int)grid, g->waves7, g->lds7, ladder_range_conv(s),
                                        g->hsplit7, g->src_kind, st));
             continue;
         }

@@ -418,6 +418,9 @@ struct TonemapParams {
     float param, desat, peak, hpeak, inv_hpeak, scale;   // hpeak = hable(peak), scale = 10000 / npl
     float inv_hpeak_n;              // kTmLutN / hpeak (hable's normalisation folded into the OETF table scale)
     float hk1, hk0;                 // hable(x) / x = (A (1 - E/F) x + B (C - E/F)) / den, x kTmLutN / hpeak
+    float qy[4];                    // output range (zscale r=tv / r=pc): Y = qy0 R' + qy1 G' + qy2 B' + qy3
+    float qcb[2], qcr[2];           // Cb' = sb B' + qcb0 Y + qcb1 (Cr' likewise), Y as above
+    float qc;                       // chroma scale: 224 C + 128.5 (tv) / 255 C + 128.5 (pc)
     float m[9];                     // bt2020 -> bt709 linear primaries, row-major
     const float2 *lut;              // device [2][kTmLutN + 1] (intercept, slope) chords in table units: PQ EOTF
                                     // x 10000 / npl, BT.709 OETF

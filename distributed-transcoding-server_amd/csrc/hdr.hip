@@ -179,19 +179,24 @@ __device__ __forceinline__ void pixel(const TonemapParams &P, const float2 *tl, 
         bb = lut(oetf, b * k);
     }
 #endif
-    // Y returned as 219 Y' + 16.5 (the quantiser's scale and rounding half folded into the
-    // weights: q8y is one truncation); Cb' = (B' - Y') / (2 (1 - kb)) from that
+    // Y returned as 219 Y' + 16.5 (r=tv) or 255 Y' + 0.5 (r=pc): the quantiser's scale and
+    // rounding half folded into the weights (api.cpp tonemap_params), so q8y is one truncation;
+    // Cb' = (B' - Y') / (2 (1 - kb)) from that
     constexpr float sb = 1.f / (2.f * (1.f - kb7)), sr = 1.f / (2.f * (1.f - kr7));
-    Y = __builtin_fmaf(219.f * kb7, bb, __builtin_fmaf(219.f * kg7, gg, __builtin_fmaf(219.f * kr7, rr, 16.5f)));
-    C = make_float2(__builtin_fmaf(bb, sb, __builtin_fmaf(Y, -sb / 219.f, sb * 16.5f / 219.f)),
-                    __builtin_fmaf(rr, sr, __builtin_fmaf(Y, -sr / 219.f, sr * 16.5f / 219.f)));
+    Y = __builtin_fmaf(P.qy[2], bb, __builtin_fmaf(P.qy[1], gg, __builtin_fmaf(P.qy[0], rr, P.qy[3])));
+    C = make_float2(__builtin_fmaf(bb, sb, __builtin_fmaf(Y, P.qcb[0], P.qcb[1])),
+                    __builtin_fmaf(rr, sr, __builtin_fmaf(Y, P.qcr[0], P.qcr[1])));
 }
 
 // Y' = kr R' + kg G' + kb B' with R', G', B' in [0, 1] (the OETF table's values, or oetf709's):
-// pixel<> returns 219 Y' + 16.5, in [16.5, 235.5], so the quantiser is a truncation, no clip
+// pixel<> returns 219 Y' + 16.5 in [16.5, 235.5] or 255 Y' + 0.5 in [0.5, 255.5], so the
+// quantiser is a truncation, no clip
 __device__ __forceinline__ uint32_t q8y(float Y) { return (uint32_t)Y; }
-// Cb', Cr' in [-1/2, 1/2] for the same reason: 224 C + 128.5 in [16.5, 240.5]
-__device__ __forceinline__ int q8c(float C) { return (int)__builtin_fmaf(224.f, C, 128.5f); }
+// Cb', Cr' in [-1/2, 1/2]: 224 C + 128.5 in [16.5, 240.5]; 255 C + 128.5 reaches 256 at C = 1/2
+__device__ __forceinline__ int q8c(const TonemapParams &P, float C)
+{
+    return (int)__builtin_fminf(__builtin_fmaf(P.qc, C, 128.5f), 255.f);
+}
 
 } // namespace
 
@@ -397,7 +402,7 @@ __global__ void __launch_bounds__(256) k_tonemap(const TonemapParams P)
             sb += wy[a] * (0.25f * l.x + 0.5f * mr.x + 0.25f * mr.z);
             sr += wy[a] * (0.25f * l.y + 0.5f * mr.y + 0.25f * mr.w);
         }
-        const int u = q8c(sb), v = q8c(sr);
+        const int u = q8c(P, sb), v = q8c(P, sr);
         if (P.dst_fmt == DTS_FMT_NV12) {
             gst<uint16_t>(P.dst.data[1] + df + (uint64_t)by * P.dst.pitch[1] + 2 * bx, (uint16_t)(u | (v << 8)));
         } else {
@@ -530,7 +535,7 @@ __global__ void __launch_bounds__(64 * kTwWaves) k_tonemap_w(const TonemapParams
             sb += wy[k] * h[k].x;
             sr += wy[k] * h[k].y;
         }
-        const int u = q8c(sb), v = q8c(sr);
+        const int u = q8c(P, sb), v = q8c(P, sr);
         if (!out_col) return;
         if (nv12) {
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(u | (v << 8)), wU, 2 * cx, by * dp1, 0);

@@ -12,7 +12,11 @@
 //                             nv12, p010le; gbrpf32le / gbrp inside the HDR chain)
 //   yadif     mode:parity:deint (vf_yadif.c; the frame-rate modes 0 / 2 -- one output per frame)
 //   zscale    t / transfer, npl, p / primaries, m / matrix, r / range (vf_zscale.c: the HDR10 ->
-//                             SDR chain's linearise and bt709 steps; npl is the one that matters)
+//                             SDR chain's linearise and bt709 steps; npl, and r of a zscale after
+//                             the tonemap -- the SDR output's range, tv or pc -- are the ones that
+//                             matter)
+// In an HDR graph the GPU scales the p010 source before the tone map (dts.h hdr_to_sdr), so a
+// scale must come ahead of the zscale / tonemap chain and carry no range conversion.
 //   tonemap   tonemap:param:desat:peak (vf_tonemap.c)
 //   fps       fps            (vf_fps.c: checked against the Jobs row's framerate)
 // Anything else is an error: the worker refuses a graph it would not run exactly.
@@ -94,7 +98,7 @@ function checkKeys(f, allowed) {
 // against the Jobs row.
 function parseFiltergraph(graph) {
     const s = {};
-    let size = null, fps = null, linear = false, npl = null;
+    let size = null, fps = null, linear = false, npl = null, scaleRange = false, tmOutRange = null;
     const filters = String(graph).split(",").map(function (t) { return t.trim(); }).filter(function (t) { return t; });
     if (!filters.length) fail("empty graph");
     filters.forEach(function (text) {
@@ -104,6 +108,8 @@ function parseFiltergraph(graph) {
         case "scale": {
             checkKeys(f, ["w", "h", "flags", "in_range", "out_range", "param0", "param1"]);
             if (s.scale) fail("one scale per graph");
+            if (linear || s.tonemap) fail("scale after zscale / tonemap (the GPU graph scales the p010 source first)");
+            scaleRange = o.in_range !== undefined || o.out_range !== undefined;
             let method = null;
             String(o.flags || "bicubic").split("+").forEach(function (t) {
                 t = t.trim();
@@ -158,6 +164,10 @@ function parseFiltergraph(graph) {
             checkKeys(f, ["t", "npl", "p", "m", "r", "w", "h"]);
             if (o.t === "linear") linear = true;
             if (o.npl !== undefined) npl = num(o.npl, "zscale npl");
+            if (o.r !== undefined && s.tonemap) {        // the SDR output's quantisation
+                if (!RANGES[o.r]) fail("zscale: r=" + o.r);
+                tmOutRange = RANGES[o.r];
+            }
             break;
         }
         case "tonemap": {
@@ -179,6 +189,8 @@ function parseFiltergraph(graph) {
     if (s.tonemap) {
         if (!linear) fail("tonemap needs the linear light of zscale=t=linear ahead of it");
         if (npl !== null) s.tonemap.npl = npl;
+        if (scaleRange) fail("scale: in_range / out_range on the HDR source (the output range is zscale's r=)");
+        if (tmOutRange === "pc") s.outRange = "pc";
     }
     return { settings: s, size: size, fps: fps };
 }

@@ -140,8 +140,9 @@ typedef struct dts_graph_spec {
      * limited range; every output (8-bit yuv420p/nv12, even w/h) is scaled
      * bit-exactly to a p010 intermediate and then converted as by
      *   zscale=t=linear:npl=NPL,format=gbrpf32le,zscale=p=bt709,
-     *   tonemap=MODE:param=P:desat=D:peak=K,zscale=t=bt709:m=bt709:r=tv
-     * (float path, +-1 LSB vs the double restatement). */
+     *   tonemap=MODE:param=P:desat=D:peak=K,zscale=t=bt709:m=bt709:r=R
+     * (float path, +-1 LSB vs the double restatement); R = tv, or pc when
+     * `range` names a JPEG output range (the source range must be MPEG). */
     int32_t hdr_to_sdr;                 /* 0 = off */
     dts_tonemap_spec tonemap;
     /* Deinterlace ahead of the ladder (`-vf yadif=MODE:PARITY,scale=...`, vf_yadif.c):
@@ -158,8 +159,9 @@ typedef struct dts_graph_spec {
      * dstRange): source range | output range << 4, each DTS_RANGE_*.  Different
      * ranges run swscale.c's lum/chrRangeToJpeg / FromJpeg on the 15-bit
      * horizontal output (every rendition takes the output range).  Supported for
-     * 8-bit planar sources on the v7 ladder (plane widths multiples of 16, no HDR);
-     * else dts_graph_create returns DTS_E_UNSUPPORTED. */
+     * 8-bit planar sources on the v7 ladder (plane widths multiples of 16); else
+     * dts_graph_create returns DTS_E_UNSUPPORTED.  HDR graphs: no swscale step, the
+     * output range is the final zscale's r= (above). */
     int32_t range;
 } dts_graph_spec;
 

@@ -99,11 +99,11 @@ int orc_fps_map(int64_t nb_in, int in_num, int in_den, int out_num, int out_den,
 /* HDR10 (p010, PQ, bt2020nc, limited) -> SDR bt709 8-bit 4:2:0 at the same
  * size (vf_tonemap_ref.c): zscale linearise + primaries + vf_tonemap MODE
  * (0 none, 1 linear, 2 gamma, 3 clip, 4 reinhard, 5 hable, 6 mobius) + zscale
- * bt709 out.  param NaN = vf_tonemap default; peak <= 0 -> 10; npl <= 0 ->
- * 100.  w and h even.  Returns 0 or <0. */
+ * bt709 out (out_full: r=pc, else r=tv).  param NaN = vf_tonemap default;
+ * peak <= 0 -> 10; npl <= 0 -> 100.  w and h even.  Returns 0 or <0. */
 int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_t src_pitch[3],
                          int dstFmt, uint8_t *const dst[3], const int64_t dst_pitch[3],
-                         int mode, double param, double desat, double peak, double npl);
+                         int mode, double param, double desat, double peak, double npl, int out_full);
 double orc_tonemap_param(int mode, double param);
 
 /* vf_yadif (vf_yadif_ref.c) on one 8-bit yuv420p frame: prev/cur/next planes

@@ -47,7 +47,7 @@ def lib():
         L.orc_fps_map.argtypes = [i64, i32, i32, i32, i32, vp, i32]
         d = ctypes.c_double
         L.orc_hdr_to_sdr_frame.argtypes = [i32, i32, ctypes.POINTER(vp), ctypes.POINTER(i64), i32,
-                                           ctypes.POINTER(vp), ctypes.POINTER(i64), i32, d, d, d, d]
+                                           ctypes.POINTER(vp), ctypes.POINTER(i64), i32, d, d, d, d, i32]
         L.orc_tonemap_param.argtypes = [i32, d]
         L.orc_tonemap_param.restype = d
         L.orc_bt2020_to_bt709.argtypes = [ctypes.POINTER(d * 3)]
@@ -136,12 +136,13 @@ def fps_map(nb_in, in_rate, out_rate, cap=1 << 20):
 TM_MODES = {"none": 0, "linear": 1, "gamma": 2, "clip": 3, "reinhard": 4, "hable": 5, "mobius": 6}
 
 
-def hdr_to_sdr(src_planes, w, h, dst_fmt, mode=5, param=float("nan"), desat=2.0, peak=0.0, npl=0.0):
-    """HDR10 p010 -> SDR bt709 8-bit (zscale + vf_tonemap restated, double precision)."""
+def hdr_to_sdr(src_planes, w, h, dst_fmt, mode=5, param=float("nan"), desat=2.0, peak=0.0, npl=0.0, full=False):
+    """HDR10 p010 -> SDR bt709 8-bit (zscale + vf_tonemap restated, double precision);
+    full: the last zscale's r=pc (else r=tv)."""
     dst = _alloc(w, h, dst_fmt)
     sd, sp = _ptrs(src_planes)
     dd, dp = _ptrs(dst)
-    r = lib().orc_hdr_to_sdr_frame(w, h, sd, sp, dst_fmt, dd, dp, mode, param, desat, peak, npl)
+    r = lib().orc_hdr_to_sdr_frame(w, h, sd, sp, dst_fmt, dd, dp, mode, param, desat, peak, npl, 1 if full else 0)
     if r != 0:
         raise RuntimeError(f"orc_hdr_to_sdr_frame failed ({r})")
     return dst

@@ -178,11 +178,14 @@ static double chroma_up(const uint8_t *plane, int64_t pitch, int cw, int ch, int
 
 int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_t src_pitch[3],
                          int dstFmt, uint8_t *const dst[3], const int64_t dst_pitch[3],
-                         int mode, double param, double desat, double peak, double npl)
+                         int mode, double param, double desat, double peak, double npl, int out_full)
 {
     const double kr2 = 0.2627, kb2 = 0.0593, kg2 = 1.0 - kr2 - kb2;
     const double kr7 = 0.2126, kb7 = 0.0722, kg7 = 1.0 - kr7 - kb7;
     static const double wx[3] = {0.25, 0.5, 0.25}, wy[4] = {0.125, 0.375, 0.375, 0.125};
+    /* zimg's integer quantisation of the last zscale (depth conversion, no dither): r=tv Y 219 Y' + 16,
+     * C 224 C + 128; r=pc Y 255 Y', C 255 C + 128 */
+    const double qy = out_full ? 255.0 : 219.0, qo = out_full ? 0.0 : 16.0, qc = out_full ? 255.0 : 224.0;
     double M[3][3], scale, hpeak, *cb4, *cr4;
     int x, y, bx, by;
     const int cw = w / 2, ch = h / 2;
@@ -245,7 +248,7 @@ int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_
             Y = kr7 * r + kg7 * g + kb7 * b;
             cb4[(size_t)y * w + x] = (b - Y) / (2.0 * (1.0 - kb7));
             cr4[(size_t)y * w + x] = (r - Y) / (2.0 * (1.0 - kr7));
-            dst[0][(int64_t)y * dst_pitch[0] + x] = (uint8_t)q8(16.0 + 219.0 * Y);
+            dst[0][(int64_t)y * dst_pitch[0] + x] = (uint8_t)q8(qo + qy * Y);
         }
     /* 4:4:4 -> 4:2:0, chroma location left: taps 1/4 1/2 1/4 around column 2 bx,
      * 1/8 3/8 3/8 1/8 over rows 2 by - 1 .. 2 by + 2, edge samples repeated */
@@ -262,11 +265,11 @@ int orc_hdr_to_sdr_frame(int w, int h, const uint8_t *const src[3], const int64_
                 }
             }
             if (dstFmt == ORC_FMT_NV12) {
-                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx] = (uint8_t)q8(128.0 + 224.0 * sb);
-                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx + 1] = (uint8_t)q8(128.0 + 224.0 * sr);
+                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx] = (uint8_t)q8(128.0 + qc * sb);
+                dst[1][(int64_t)by * dst_pitch[1] + 2 * bx + 1] = (uint8_t)q8(128.0 + qc * sr);
             } else {
-                dst[1][(int64_t)by * dst_pitch[1] + bx] = (uint8_t)q8(128.0 + 224.0 * sb);
-                dst[2][(int64_t)by * dst_pitch[2] + bx] = (uint8_t)q8(128.0 + 224.0 * sr);
+                dst[1][(int64_t)by * dst_pitch[1] + bx] = (uint8_t)q8(128.0 + qc * sb);
+                dst[2][(int64_t)by * dst_pitch[2] + bx] = (uint8_t)q8(128.0 + qc * sr);
             }
         }
     free(cb4);

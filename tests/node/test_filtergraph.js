@@ -32,13 +32,21 @@ assert.deepStrictEqual(ladder.deintOf({ id: 3, codecSettings: "-vf yadif=0:-1:0,
 assert.deepStrictEqual(ladder.deintOf({ id: 4, codecSettings: "-vf yadif=mode=send_frame_nospatial:parity=bff,scale=1280:720" }),
                        { mode: 2, tff: 0 });
 assert.throws(function () { ladder.deintOf({ id: 5, codecSettings: "-vf yadif=1,scale=1280:720" }); }, /yadif mode 1/);
-// the HDR10 -> SDR chain
-const hdr = "-vf zscale=t=linear:npl=100,format=gbrpf32le,zscale=p=bt709,tonemap=tonemap=hable:desat=0," +
-            "zscale=t=bt709:m=bt709:r=tv,format=yuv420p,scale=1920:1080:flags=bicubic";
+// the HDR10 -> SDR chain (the p010 source scaled first, SURVEY.md §3: vf_scale -> zscale + tonemap)
+const chain = "zscale=t=linear:npl=100,format=gbrpf32le,zscale=p=bt709,tonemap=tonemap=hable:desat=0," +
+              "zscale=t=bt709:m=bt709:r=tv,format=yuv420p";
+const hdr = "-vf scale=1920:1080:flags=bicubic," + chain;
 s = settings(hdr);
 assert.strictEqual(s.format, "yuv420p");
+assert.strictEqual(s.outRange, undefined);
 assert.deepStrictEqual(ladder.tonemapOf({ id: 6, codecSettings: hdr }), { mode: 5, desat: 0, npl: 100 });
 assert.throws(function () { fg.parseFiltergraph("tonemap=hable"); }, /linear light/);
+// the final zscale's r=pc: a full-range SDR output (dts_graph_spec.range, JPEG output)
+const hdrPc = hdr.replace("r=tv", "r=pc");
+assert.deepStrictEqual(ladder.rangeOf({ id: 6, codecSettings: hdrPc }), { src: 0, dst: 1 });
+// the GPU graph does not scale the SDR result, nor range-convert the HDR source
+assert.throws(function () { fg.parseFiltergraph(chain + ",scale=1920:1080"); }, /scale after zscale/);
+assert.throws(function () { fg.parseFiltergraph("scale=1920:1080:out_range=pc," + chain); }, /in_range \/ out_range/);
 // fps agrees with the row
 s = settings("-vf fps=30000/1001,scale=1280:720");
 assert.ok(Math.abs(s._fps - 29.97002997) < 1e-6);

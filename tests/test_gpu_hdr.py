@@ -101,14 +101,14 @@ def _check_tol(got, want, what):
     assert bad <= MAX_OFF_BY_ONE * n, f"{what}: {bad}/{n} samples off by one"
 
 
-def _hdr_case(ctx, sw, sh, outs, frames, tm):
-    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_P010LE, outs, tonemap=tm))
+def _hdr_case(ctx, sw, sh, outs, frames, tm, full=False):
+    g = D.Graph(ctx, D.make_spec(sw, sh, D.FMT_P010LE, outs, tonemap=tm, dst_range=int(full)))
     got, _ = g.run_host(frames)
     for f, src in enumerate(frames):
         for k, (w, h, fmt, m) in enumerate(outs):
             mid = orc.scale_frame(src, sw, sh, D.FMT_P010LE, w, h, D.FMT_P010LE, m)
             want = orc.hdr_to_sdr(mid, w, h, fmt, tm.get("mode", D.TM_HABLE), tm.get("param", float("nan")),
-                                  tm.get("desat", 2.0), tm.get("peak", 0.0), tm.get("npl", 100.0))
+                                  tm.get("desat", 2.0), tm.get("peak", 0.0), tm.get("npl", 100.0), full)
             _check_tol(got[f][k], want, f"frame {f} out {k} tm {tm}")
     g.close()
 
@@ -129,6 +129,17 @@ def test_hdr_to_sdr_params(ctx, tm):
     frames = [D.synth_host(258, 146, D.FMT_P010LE, 0, 11, 2),
               random_frame(258, 146, D.FMT_P010LE, np.random.default_rng(3))]
     _hdr_case(ctx, 258, 146, [(130, 74, D.FMT_YUV420P, LAN)], frames, tm)
+
+
+@pytest.mark.parametrize("mode", ["hable", "clip", "mobius"])
+def test_hdr_to_sdr_full_range(ctx, mode):
+    """The last zscale with r=pc (dst_range JPEG): the tone-map kernels' full-range quantiser
+    (255 Y', 255 C + 128, chroma clamped at 255) vs the restatement, both column walks'
+    edge handling included (130 x 74 is not a multiple of the walk's tiles)."""
+    frames = [D.synth_host(384, 216, D.FMT_P010LE, 0, 0x5EED, 1),
+              random_frame(384, 216, D.FMT_P010LE, np.random.default_rng(21))]
+    _hdr_case(ctx, 384, 216, [(192, 108, D.FMT_YUV420P, BIC), (130, 74, D.FMT_NV12, BIL)], frames,
+              {"mode": D.TM_MODES[mode], "peak": 100.0 if mode != "hable" else 0.0}, full=True)
 
 
 def test_hdr_4k_to_1080p_one_frame(ctx):

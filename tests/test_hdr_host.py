@@ -54,6 +54,29 @@ def test_clip_100_nits_is_white():
     assert int(out[0][0, 0]) in (234, 235)
 
 
+def test_full_range_output():
+    """zscale r=pc (zimg full-range 8-bit: 255 Y', 255 C + 128): black is 0, clip's 100-nit
+    white 254 / 255, neutral chroma 128, and every sample the r=tv one re-quantised to
+    within 1."""
+    for mode in (D.TM_HABLE, D.TM_CLIP):
+        out = orc.hdr_to_sdr(_p010(8, 4, 64, 512, 512), 8, 4, D.FMT_YUV420P, mode, full=True)
+        assert (out[0] == 0).all() and (out[1] == 128).all() and (out[2] == 128).all()
+    y10 = round(64 + 876 * 0.5081)
+    out = orc.hdr_to_sdr(_p010(2, 2, y10, 512, 512), 2, 2, D.FMT_YUV420P, D.TM_CLIP, full=True)
+    assert int(out[0][0, 0]) in (254, 255)
+    rng = np.random.default_rng(4)
+    src = D.alloc_frame(64, 36, D.FMT_P010LE)
+    for p in src[:2]:
+        p.view(np.uint16)[...] = (rng.integers(64, 941, p.view(np.uint16).shape) << 6).astype(np.uint16)
+    tv = orc.hdr_to_sdr(src, 64, 36, D.FMT_NV12, D.TM_CLIP)
+    pc = orc.hdr_to_sdr(src, 64, 36, D.FMT_NV12, D.TM_CLIP, full=True)
+    ty, py = tv[0].astype(np.float64), pc[0].astype(np.float64)
+    assert np.abs((ty - 16) * 255 / 219 - py).max() <= 1.5
+    tc, pcc = tv[1].astype(np.float64), pc[1].astype(np.float64)
+    assert np.abs(np.clip((tc - 128) * 255 / 224 + 128, 0, 255) - pcc).max() <= 1.5
+    assert py.max() > 235                           # the wider code range is used
+
+
 def test_param_defaults():
     nan = float("nan")
     assert orc.lib().orc_tonemap_param(D.TM_GAMMA, nan) == pytest.approx(1.8)

@@ -195,8 +195,9 @@ def test_plan_v7_groups(monkeypatch):
 
 def test_plan_range_conversion(monkeypatch):
     """Range conversion (dts_graph_spec.range) plans onto k_ladder7 only: 8-bit planar
-    and nv12 sources with plane widths multiples of 16; p010 sources, HDR graphs, other
-    widths and DTS_LADDER=6 are refused with DTS_E_UNSUPPORTED, bad bits with INVAL."""
+    and nv12 sources with plane widths multiples of 16; p010 sources, other widths and
+    DTS_LADDER=6 are refused with DTS_E_UNSUPPORTED, bad bits with INVAL.  HDR graphs take
+    a JPEG output range (the tone map's r=pc) and refuse a JPEG source range."""
     monkeypatch.delenv("DTS_LADDER", raising=False)
     outs = [(1920, 1080, D.FMT_NV12, D.SCALE_BICUBIC), (1280, 720, D.FMT_YUV420P, D.SCALE_BICUBIC)]
     for sr, dr in [(0, 1), (1, 0), (1, 1)]:
@@ -211,6 +212,16 @@ def test_plan_range_conversion(monkeypatch):
     s.range = 2
     with pytest.raises(D.DtsError):
         D.graph_plan(s)
+    # HDR graphs: the output range is the tone map's zscale r=pc, no ladder conversion; HDR10
+    # sources are limited range
+    tv, pc = (D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, outs, dst_range=dr, tonemap={"mode": D.TM_HABLE}))
+              for dr in (0, 1))
+    assert (pc.ladder_v5, pc.ladder_v4_mask, pc.njobs, pc.lds_bytes) == (tv.ladder_v5, tv.ladder_v4_mask, tv.njobs,
+                                                                      tv.lds_bytes)
+    for sr, dr in [(1, 0), (1, 1)]:
+        with pytest.raises(D.DtsError):
+            D.graph_plan(D.make_spec(3840, 2160, D.FMT_P010LE, outs, src_range=sr, dst_range=dr,
+                                     tonemap={"mode": D.TM_HABLE}))
     monkeypatch.setenv("DTS_LADDER", "6")
     with pytest.raises(D.DtsError):
         D.graph_plan(D.make_spec(3840, 2160, D.FMT_YUV420P, outs, src_range=1))
