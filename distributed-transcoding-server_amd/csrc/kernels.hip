@@ -647,6 +647,16 @@ __device__ __forceinline__ int4 sums4(const uint32_t (&va)[4], const uint32_t (&
     return make_int4((int)s1, (int)s2, (int)ss, (int)s12);
 }
 
+#ifndef DTS_BOUNDS_CHECK
+// 1 (diagnostic builds, tools/build_qvar.sh): every k_quality global access is checked against the
+// scored plane's rows and row bytes; an access outside is skipped and poisons the tile's partials
+// (SSE all ones, SSIM NaN), so a parity test fails on it instead of the GPU faulting
+#define DTS_BOUNDS_CHECK 0
+#endif
+#ifndef DTS_BCHK_SHRINK
+#define DTS_BCHK_SHRINK 0   // > 0: the check's row bytes shrunk (a negative control: the tests must fail)
+#endif
+
 #ifndef DTS_Q_PREFETCH
 #define DTS_Q_PREFETCH 1    // 0: a tile's rows loaded when the tile starts (fewer VGPRs; A/B knob)
 #endif
@@ -692,12 +702,21 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
 
     unsigned long long sse[2] = {0, 0};
     double ssim[2] = {0.0, 0.0};
+    bool oob = false;                               // DTS_BOUNDS_CHECK: an access outside the plane
+    const int rowb = (inter ? 2 * w : w) - DTS_BCHK_SHRINK;   // bytes of a scored row
+    auto outside = [&](int y, int xb, int nb) {
+        if (!DTS_BOUNDS_CHECK) return false;
+        const bool o = y < 0 || y >= h || xb < 0 || xb + nb > rowb;
+        oob |= o;
+        return o;
+    };
     // one block by 4-byte loads (edges, the apron column, unaligned planes); zero outside
     auto block = [&](int gx, int gy, int comp) {
         if (gx >= W4 || gy >= H4 || gx < 0) return make_int4(0, 0, 0, 0);
         uint32_t va[4], vb[4];
 #pragma unroll
         for (int yy = 0; yy < 4; ++yy) {
+            if (outside(4 * gy + yy, (inter ? 2 : 1) * 4 * gx, inter ? 8 : 4)) return make_int4(0, 0, 0, 0);
             va[yy] = load4(A + (int64_t)(4 * gy + yy) * pa, 4 * gx, inter, comp);
             vb[yy] = load4(B + (int64_t)(4 * gy + yy) * pb, 4 * gx, inter, comp);
         }
@@ -710,6 +729,7 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
         if (vec16 && gy < H4 && gx + NB <= W4) {
 #pragma unroll
             for (int yy = 0; yy < 4; ++yy) {
+                if (outside(4 * gy + yy, 4 * (inter ? 2 : 1) * gx, 16)) continue;
                 ra[yy] = *reinterpret_cast<const uint4 *>(A + (int64_t)(4 * gy + yy) * pa + 4 * (inter ? 2 : 1) * gx);
                 rb[yy] = *reinterpret_cast<const uint4 *>(B + (int64_t)(4 * gy + yy) * pb + 4 * (inter ? 2 : 1) * gx);
             }
@@ -759,6 +779,7 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
             const int y = py0 + i / aw, x = ax0 + i % aw;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
+                if (outside(y, inter ? 2 * x + c + (plane == 2) : x, 1)) continue;
                 const int d = load1(A + (int64_t)y * pa, x, inter, c + (plane == 2)) -
                               load1(B + (int64_t)y * pb, x, inter, c + (plane == 2));
                 sse[c] += (unsigned long long)(d * d);
@@ -770,6 +791,7 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
             const int y = by0p + i / bw, x = px0 + i % bw;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
+                if (outside(y, inter ? 2 * x + c + (plane == 2) : x, 1)) continue;
                 const int d = load1(A + (int64_t)y * pa, x, inter, c + (plane == 2)) -
                               load1(B + (int64_t)y * pb, x, inter, c + (plane == 2));
                 sse[c] += (unsigned long long)(d * d);
@@ -837,7 +859,8 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
             red_e[c][t >> 6] = sse[c];
         }
     }
-    __syncthreads();
+    const bool poison = DTS_BOUNDS_CHECK && __syncthreads_or(oob);
+    if (!DTS_BOUNDS_CHECK) __syncthreads();
     if (t < NC) {
         double s = 0;
         unsigned long long e = 0;
@@ -846,8 +869,9 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
             e += red_e[t][i];
         }
         const int g = gt + t * (P.tile_base[2] - P.tile_base[1]);      // V: the same tile of plane 2
-        P.partial_ssim[(int64_t)frame * total + g] = s;
-        P.partial_sse[(int64_t)frame * total + g] = e;
+        if (DTS_BOUNDS_CHECK && (g < 0 || g >= total || frame >= P.nframes)) return;
+        P.partial_ssim[(int64_t)frame * total + g] = poison ? __builtin_nan("") : s;
+        P.partial_sse[(int64_t)frame * total + g] = poison ? ~0ull : e;
     }
 }
 
