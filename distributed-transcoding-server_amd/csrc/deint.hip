@@ -351,7 +351,7 @@ static_assert(kYtNP == 8 || kYtNP == 16, "8 or 16 pixels per thread");
 #endif
 constexpr int kYtWalk = DTS_YADIF_WALK;         // input frames per workgroup
 #ifndef DTS_YT_SB
-#define DTS_YT_SB 1                             // pixels of the spatial search between scheduling barriers
+#define DTS_YT_SB 1                             // pixels (yspatial_pk: pixel pairs) of the spatial search between scheduling barriers
 #endif
 #ifndef DTS_YT_ABLATE
 #define DTS_YT_ABLATE 0                         // diagnostic bits (wrong output): 1 no arithmetic
@@ -455,6 +455,88 @@ __device__ __forceinline__ void yspatial(const uint32_t (&cm)[(2 * kYtCB + NP) /
         const uint32_t pv = (uint32_t)ps >> 1;
         pr[k >> 1] = (k & 1) ? pr[k >> 1] | (pv << 16) : pv;
         if ((k + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ne != (1u << NP) - 1) {                           // filter_edges: no spatial search
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (!((ne >> k) & 1u)) {
+                const uint32_t pv = (uint32_t)(byte_at(cm, CB + k) + byte_at(cp, CB + k)) >> 1;
+                pr[k >> 1] = (k & 1) ? (pr[k >> 1] & 0xffffu) | (pv << 16) : (pr[k >> 1] & 0xffff0000u) | pv;
+            }
+    }
+}
+
+#ifndef DTS_YT_PK
+#define DTS_YT_PK 1     // the spatial search two pixels per dword (yspatial_pk); 0: per pixel (yspatial)
+#endif
+
+// The spatial search of NP pixels as 16-bit pairs (round 6): pixels 2p and 2p + 1 share every
+// instruction after the sums of absolute differences.  v_sad_u8 makes pixel 2p's score and
+// v_sad_hi_u8 adds pixel 2p + 1's in the high half, so the five scores of a pair arrive packed;
+// the candidate predictions cm[X + j] + cp[X - j] are sums of byte pairs unpacked by v_perm
+// (bytes i, i + 1 of a row as two 16-bit lanes: one unpacking serves the five j of neighbouring
+// pairs); each CHECK(j) of filter_line_c is a packed subtract whose sign (>> 15) is the lane mask
+// of `score < spatial_score`, nested checks AND their masks, and the updates are bit selects.
+// Scores stay in [-1, 765], their differences in 16 bits.  The result is the same bytes as
+// yspatial's, which it replaces.
+template <int NP>
+__device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP) / 4], const uint32_t (&cp)[(2 * kYtCB + NP) / 4],
+                                            uint32_t ne, uint32_t (&pr)[NP / 2])
+{
+    constexpr int CB = kYtCB;                          // pixel k of cm / cp at byte CB + k
+    uint32_t wm[NP + 4], wp[NP + 4];                   // 3-byte windows starting at byte CB - 3 + i
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        wm[i] = win3(cm, CB - 3 + i);
+        wp[i] = win3(cp, CB - 3 + i);
+        asm volatile("" : "+v"(wm[i]), "+v"(wp[i]));
+    }
+    // bytes i, i + 1 of a row, zero-extended into two 16-bit lanes
+    auto u2 = [](const uint32_t *a, int i) {
+        const uint32_t b = (uint32_t)(i & 3);
+        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
+    };
+    // the lane masks pass through an empty asm: seen as sign splats, the compiler turns the bit
+    // selects back into a compare and a select per 16-bit lane
+    auto lt = [](i16x2y a, i16x2y b) {                // a < b per lane: 0xffff / 0
+        uint32_t m = __builtin_bit_cast(uint32_t, (i16x2y)((a - b) >> 15));
+        asm volatile("" : "+v"(m));
+        return m;
+    };
+    auto sel = [](uint32_t m, i16x2y a, i16x2y b) {  // v_bfi_b32
+        return __builtin_bit_cast(i16x2y, (__builtin_bit_cast(uint32_t, a) & m) | (__builtin_bit_cast(uint32_t, b) & ~m));
+    };
+#pragma unroll
+    for (int q = 0; q < NP / 2; ++q) {
+        const int k = 2 * q, X = CB + k;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {                  // the windows pixels k, k + 1 reach first
+            wm[k + 4 + i] = win3(cm, X + 1 + i);
+            wp[k + 4 + i] = win3(cp, X + 1 + i);
+            asm volatile("" : "+v"(wm[k + 4 + i]), "+v"(wp[k + 4 + i]));
+        }
+        // pixel k + h: windows k + h .. k + h + 4 are X + h - 3 .. X + h + 1; CHECK(j) compares the cm
+        // window at X + j - 1 with the cp window at X - j - 1
+        auto sc = [&](int jm, int jp) {               // (pixel k, pixel k + 1) scores of one check
+            const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], 0u);
+            return __builtin_bit_cast(i16x2y, __builtin_amdgcn_sad_hi_u8(wm[k + 1 + jm], wp[k + 1 + jp], lo));
+        };
+        i16x2y score = sc(2, 2) - (i16x2y){1, 1};
+        const i16x2y sm1 = sc(1, 3), sm2 = sc(0, 4), s1 = sc(3, 1), s2 = sc(4, 0);
+        i16x2y ps = u2(cm, X) + u2(cp, X);
+        uint32_t m = lt(sm1, score);                                       // CHECK(-1)
+        score = sel(m, sm1, score);
+        ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
+        uint32_t mm = lt(sm2, score) & m;                                  // CHECK(-2) inside it
+        score = sel(mm, sm2, score);
+        ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
+        m = lt(s1, score);                                                 // CHECK(1)
+        score = sel(m, s1, score);
+        ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
+        mm = lt(s2, score) & m;                                            // CHECK(2) inside it
+        ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
+        pr[q] = __builtin_bit_cast(uint32_t, ps) >> 1 & 0x7fff7fffu;       // both halves: ps <= 510
+        if ((q + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
     if (ne != (1u << NP) - 1) {                           // filter_edges: no spatial search
 #pragma unroll
@@ -636,7 +718,12 @@ __global__ void __launch_bounds__(kYtThreads, DTS_YT_WPE) k_yadif_t(const YadifP
                 // the spatial search first, then the other frames' rows (loaded past a scheduling
                 // barrier, a dword at a time: the two phases' operands are not live at once)
                 uint32_t pr[NP / 2], res[NQ];
-                if (!(DTS_YT_ABLATE & 1)) yspatial<NP>(cm, cp, ne, pr);
+                if (!(DTS_YT_ABLATE & 1)) {
+                    if (DTS_YT_PK)
+                        yspatial_pk<NP>(cm, cp, ne, pr);
+                    else
+                        yspatial<NP>(cm, cp, ne, pr);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 const int rm2 = 2 * rm - y, rp2 = 2 * rp - y;   // 2 mrefs / 2 prefs
                 const uint8_t *rows[10] = {row(prv, rm), row(prv, rp), row(nxt, rm), row(nxt, rp), row(pv2, y),
