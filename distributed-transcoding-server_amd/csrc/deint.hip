@@ -337,14 +337,21 @@ constexpr int kYtChunks = kYtPitch / 16;        // 16-byte chunks per LDS row (3
 constexpr int kYtSlot = kYtRows * kYtPitch;     // one frame tile (19,584 B)
 constexpr int kYtPieces = (kYtRows * kYtChunks + 63) / 64;   // 1-KB LDS-DMA pieces per frame tile
 #ifndef DTS_YT_NP
-#define DTS_YT_NP 16
+#define DTS_YT_NP 8
+#endif
+#ifndef DTS_YT_R2
+#define DTS_YT_R2 (DTS_YT_NP == 8)
 #endif
 constexpr int kYtNP = DTS_YT_NP;                // pixels of an interpolated row per thread (8 or 16)
 constexpr int kYtCB = kYtNP == 16 ? 16 : 8;     // cur-row bytes staged in registers left / right of them
-constexpr int kYtThreads = (kYtW / kYtNP) * (kYtH / 2);
+// 1: a thread takes two interpolated rows y, y + 2 (and the kept rows beside them), which share
+// the cur row y + 1, the prev / next rows y + 1 and the prev2 / next2 rows y, y + 2 (ytemporal2)
+constexpr int kYtR2 = DTS_YT_R2;
+constexpr int kYtThreads = (kYtW / kYtNP) * (kYtH / (2 << kYtR2));
 static_assert(kYtNP == 8 || kYtNP == 16, "8 or 16 pixels per thread");
+static_assert(!kYtR2 || kYtNP == 8, "two rows per thread: 8 pixels each");
 #ifndef DTS_YT_WPE
-#define DTS_YT_WPE (kYtNP == 8 ? 8 : 1)         // waves per SIMD the register budget is sized for
+#define DTS_YT_WPE (kYtNP == 8 && !DTS_YT_R2 ? 8 : 1)   // waves per SIMD the register budget is sized for
 #endif
 #ifndef DTS_YADIF_WALK
 #define DTS_YADIF_WALK 16
@@ -548,6 +555,82 @@ __device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP
     }
 }
 
+// yspatial_pk for two interpolated rows y, y + 2 (cur rows c0 = y - 1, c1 = y + 1, c2 = y + 3):
+// row y + 1's windows and byte pairs serve both (its cp and the other's cm)
+template <int NP>
+__device__ __forceinline__ void yspatial_pk3(const uint32_t (&c0)[(2 * kYtCB + NP) / 4], const uint32_t (&c1)[(2 * kYtCB + NP) / 4],
+                                             const uint32_t (&c2)[(2 * kYtCB + NP) / 4], uint32_t ne, uint32_t (&pa)[NP / 2],
+                                             uint32_t (&pb)[NP / 2])
+{
+    constexpr int CB = kYtCB;
+    uint32_t w0[NP + 4], w1[NP + 4], w2[NP + 4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w0[i] = win3(c0, CB - 3 + i);
+        w1[i] = win3(c1, CB - 3 + i);
+        w2[i] = win3(c2, CB - 3 + i);
+        asm volatile("" : "+v"(w0[i]), "+v"(w1[i]), "+v"(w2[i]));
+    }
+    auto u2 = [](const uint32_t *a, int i) {
+        const uint32_t b = (uint32_t)(i & 3);
+        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
+    };
+    auto lt = [](i16x2y a, i16x2y b) {
+        uint32_t m = __builtin_bit_cast(uint32_t, (i16x2y)((a - b) >> 15));
+        asm volatile("" : "+v"(m));
+        return m;
+    };
+    auto sel = [](uint32_t m, i16x2y a, i16x2y b) {
+        return __builtin_bit_cast(i16x2y, (__builtin_bit_cast(uint32_t, a) & m) | (__builtin_bit_cast(uint32_t, b) & ~m));
+    };
+#pragma unroll
+    for (int q = 0; q < NP / 2; ++q) {
+        const int k = 2 * q, X = CB + k;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            w0[k + 4 + i] = win3(c0, X + 1 + i);
+            w1[k + 4 + i] = win3(c1, X + 1 + i);
+            w2[k + 4 + i] = win3(c2, X + 1 + i);
+            asm volatile("" : "+v"(w0[k + 4 + i]), "+v"(w1[k + 4 + i]), "+v"(w2[k + 4 + i]));
+        }
+        // one row's pair of pixels: cm windows / bytes wm, cm; cp windows / bytes wp, cp
+        auto one = [&](const uint32_t *wm, const uint32_t *wp, const uint32_t *cm, const uint32_t *cp) {
+            auto sc = [&](int jm, int jp) {
+                const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], 0u);
+                return __builtin_bit_cast(i16x2y, __builtin_amdgcn_sad_hi_u8(wm[k + 1 + jm], wp[k + 1 + jp], lo));
+            };
+            i16x2y score = sc(2, 2) - (i16x2y){1, 1};
+            const i16x2y sm1 = sc(1, 3), sm2 = sc(0, 4), s1 = sc(3, 1), s2 = sc(4, 0);
+            i16x2y ps = u2(cm, X) + u2(cp, X);
+            uint32_t m = lt(sm1, score);
+            score = sel(m, sm1, score);
+            ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
+            uint32_t mm = lt(sm2, score) & m;
+            score = sel(mm, sm2, score);
+            ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
+            m = lt(s1, score);
+            score = sel(m, s1, score);
+            ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
+            mm = lt(s2, score) & m;
+            ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
+            return __builtin_bit_cast(uint32_t, ps) >> 1 & 0x7fff7fffu;
+        };
+        pa[q] = one(w0, w1, c0, c1);
+        pb[q] = one(w1, w2, c1, c2);
+        if ((q + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ne != (1u << NP) - 1) {                           // filter_edges: no spatial search
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            if (!((ne >> k) & 1u)) {
+                const uint32_t va = (uint32_t)(byte_at(c0, CB + k) + byte_at(c1, CB + k)) >> 1;
+                const uint32_t vb = (uint32_t)(byte_at(c1, CB + k) + byte_at(c2, CB + k)) >> 1;
+                pa[k >> 1] = (k & 1) ? (pa[k >> 1] & 0xffffu) | (va << 16) : (pa[k >> 1] & 0xffff0000u) | va;
+                pb[k >> 1] = (k & 1) ? (pb[k >> 1] & 0xffffu) | (vb << 16) : (pb[k >> 1] & 0xffff0000u) | vb;
+            }
+    }
+}
+
 // the temporal bounds d -+ diff of NP pixels (two per dword as packed 16-bit lanes: v_pk_*
 // arithmetic, no value leaves [-510, 510]) and the reference's two-sided clamp of the
 // spatial predictions pr[] (diff >= 0: a median), packed back to bytes.  ld(r, q) reads dword
@@ -584,6 +667,57 @@ __device__ __forceinline__ void ytemporal(const uint32_t (&cm)[(2 * kYtCB + NP) 
             r[h] = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pr[2 * q + h]), d - diff), d + diff);
         }
         out[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, r[1]), __builtin_bit_cast(uint32_t, r[0]), 0x06040200u);
+    }
+}
+
+// ytemporal for two interpolated rows a = y and b = y + 2 (both interior: rows y - 2 .. y + 4 in
+// the tile, the same FAR), sharing what row y + 1 and the frames' rows y, y + 2 give both: b's c
+// is a's e, b's prev / next mrefs rows are a's prefs rows (so |pp - e| and |np - e| are computed
+// once), b's d is a's f and a's d is b's b.  ld(r, q): 0 .. 9 as ytemporal's rows for a, then
+// 10 / 11 prev / next row y + 3, 12 / 13 prev2 / next2 row y + 4
+template <int NP, bool FAR, class LD>
+__device__ __forceinline__ void ytemporal2(const uint32_t (&c0)[(2 * kYtCB + NP) / 4], const uint32_t (&c1)[(2 * kYtCB + NP) / 4],
+                                           const uint32_t (&c2)[(2 * kYtCB + NP) / 4], LD ld, const uint32_t (&pra)[NP / 2],
+                                           const uint32_t (&prb)[NP / 2], uint32_t (&oa)[NP / 4], uint32_t (&ob)[NP / 4])
+{
+    constexpr int CQ = kYtCB / 4;
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) {
+        const uint32_t pm = ld(0, q), pp = ld(1, q), nm = ld(2, q), np = ld(3, q), p2 = ld(4, q), n2 = ld(5, q);
+        const uint32_t p2b = ld(7, q), n2b = ld(9, q), ppb = ld(10, q), npb = ld(11, q);
+        const uint32_t p2m = FAR ? ld(6, q) : 0u, n2m = FAR ? ld(8, q) : 0u, p2pb = FAR ? ld(12, q) : 0u,
+                       n2pb = FAR ? ld(13, q) : 0u;
+        i16x2y ra[2], rb[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const i16x2y ca = pair16(c0[CQ + q], h), e = pair16(c1[CQ + q], h), eb = pair16(c2[CQ + q], h);
+            const i16x2y A = pair16(p2, h), B = pair16(n2, h), Ab = pair16(p2b, h), Bb = pair16(n2b, h);
+            const i16x2y da = (A + B) >> 1, db = (Ab + Bb) >> 1;
+            const i16x2y X = absd16(pair16(pp, h), e), Y = absd16(pair16(np, h), e);
+            const i16x2y t1a = (absd16(pair16(pm, h), ca) + X) >> 1, t1b = (X + absd16(pair16(ppb, h), eb)) >> 1;
+            const i16x2y t2a = (absd16(pair16(nm, h), ca) + Y) >> 1, t2b = (Y + absd16(pair16(npb, h), eb)) >> 1;
+            i16x2y da_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(A, B) >> 1, t1a), t2a);
+            i16x2y db_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(Ab, Bb) >> 1, t1b), t2b);
+            if (FAR) {
+                const i16x2y ba = (pair16(p2m, h) + pair16(n2m, h)) >> 1, fb = (pair16(p2pb, h) + pair16(n2pb, h)) >> 1;
+                {   // row a: b = ba, f = db, c = ca, e = e
+                    const i16x2y de = da - e, dc = da - ca, bc = ba - ca, fe = db - e;
+                    const i16x2y mx = __builtin_elementwise_max(__builtin_elementwise_max(de, dc), __builtin_elementwise_min(bc, fe));
+                    const i16x2y mn = __builtin_elementwise_min(__builtin_elementwise_min(de, dc), __builtin_elementwise_max(bc, fe));
+                    da_ = __builtin_elementwise_max(__builtin_elementwise_max(da_, mn), -mx);
+                }
+                {   // row b: b = da, f = fb, c = e, e = eb
+                    const i16x2y de = db - eb, dc = db - e, bc = da - e, fe = fb - eb;
+                    const i16x2y mx = __builtin_elementwise_max(__builtin_elementwise_max(de, dc), __builtin_elementwise_min(bc, fe));
+                    const i16x2y mn = __builtin_elementwise_min(__builtin_elementwise_min(de, dc), __builtin_elementwise_max(bc, fe));
+                    db_ = __builtin_elementwise_max(__builtin_elementwise_max(db_, mn), -mx);
+                }
+            }
+            ra[h] = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, pra[2 * q + h]), da - da_), da + da_);
+            rb[h] = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2y, prb[2 * q + h]), db - db_), db + db_);
+        }
+        oa[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, ra[1]), __builtin_bit_cast(uint32_t, ra[0]), 0x06040200u);
+        ob[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, rb[1]), __builtin_bit_cast(uint32_t, rb[0]), 0x06040200u);
     }
 }
 
@@ -671,6 +805,7 @@ __global__ void __launch_bounds__(kYtThreads, DTS_YT_WPE) k_yadif_t(const YadifP
     // NP columns of one interpolated and one kept row (8 pixels: one row pair per wave, its row
     // arithmetic scalar)
     const int ci = t % (kYtW / NP), ri = kYtW / NP == 64 ? __builtin_amdgcn_readfirstlane(t / 64) : t / (kYtW / NP);
+    constexpr int RR = 1 << kYtR2;             // interpolated rows per thread
     const int x = x0 + NP * ci;
     const uint64_t obase0 = P.dst.data[p] + (uint64_t)x;
     for (int j = j0; j < j1; ++j) {
@@ -690,16 +825,57 @@ __global__ void __launch_bounds__(kYtThreads, DTS_YT_WPE) k_yadif_t(const YadifP
             const uint64_t obase = obase0 + (uint64_t)o * (uint64_t)P.dst.fstride;
             const int64_t dp = P.dst.pitch[p];
             const int off = ((y0 ^ td_parity) & 1) ? 0 : 1;     // y0 + off: the tile's first interpolated row
-            // kept row: a copy of cur
-            {
-                const int y = y0 + 2 * ri + (1 - off);
+            // kept rows: copies of cur
+#pragma unroll
+            for (int rr = 0; rr < RR; ++rr) {
+                const int y = y0 + 2 * RR * ri + 2 * rr + (1 - off);
                 if (y < h && x < w) {
                     uint32_t v[NQ];
                     ldsn<NP>(sl_c + (y - y0 + 2) * kYtPitch + NP * ci + 16, v);
                     putn<NP>(obase + (uint64_t)((int64_t)y * dp), v, w - x);
                 }
             }
-            const int y = y0 + 2 * ri + off;
+            const int ya = y0 + 2 * RR * ri + off;
+            auto rowp = [&](const uint8_t *sl, int yy) { return sl + (yy - y0 + 2) * kYtPitch + NP * ci + 16; };
+            // two interior rows (rows ya - 2 .. ya + 4 in the plane: no clamped mrefs / prefs, and
+            // both FAR unless the mode skips the spatial interlacing check)
+            const bool pair2 = kYtR2 && ya >= 2 && ya + 4 < h;
+            if (kYtR2 && pair2) {
+                if (x < w) {
+                    const bool far = !(P.mode & 2);
+                    const uint8_t *prv = sl_p, *cur = sl_c, *nxt = sl_n;
+                    const uint8_t *pv2 = parity ? prv : cur, *nx2 = parity ? cur : nxt;
+                    uint32_t c0[CW], c1[CW], c2[CW];
+#pragma unroll
+                    for (int h3 = 0; h3 < 3; ++h3) {
+                        ldsn<NP>(rowp(cur, ya - 1) - kYtCB + NP * h3, c0 + NQ * h3);
+                        ldsn<NP>(rowp(cur, ya + 1) - kYtCB + NP * h3, c1 + NQ * h3);
+                        ldsn<NP>(rowp(cur, ya + 3) - kYtCB + NP * h3, c2 + NQ * h3);
+                    }
+                    uint32_t ne = 0;
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) ne |= (x + k >= 3 && x + k < w - 3) ? 1u << k : 0u;
+                    uint32_t pa[NP / 2], pb[NP / 2], ra[NQ], rb[NQ];
+                    yspatial_pk3<NP>(c0, c1, c2, ne, pa, pb);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint8_t *rows[14] = {rowp(prv, ya - 1), rowp(prv, ya + 1), rowp(nxt, ya - 1), rowp(nxt, ya + 1),
+                                               rowp(pv2, ya), rowp(nx2, ya), rowp(pv2, ya - 2), rowp(pv2, ya + 2),
+                                               rowp(nx2, ya - 2), rowp(nx2, ya + 2), rowp(prv, ya + 3), rowp(nxt, ya + 3),
+                                               rowp(pv2, ya + 4), rowp(nx2, ya + 4)};
+                    auto ld = [&](int r, int q) { return *reinterpret_cast<const uint32_t *>(rows[r] + 4 * q); };
+                    if (far)
+                        ytemporal2<NP, true>(c0, c1, c2, ld, pa, pb, ra, rb);
+                    else
+                        ytemporal2<NP, false>(c0, c1, c2, ld, pa, pb, ra, rb);
+                    putn<NP>(obase + (uint64_t)((int64_t)ya * dp), ra, w - x);
+                    putn<NP>(obase + (uint64_t)((int64_t)(ya + 2) * dp), rb, w - x);
+                }
+                nst += 2 * RR;
+                continue;
+            }
+#pragma unroll 1
+            for (int rr = 0; rr < RR; ++rr) {
+            const int y = ya + 2 * rr;
             if (y < h && x < w) {
                 const int rm = y ? y - 1 : y + 1, rp = y + 1 < h ? y + 1 : y - 1;
                 const bool far = !((P.mode & 2) || y == 1 || y + 2 == h);
@@ -739,7 +915,8 @@ __global__ void __launch_bounds__(kYtThreads, DTS_YT_WPE) k_yadif_t(const YadifP
                 }
                 putn<NP>(obase + (uint64_t)((int64_t)y * dp), res, w - x);
             }
-            nst += 2;
+            }
+            nst += 2 * RR;
         }
         if (!whole) nst = 0;                   // (edge tiles: wait for their stores too)
     }
