@@ -327,7 +327,10 @@ __global__ void __launch_bounds__(256) k_yadif(const YadifParams P)
 // after it a dword at a time (round 5: 90 registers instead of 93).  Round-5 A/B:
 // 8 pixels per thread in 1024-thread workgroups fits 64 registers, two workgroups per CU and
 // 8 waves per SIMD, yet runs 69.0 k fps against 78.4 k here -- the window sharing of the
-// spatial search is worth more than the occupancy.  Sources and outputs 16-byte aligned, w >= 16.
+// spatial search is worth more than the occupancy.  Round 6: the spatial search two pixels per
+// dword (yspatial_pk) and, by default, two interpolated rows of 8 pixels per thread sharing their
+// common rows (DTS_YT_R2: yspatial_pk3 + ytemporal2).  Sources and outputs 16-byte
+// aligned, w >= 16.
 // ---------------------------------------------------------------------------
 constexpr int kYtW = 512;                       // output columns per tile (32 lanes x 16)
 constexpr int kYtH = 32;                        // output rows per tile (16 interpolated + 16 kept)
