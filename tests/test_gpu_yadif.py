@@ -141,14 +141,17 @@ def _aligned_seq(frames, w, h, n_extra_out=0):
 
 
 @pytest.mark.parametrize("w,h,n,first,count", [(720, 480, 5, 0, 5), (130, 74, 4, 0, 4), (1000, 36, 3, 0, 3),
-                                               (1920, 1080, 20, 1, 18), (3840, 2160, 3, 0, 3), (16, 6, 3, 0, 3)])
+                                               (1920, 1080, 20, 1, 18), (3840, 2160, 3, 0, 3), (16, 6, 3, 0, 3),
+                                               (264, 45, 3, 0, 3)])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("tff", [1, 0])
 def test_yadif_temporal_walk_vs_oracle(ctx, w, h, n, first, count, mode, tff):
     """k_yadif_t (16-byte aligned sequences: every frame tile staged once, a ring of prev /
     cur / next in LDS): bit-exact vs the oracle in every mode and field order; tiles at every
     plane edge, widths not multiples of 16, walks longer than one workgroup's (16 frames) and
-    starting inside the sequence (first > 0: the graph path's context frame)."""
+    starting inside the sequence (first > 0: the graph path's context frame); odd heights put the
+    two-row threads' boundary (rows y - 2 .. y + 4 inside the plane, else the one-row code) at
+    every offset from the bottom edge."""
     import torch
     from bench import dev_batch, frame_bytes, unpack_dev_frame
     if w >= 1920 and (mode, tff) not in [(0, 1), (1, 0), (2, 0)]:
