@@ -409,6 +409,7 @@ __device__ __forceinline__ uint32_t win3(const uint32_t *a, int i)
 //   windows read the staged halo (clamped columns) and are replaced afterwards;
 // - the clamp, packed again.
 typedef short i16x2y __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2y __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ i16x2y pair16(uint32_t d, int h)   // bytes 2h, 2h + 1 of d, zero-extended
 {
     return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(0u, d, h ? 0x0c030c02u : 0x0c010c00u));
@@ -487,8 +488,8 @@ __device__ __forceinline__ void yspatial(const uint32_t (&cm)[(2 * kYtCB + NP) /
 // (bytes i, i + 1 of a row as two 16-bit lanes: one unpacking serves the five j of neighbouring
 // pairs); each CHECK(j) of filter_line_c is a packed subtract whose sign (>> 15) is the lane mask
 // of `score < spatial_score`, nested checks AND their masks, and the updates are bit selects.
-// Scores stay in [-1, 765], their differences in 16 bits.  The result is the same bytes as
-// yspatial's, which it replaces.
+// Scores stay in [0, 766] (held as score + 1), their differences in 16 bits.  The result is the
+// same bytes as yspatial's, which it replaces.
 template <int NP>
 __device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP) / 4], const uint32_t (&cp)[(2 * kYtCB + NP) / 4],
                                             uint32_t ne, uint32_t (&pr)[NP / 2])
@@ -527,25 +528,29 @@ __device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP
         }
         // pixel k + h: windows k + h .. k + h + 4 are X + h - 3 .. X + h + 1; CHECK(j) compares the cm
         // window at X + j - 1 with the cp window at X - j - 1
-        auto sc = [&](int jm, int jp) {               // (pixel k, pixel k + 1) scores of one check
-            const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], 0u);
+        // (pixel k, pixel k + 1) scores of one check, + acc per half: scores are held as score + 1,
+        // so spatial_score's initial - 1 disappears and each candidate's + 1 rides in the
+        // accumulator operand (0x00010001: no carry between the halves)
+        auto sc = [&](int jm, int jp, uint32_t acc) {
+            const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], acc);
             return __builtin_bit_cast(i16x2y, __builtin_amdgcn_sad_hi_u8(wm[k + 1 + jm], wp[k + 1 + jp], lo));
         };
-        i16x2y score = sc(2, 2) - (i16x2y){1, 1};
-        const i16x2y sm1 = sc(1, 3), sm2 = sc(0, 4), s1 = sc(3, 1), s2 = sc(4, 0);
+        i16x2y score = sc(2, 2, 0u);
+        const i16x2y sm1 = sc(1, 3, 0x00010001u), sm2 = sc(0, 4, 0x00010001u), s1 = sc(3, 1, 0x00010001u),
+                     s2 = sc(4, 0, 0x00010001u);
         i16x2y ps = u2(cm, X) + u2(cp, X);
         uint32_t m = lt(sm1, score);                                       // CHECK(-1)
-        score = sel(m, sm1, score);
+        score = __builtin_elementwise_min(sm1, score);                     // = sel(m, sm1, score)
         ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
         uint32_t mm = lt(sm2, score) & m;                                  // CHECK(-2) inside it
         score = sel(mm, sm2, score);
         ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
         m = lt(s1, score);                                                 // CHECK(1)
-        score = sel(m, s1, score);
+        score = __builtin_elementwise_min(s1, score);
         ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
         mm = lt(s2, score) & m;                                            // CHECK(2) inside it
         ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
-        pr[q] = __builtin_bit_cast(uint32_t, ps) >> 1 & 0x7fff7fffu;       // both halves: ps <= 510
+        pr[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2y, ps) >> 1);   // v_pk_lshrrev_b16
         if ((q + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
     if (ne != (1u << NP) - 1) {                           // filter_edges: no spatial search
@@ -598,25 +603,28 @@ __device__ __forceinline__ void yspatial_pk3(const uint32_t (&c0)[(2 * kYtCB + N
         }
         // one row's pair of pixels: cm windows / bytes wm, cm; cp windows / bytes wp, cp
         auto one = [&](const uint32_t *wm, const uint32_t *wp, const uint32_t *cm, const uint32_t *cp) {
-            auto sc = [&](int jm, int jp) {
-                const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], 0u);
+            // scores held as score + 1: spatial_score's initial - 1 disappears and the candidates'
+            // + 1 rides in the sums' accumulator operand (0x00010001: no carry between the halves)
+            auto sc = [&](int jm, int jp, uint32_t acc) {
+                const uint32_t lo = __builtin_amdgcn_sad_u8(wm[k + jm], wp[k + jp], acc);
                 return __builtin_bit_cast(i16x2y, __builtin_amdgcn_sad_hi_u8(wm[k + 1 + jm], wp[k + 1 + jp], lo));
             };
-            i16x2y score = sc(2, 2) - (i16x2y){1, 1};
-            const i16x2y sm1 = sc(1, 3), sm2 = sc(0, 4), s1 = sc(3, 1), s2 = sc(4, 0);
+            i16x2y score = sc(2, 2, 0u);
+            const i16x2y sm1 = sc(1, 3, 0x00010001u), sm2 = sc(0, 4, 0x00010001u), s1 = sc(3, 1, 0x00010001u),
+                         s2 = sc(4, 0, 0x00010001u);
             i16x2y ps = u2(cm, X) + u2(cp, X);
             uint32_t m = lt(sm1, score);
-            score = sel(m, sm1, score);
+            score = __builtin_elementwise_min(sm1, score);                     // = sel(m, sm1, score)
             ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
             uint32_t mm = lt(sm2, score) & m;
             score = sel(mm, sm2, score);
             ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
             m = lt(s1, score);
-            score = sel(m, s1, score);
+            score = __builtin_elementwise_min(s1, score);
             ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
             mm = lt(s2, score) & m;
             ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
-            return __builtin_bit_cast(uint32_t, ps) >> 1 & 0x7fff7fffu;
+            return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2y, ps) >> 1);   // v_pk_lshrrev_b16
         };
         pa[q] = one(w0, w1, c0, c1);
         pb[q] = one(w1, w2, c1, c2);
