@@ -418,6 +418,19 @@ __device__ __forceinline__ i16x2y absd16(i16x2y a, i16x2y b)
 {
     return __builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b);
 }
+// byte b of lo and byte b of hi in bytes 0, 1 (bytes 2, 3 zero)
+__device__ __forceinline__ uint32_t two8(uint32_t hi, uint32_t lo, int b)
+{
+    return __builtin_amdgcn_perm(hi, lo, (uint32_t)b | ((uint32_t)(4 + b) << 8) | 0x0c0c0000u);
+}
+// |x0 - y0| + |x1 - y1| for the pixels 2h, 2h + 1 of four rows' dwords, as a 16-bit pair:
+// v_sad_u8 of (x0, x1) against (y0, y1) per pixel, the second pixel's by v_sad_hi_u8 into the
+// high half (td1 / td2 of filter_line_c before their halving)
+__device__ __forceinline__ i16x2y sad2x(uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1, int h)
+{
+    const uint32_t lo = __builtin_amdgcn_sad_u8(two8(x1, x0, 2 * h), two8(y1, y0, 2 * h), 0u);
+    return __builtin_bit_cast(i16x2y, __builtin_amdgcn_sad_hi_u8(two8(x1, x0, 2 * h + 1), two8(y1, y0, 2 * h + 1), lo));
+}
 
 // the spatial search of NP pixels: pr[] = 2 x 16-bit predictions per dword
 template <int NP>
@@ -664,8 +677,8 @@ __device__ __forceinline__ void ytemporal(const uint32_t (&cm)[(2 * kYtCB + NP) 
             const i16x2y a2 = pair16(p2, h), b2 = pair16(n2, h);
             const i16x2y d = (a2 + b2) >> 1;
             const i16x2y td0 = absd16(a2, b2);
-            const i16x2y td1 = (absd16(pair16(pm, h), c) + absd16(pair16(pp, h), e)) >> 1;
-            const i16x2y td2 = (absd16(pair16(nm, h), c) + absd16(pair16(np, h), e)) >> 1;
+            const i16x2y td1 = sad2x(pm, pp, cm[CQ + q], cp[CQ + q], h) >> 1;
+            const i16x2y td2 = sad2x(nm, np, cm[CQ + q], cp[CQ + q], h) >> 1;
             i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0 >> 1, td1), td2);
             if (FAR) {
                 const i16x2y b = (pair16(p2m, h) + pair16(n2m, h)) >> 1;
@@ -704,9 +717,10 @@ __device__ __forceinline__ void ytemporal2(const uint32_t (&c0)[(2 * kYtCB + NP)
             const i16x2y ca = pair16(c0[CQ + q], h), e = pair16(c1[CQ + q], h), eb = pair16(c2[CQ + q], h);
             const i16x2y A = pair16(p2, h), B = pair16(n2, h), Ab = pair16(p2b, h), Bb = pair16(n2b, h);
             const i16x2y da = (A + B) >> 1, db = (Ab + Bb) >> 1;
-            const i16x2y X = absd16(pair16(pp, h), e), Y = absd16(pair16(np, h), e);
-            const i16x2y t1a = (absd16(pair16(pm, h), ca) + X) >> 1, t1b = (X + absd16(pair16(ppb, h), eb)) >> 1;
-            const i16x2y t2a = (absd16(pair16(nm, h), ca) + Y) >> 1, t2b = (Y + absd16(pair16(npb, h), eb)) >> 1;
+            // td1 / td2 of both rows as sums of absolute byte differences (the (c, e) byte pairs
+            // of a row shared by its two sums)
+            const i16x2y t1a = sad2x(pm, pp, c0[CQ + q], c1[CQ + q], h) >> 1, t1b = sad2x(pp, ppb, c1[CQ + q], c2[CQ + q], h) >> 1;
+            const i16x2y t2a = sad2x(nm, np, c0[CQ + q], c1[CQ + q], h) >> 1, t2b = sad2x(np, npb, c1[CQ + q], c2[CQ + q], h) >> 1;
             i16x2y da_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(A, B) >> 1, t1a), t2a);
             i16x2y db_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(Ab, Bb) >> 1, t1b), t2b);
             if (FAR) {
