@@ -551,18 +551,15 @@ __device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP
         i16x2y score = sc(2, 2, 0u);
         const i16x2y sm1 = sc(1, 3, 0x00010001u), sm2 = sc(0, 4, 0x00010001u), s1 = sc(3, 1, 0x00010001u),
                      s2 = sc(4, 0, 0x00010001u);
+        // CHECK(-1) { CHECK(-2) }: when sm1 < score, the pair's outcome is the better of -1 and -2
+        // (-2 only if strictly better), decided apart from score; the same for CHECK(1) { CHECK(2) }
+        const i16x2y psl = sel(lt(sm2, sm1), u2(cm, X - 2) + u2(cp, X + 2), u2(cm, X - 1) + u2(cp, X + 1));
+        const i16x2y psr = sel(lt(s2, s1), u2(cm, X + 2) + u2(cp, X - 2), u2(cm, X + 1) + u2(cp, X - 1));
         i16x2y ps = u2(cm, X) + u2(cp, X);
-        uint32_t m = lt(sm1, score);                                       // CHECK(-1)
-        score = __builtin_elementwise_min(sm1, score);                     // = sel(m, sm1, score)
-        ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
-        uint32_t mm = lt(sm2, score) & m;                                  // CHECK(-2) inside it
-        score = sel(mm, sm2, score);
-        ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
-        m = lt(s1, score);                                                 // CHECK(1)
-        score = __builtin_elementwise_min(s1, score);
-        ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
-        mm = lt(s2, score) & m;                                            // CHECK(2) inside it
-        ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
+        const uint32_t ml = lt(sm1, score);
+        score = sel(ml, __builtin_elementwise_min(sm1, sm2), score);
+        ps = sel(ml, psl, ps);
+        ps = sel(lt(s1, score), psr, ps);
         pr[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2y, ps) >> 1);   // v_pk_lshrrev_b16
         if ((q + 1) % DTS_YT_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
@@ -625,18 +622,14 @@ __device__ __forceinline__ void yspatial_pk3(const uint32_t (&c0)[(2 * kYtCB + N
             i16x2y score = sc(2, 2, 0u);
             const i16x2y sm1 = sc(1, 3, 0x00010001u), sm2 = sc(0, 4, 0x00010001u), s1 = sc(3, 1, 0x00010001u),
                          s2 = sc(4, 0, 0x00010001u);
+            // CHECK(-1) { CHECK(-2) } and CHECK(1) { CHECK(2) } as in yspatial_pk
+            const i16x2y psl = sel(lt(sm2, sm1), u2(cm, X - 2) + u2(cp, X + 2), u2(cm, X - 1) + u2(cp, X + 1));
+            const i16x2y psr = sel(lt(s2, s1), u2(cm, X + 2) + u2(cp, X - 2), u2(cm, X + 1) + u2(cp, X - 1));
             i16x2y ps = u2(cm, X) + u2(cp, X);
-            uint32_t m = lt(sm1, score);
-            score = __builtin_elementwise_min(sm1, score);                     // = sel(m, sm1, score)
-            ps = sel(m, u2(cm, X - 1) + u2(cp, X + 1), ps);
-            uint32_t mm = lt(sm2, score) & m;
-            score = sel(mm, sm2, score);
-            ps = sel(mm, u2(cm, X - 2) + u2(cp, X + 2), ps);
-            m = lt(s1, score);
-            score = __builtin_elementwise_min(s1, score);
-            ps = sel(m, u2(cm, X + 1) + u2(cp, X - 1), ps);
-            mm = lt(s2, score) & m;
-            ps = sel(mm, u2(cm, X + 2) + u2(cp, X - 2), ps);
+            const uint32_t ml = lt(sm1, score);
+            score = sel(ml, __builtin_elementwise_min(sm1, sm2), score);
+            ps = sel(ml, psl, ps);
+            ps = sel(lt(s1, score), psr, ps);
             return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2y, ps) >> 1);   // v_pk_lshrrev_b16
         };
         pa[q] = one(w0, w1, c0, c1);
