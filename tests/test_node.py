@@ -336,12 +336,17 @@ def _write_y4m_p010(path, frames, w, h, fps=(60, 1)):
 
 
 @pytest.mark.gpu
-def test_worker_gpu_hdr10_fifo(tmp_path):
+@pytest.mark.parametrize("settings,full", [
+    (json.dumps({"tonemap": "hable", "format": "yuv420p"}), False),
+    ("-vf scale=128:72:flags=bicubic,zscale=t=linear:npl=100,format=gbrpf32le,zscale=p=bt709,"
+     "tonemap=tonemap=hable:desat=2,zscale=t=bt709:m=bt709:r=pc,format=yuv420p -c:v libx264", True)])
+def test_worker_gpu_hdr10_fifo(tmp_path, settings, full):
     """An HDR10 job through the Node worker on the GPU: a C420p10 (p010) source streamed
     through a FIFO, codecSettings {"tonemap": "hable"} -> the ladder's bit-exact p010 scale +
     k_tonemap, 8-bit segments written as Y4M; every sample within +-1 LSB of
     orc.hdr_to_sdr and at most 1 % off by one (database.js:73-79: the job row's fields drive
-    the graph)."""
+    the graph).  Second case: the ffmpeg graph a CPU worker would run, with the last zscale's
+    r=pc (full-range SDR output)."""
     import threading
     sw, sh, n, seg, w, h = 256, 144, 5, 3, 128, 72
     frames = [D.synth_host(sw, sh, D.FMT_P010LE, 0, 0x5EED, i) for i in range(n)]
@@ -356,7 +361,7 @@ def test_worker_gpu_hdr10_fifo(tmp_path):
     th = threading.Thread(target=feed, daemon=True)
     th.start()
     jobs = [{"id": 91, "sourceID": 3, "width": w, "height": h, "framerate": 60, "chunks": 2,
-             "codecSettings": json.dumps({"tonemap": "hable", "format": "yuv420p"})}]
+             "codecSettings": settings}]
     chunks = [{"id": 100 + o, "mainJob": 91, "chunkOffset": o, "status": None} for o in range(2)]
     cfg = {"workerId": 2, "segmentFrames": seg, "gpus": [0], "sources": {"3": {"path": str(fifo)}},
            "jobs": jobs, "chunks": chunks}
@@ -377,7 +382,7 @@ def test_worker_gpu_hdr10_fifo(tmp_path):
         assert (gw, gh, len(got)) == (w, h, len(idx))
         for i, g in zip(idx, got):
             mid = orc.scale_frame(frames[i], sw, sh, D.FMT_P010LE, w, h, D.FMT_P010LE, D.SCALE_BICUBIC)
-            want = orc.hdr_to_sdr(mid, w, h, D.FMT_YUV420P, D.TM_HABLE, float("nan"), 2.0, 0.0, 100.0)
+            want = orc.hdr_to_sdr(mid, w, h, D.FMT_YUV420P, D.TM_HABLE, float("nan"), 2.0, 0.0, 100.0, full)
             bad = tot = 0
             for a, b in zip(g, want):
                 d = np.abs(a.astype(np.int16) - np.asarray(b).astype(np.int16))
