@@ -518,7 +518,10 @@ __device__ __forceinline__ void yspatial_pk(const uint32_t (&cm)[(2 * kYtCB + NP
     // bytes i, i + 1 of a row, zero-extended into two 16-bit lanes
     auto u2 = [](const uint32_t *a, int i) {
         const uint32_t b = (uint32_t)(i & 3);
-        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
+        // (b <= 2: the bytes lie in one dword and the other operand is 0, as pair16 has it, so the
+        // temporal part's unpacking of the same cur-row pairs is the same instruction)
+        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(b <= 2 ? 0u : a[(i >> 2) + 1], a[i >> 2],
+                                                                b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
     };
     // the lane masks pass through an empty asm: seen as sign splats, the compiler turns the bit
     // selects back into a compare and a select per 16-bit lane
@@ -591,7 +594,10 @@ __device__ __forceinline__ void yspatial_pk3(const uint32_t (&c0)[(2 * kYtCB + N
     }
     auto u2 = [](const uint32_t *a, int i) {
         const uint32_t b = (uint32_t)(i & 3);
-        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(a[(i >> 2) + 1], a[i >> 2], b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
+        // (b <= 2: the bytes lie in one dword and the other operand is 0, as pair16 has it, so the
+        // temporal part's unpacking of the same cur-row pairs is the same instruction)
+        return __builtin_bit_cast(i16x2y, __builtin_amdgcn_perm(b <= 2 ? 0u : a[(i >> 2) + 1], a[i >> 2],
+                                                                b | (0x0cu << 8) | ((b + 1) << 16) | (0x0cu << 24)));
     };
     auto lt = [](i16x2y a, i16x2y b) {
         uint32_t m = __builtin_bit_cast(uint32_t, (i16x2y)((a - b) >> 15));
