@@ -675,10 +675,11 @@ __device__ __forceinline__ void ytemporal(const uint32_t (&cm)[(2 * kYtCB + NP) 
             const i16x2y c = pair16(cm[CQ + q], h), e = pair16(cp[CQ + q], h);
             const i16x2y a2 = pair16(p2, h), b2 = pair16(n2, h);
             const i16x2y d = (a2 + b2) >> 1;
+            // max(td0 >> 1, td1, td2) with td1, td2 the halved sums: all non-negative, so the three
+            // halvings are one, after the max
             const i16x2y td0 = absd16(a2, b2);
-            const i16x2y td1 = sad2x(pm, pp, cm[CQ + q], cp[CQ + q], h) >> 1;
-            const i16x2y td2 = sad2x(nm, np, cm[CQ + q], cp[CQ + q], h) >> 1;
-            i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0 >> 1, td1), td2);
+            const i16x2y s1 = sad2x(pm, pp, cm[CQ + q], cp[CQ + q], h), s2 = sad2x(nm, np, cm[CQ + q], cp[CQ + q], h);
+            i16x2y diff = __builtin_elementwise_max(__builtin_elementwise_max(td0, s1), s2) >> 1;
             if (FAR) {
                 const i16x2y b = (pair16(p2m, h) + pair16(n2m, h)) >> 1;
                 const i16x2y f = (pair16(p2p, h) + pair16(n2p, h)) >> 1;
@@ -718,10 +719,11 @@ __device__ __forceinline__ void ytemporal2(const uint32_t (&c0)[(2 * kYtCB + NP)
             const i16x2y da = (A + B) >> 1, db = (Ab + Bb) >> 1;
             // td1 / td2 of both rows as sums of absolute byte differences (the (c, e) byte pairs
             // of a row shared by its two sums)
-            const i16x2y t1a = sad2x(pm, pp, c0[CQ + q], c1[CQ + q], h) >> 1, t1b = sad2x(pp, ppb, c1[CQ + q], c2[CQ + q], h) >> 1;
-            const i16x2y t2a = sad2x(nm, np, c0[CQ + q], c1[CQ + q], h) >> 1, t2b = sad2x(np, npb, c1[CQ + q], c2[CQ + q], h) >> 1;
-            i16x2y da_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(A, B) >> 1, t1a), t2a);
-            i16x2y db_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(Ab, Bb) >> 1, t1b), t2b);
+            // (the halvings of td0, td1, td2 as one after their max: all non-negative)
+            const i16x2y t1a = sad2x(pm, pp, c0[CQ + q], c1[CQ + q], h), t1b = sad2x(pp, ppb, c1[CQ + q], c2[CQ + q], h);
+            const i16x2y t2a = sad2x(nm, np, c0[CQ + q], c1[CQ + q], h), t2b = sad2x(np, npb, c1[CQ + q], c2[CQ + q], h);
+            i16x2y da_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(A, B), t1a), t2a) >> 1;
+            i16x2y db_ = __builtin_elementwise_max(__builtin_elementwise_max(absd16(Ab, Bb), t1b), t2b) >> 1;
             if (FAR) {
                 const i16x2y ba = (pair16(p2m, h) + pair16(n2m, h)) >> 1, fb = (pair16(p2pb, h) + pair16(n2pb, h)) >> 1;
                 {   // row a: b = ba, f = db, c = ca, e = e
