@@ -1387,11 +1387,16 @@ static int quality_enqueue(dts_ctx *ctx, QScratch &qs, int w, int h, int fmt, co
     q.pw[1] = q.pw[2] = (w + 1) >> 1;
     q.ph[1] = q.ph[2] = (h + 1) >> 1;
     int total = 0;
-    q.walk = fmt == DTS_FMT_NV12 ? kQWalkNV12 : kQWalk;
+    const int walk = fmt == DTS_FMT_NV12 ? kQWalkNV12 : kQWalk;
     for (int p = 0; p < 3; ++p) {
         q.tbx[p] = fmt == DTS_FMT_NV12 && p > 0 ? kQTileBX / 2 : kQTileBX;
         q.tiles_x[p] = (q.pw[p] + 4 * q.tbx[p] - 1) / (4 * q.tbx[p]);
-        q.tiles_y[p] = (q.ph[p] + 4 * kQTileBY * q.walk - 1) / (4 * kQTileBY * q.walk);
+        // walks of about `walk` tiles, as many as the plane's tile rows round to, evened out: a
+        // last walk of a few rows would cost a workgroup's setup, apron row and reduction
+        const int trows = (q.ph[p] + 4 * kQTileBY - 1) / (4 * kQTileBY);
+        const int nw = DTS_Q_BAL ? std::max(1, (trows + walk / 2) / walk) : (trows + walk - 1) / walk;
+        q.walk[p] = DTS_Q_BAL ? (trows + nw - 1) / nw : walk;
+        q.tiles_y[p] = (trows + q.walk[p] - 1) / q.walk[p];
         q.tile_base[p] = total;
         total += q.tiles_x[p] * q.tiles_y[p];
     }

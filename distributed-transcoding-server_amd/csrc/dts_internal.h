@@ -381,6 +381,9 @@ constexpr int kQTileBY = 16;        // 4x4 blocks per tile, y
 #ifndef DTS_Q_WALK_NV12
 #define DTS_Q_WALK_NV12 DTS_Q_WALK
 #endif
+#ifndef DTS_Q_BAL
+#define DTS_Q_BAL 1        // 0: walks of exactly kQWalk tiles (the last one short)
+#endif
 constexpr int kQWalk = DTS_Q_WALK;  // tiles per k_quality workgroup, walked top to bottom
 constexpr int kQWalkNV12 = DTS_Q_WALK_NV12;   // the same for nv12 renditions
 
@@ -389,7 +392,7 @@ struct QualityParams {
     int32_t pw[3], ph[3];           // plane sizes
     int32_t tbx[3];                 // tile width in blocks (kQTileBX; nv12 chroma kQTileBX / 2)
     int32_t tiles_x[3], tiles_y[3]; // tiles_y: walks of `walk` tiles
-    int32_t walk;                   // tiles per walk (kQWalk / kQWalkNV12)
+    int32_t walk[3];                // tiles per walk, per plane (about kQWalk / kQWalkNV12: quality_enqueue)
     int32_t tile_base[4];           // prefix of tiles per plane
     int32_t interleaved;            // 1 = nv12 (plane 1 holds U,V interleaved)
     int32_t nframes;

@@ -697,8 +697,8 @@ __global__ void __launch_bounds__(kThreads) k_quality(const QualityParams P, int
     const bool vec16 = (((uintptr_t)A | (uintptr_t)B | (uint64_t)pa | (uint64_t)pb) & 15) == 0;
     constexpr int NB = INTER ? 2 : 4;               // blocks per item: 16 bytes of an image row
     const int iby = t >> 4, iq = t & 15;            // item: blocks NB iq .. NB iq + NB - 1 of block row iby
-    const int by00 = tw * P.walk * kQTileBY;        // first block row of the walk
-    const int nk = min(P.walk, (h - 4 * by00 + 4 * kQTileBY - 1) / (4 * kQTileBY));
+    const int by00 = tw * P.walk[plane] * kQTileBY; // first block row of the walk
+    const int nk = min(P.walk[plane], (h - 4 * by00 + 4 * kQTileBY - 1) / (4 * kQTileBY));
 
     unsigned long long sse[2] = {0, 0};
     double ssim[2] = {0.0, 0.0};
